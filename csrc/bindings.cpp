@@ -1,0 +1,130 @@
+// Python bindings of the native runtime (module distributed_amd._C).
+//
+// The extension deliberately does not link libtorch: tensors cross the boundary as raw
+// device pointers (tensor.data_ptr()) and streams as hipStream_t integers, so the module
+// only depends on the HIP runtime and RCCL that torch itself has already loaded.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "comm.h"
+#include "convnet.h"
+#include "damd_common.h"
+#include "kernels_api.h"
+#include "step_executor.h"
+
+namespace py = pybind11;
+using namespace damd;
+
+#define HIP_CHECK(x)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess)                                                               \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) +     \
+                               " at " #x);                                              \
+  } while (0)
+
+template <typename T>
+static T* P_(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+// Fused MNIST-CNN trainer: every per-step buffer is preallocated by Python (torch
+// tensors) and passed in as device pointers.
+class ConvNetTrainer : public StepExecutor {
+ public:
+  ConvNetTrainer(int device, py::dict bufs, int B, int PP, int grad_allreduce)
+      : StepExecutor(device), B_(B), PP_(PP), grad_allreduce_(grad_allreduce) {
+    if (B <= 0) throw std::invalid_argument("batch must be > 0");
+    if (PP < 1 || PP > 4) throw std::invalid_argument("positions per slice must be in [1,4]");
+    auto g = [&](const char* k) -> uintptr_t { return bufs[k].cast<uintptr_t>(); };
+    b_.X = nullptr; b_.labels = nullptr; b_.perm = nullptr;
+    b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
+    b_.ctrl = P_<Ctrl>(g("ctrl"));
+    b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
+    b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
+    b_.hpart = P_<float>(g("hpart")); b_.cpart = P_<float>(g("cpart"));
+    HIP_CHECK(convnet_set_lds_limits());
+  }
+  void set_data(uintptr_t X, uintptr_t labels, uintptr_t perm) {
+    b_.X = P_<const float>(X); b_.labels = P_<const int>(labels); b_.perm = P_<const int>(perm);
+    invalidate_graphs();
+  }
+  void flush() { HIP_CHECK(convnet_launch_flush(b_, stream_)); }
+  int num_slices() const { return convnet_num_slices(PP_); }
+  int batch() const { return B_; }
+
+ protected:
+  void enqueue_one_step() override {
+    if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
+    HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
+    if (grad_allreduce_ && comm_ && comm_->nranks() > 1)
+      comm_->allreduce(b_.G, b_.G, kConvNetNGrad, 0, 0, stream_);
+  }
+
+ private:
+  ConvNetBuffers b_;
+  int B_, PP_, grad_allreduce_;
+};
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "distributed_amd native runtime (HIP/gfx950 kernels, RCCL, hipGraph executor)";
+  m.attr("CONVNET_NPARAM") = kConvNetNParam;
+  m.attr("CONVNET_NGRAD") = kConvNetNGrad;
+
+  m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) n = 0; return n; });
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("rccl_version", []() { int v = 0; ncclGetVersion(&v); return v; });
+
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](int n, int r, py::bytes uid, int dev) {
+             return new RcclComm(n, r, std::string(uid), dev);
+           }),
+           py::arg("nranks"), py::arg("rank"), py::arg("uid"), py::arg("device"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def("allreduce",
+           [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int op, uintptr_t st) {
+             c.allreduce(P_<void>(s), P_<void>(r), n, dt, op, P_<ihipStream_t>(st));
+           })
+      .def("broadcast",
+           [](RcclComm& c, uintptr_t b, size_t n, int dt, int root, uintptr_t st) {
+             c.broadcast(P_<void>(b), n, dt, root, P_<ihipStream_t>(st));
+           })
+      .def("allgather",
+           [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, uintptr_t st) {
+             c.allgather(P_<const void>(s), P_<void>(r), n, dt, P_<ihipStream_t>(st));
+           })
+      .def("reduce_scatter",
+           [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int op, uintptr_t st) {
+             c.reduce_scatter(P_<const void>(s), P_<void>(r), n, dt, op, P_<ihipStream_t>(st));
+           })
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("aborted", &RcclComm::aborted);
+
+  m.def("stream_wait", [](uintptr_t st, double timeout_s) {
+    py::gil_scoped_release nogil;
+    return stream_wait_with_deadline(P_<ihipStream_t>(st), timeout_s, nullptr);
+  });
+
+  py::class_<ConvNetTrainer>(m, "ConvNetTrainer")
+      .def(py::init<int, py::dict, int, int, int>(), py::arg("device"), py::arg("buffers"),
+           py::arg("batch"), py::arg("positions_per_slice") = 4, py::arg("grad_allreduce") = 1)
+      .def("set_data", &ConvNetTrainer::set_data)
+      .def("set_comm", [](ConvNetTrainer& t, RcclComm* c) { t.set_comm(c); },
+           py::keep_alive<1, 2>())
+      .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
+      .def("capture", &ConvNetTrainer::capture)
+      .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
+      .def("flush", &ConvNetTrainer::flush)
+      .def("sync", &ConvNetTrainer::sync, py::arg("timeout_s") = 0.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("invalidate_graphs", &ConvNetTrainer::invalidate_graphs)
+      .def_property_readonly("num_graphs", &ConvNetTrainer::num_graphs)
+      .def_property_readonly("num_slices", &ConvNetTrainer::num_slices)
+      .def_property_readonly("batch", &ConvNetTrainer::batch)
+      .def_property_readonly("stream", [](ConvNetTrainer& t) { return reinterpret_cast<uintptr_t>(t.stream()); });
+
+  register_kernel_ops(m);
+}

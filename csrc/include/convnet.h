@@ -1,0 +1,21 @@
+// Host interface of the fused MNIST-CNN step kernels (csrc/kernels/convnet_fused.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace damd {
+struct Ctrl;
+struct ConvNetBuffers {
+  const float* X; const int* labels; const int* perm;
+  float* P; float* G; float* V; Ctrl* ctrl;
+  uint16_t* pooled; uint8_t* code; float* slabs; float* dh; float* hpart; float* cpart;
+};
+constexpr int kConvNetNParam = 347146;
+constexpr int kConvNetNGrad = 347152;
+int convnet_num_slices(int PP);
+size_t convnet_f1_lds(int PP);
+size_t convnet_f3_lds(int PP);
+hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
+hipError_t convnet_launch_flush(const ConvNetBuffers& b, hipStream_t st);
+hipError_t convnet_set_lds_limits();
+}  // namespace damd

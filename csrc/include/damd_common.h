@@ -1,0 +1,91 @@
+// Common device helpers for distributed_amd HIP kernels (gfx950 / CDNA4 only).
+//
+// - bf16 <-> f32 conversion by bit manipulation (round-to-nearest-even),
+// - MFMA fragment vector types for v_mfma_f32_16x16x32_bf16,
+// - the in-launch "last arriver" hand-off (agent-scope release/acquire, see
+//   cdna_hip_programming.md §6 Guideline 16 / §5 split-K counter recipe).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace damd {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  // NaN stays NaN (quiet), otherwise RNE.
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Load 8 consecutive bf16 (16 B, must be 16-B aligned) from LDS / global as an MFMA fragment.
+__device__ __forceinline__ bf16x8 ld_frag(const uint16_t* p) {
+  return *reinterpret_cast<const bf16x8*>(p);
+}
+
+// Control block shared by the fused trainer kernels and the host.  32 x 4 B.
+// Written by the host only between graph replays (stream-ordered memcpy).
+struct Ctrl {
+  float lr;                 // 0  learning rate
+  float momentum;           // 1  SGD momentum (0 = plain SGD)
+  int   nesterov;           // 2
+  int   nsamples;           // 3  dataset rows
+  int   row0;               // 4  rank * per-replica batch (offset inside global batch)
+  int   global_batch;       // 5
+  int   cursor;             // 6  step index inside the epoch (advanced on device)
+  int   iterations;         // 7  optimizer iterations (advanced on device)
+  int   cnt_a;              // 8  arrival counter, kernel F2
+  int   cnt_b;              // 9  arrival counter, kernel F3
+  float acc_loss;           // 10 epoch accumulators (sum of per-sample loss)
+  float acc_correct;        // 11
+  float acc_count;          // 12
+  int   wrap;               // 13 if > 0: cursor wraps modulo `wrap` (benchmark epochs)
+  int   pad[18];
+};
+static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
+
+// Keras tf.keras SGD update (optimizer_v2/gradient_descent.py semantics):
+//   momentum == 0 : w -= lr * g
+//   else          : v = m * v - lr * g ; w += v            (nesterov: w += m * v - lr * g)
+__device__ __forceinline__ void sgd_update(float w, float g, float v, float lr, float mom, int nest,
+                                           float& wn, float& vn) {
+  if (mom == 0.f) {
+    wn = w - lr * g;
+    vn = v;
+  } else {
+    vn = mom * v - lr * g;
+    wn = nest ? (w + mom * vn - lr * g) : (w + vn);
+  }
+}
+
+// Last-arriver election across the workgroups of one launch.  Every thread of the
+// block must call it (contains __syncthreads).  `flag` is one int in the block's LDS.
+// Returns true in every thread of the last block to arrive; that block may then read
+// every other block's plain-stored partials (agent-scope acquire done here).
+__device__ __forceinline__ bool last_arriver(int* counter, int nblocks, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int t = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == nblocks - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
+}  // namespace damd

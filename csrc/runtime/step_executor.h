@@ -1,0 +1,49 @@
+// Native step executor: owns a HIP stream, enqueues one training step (kernels +
+// optional RCCL gradient all-reduce), and captures k back-to-back steps into a
+// hipGraph that is replayed by the fit loop.  This replaces the reference's
+// tf.function tracing (reference README.md:309 — epoch 1 pays tracing) with HIP graph
+// capture: the host cost per k steps is one hipGraphLaunch.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <functional>
+#include <map>
+#include <memory>
+
+#include "comm.h"
+
+namespace damd {
+
+struct Ctrl;
+
+class StepExecutor {
+ public:
+  explicit StepExecutor(int device);
+  virtual ~StepExecutor();
+
+  hipStream_t stream() const { return stream_; }
+  void set_comm(RcclComm* comm) { comm_ = comm; invalidate_graphs(); }
+  RcclComm* comm() const { return comm_; }
+
+  // Enqueue k steps eagerly (one host launch per kernel).
+  void step(int k);
+  // Capture k steps into a graph (cached by k).
+  void capture(int k);
+  // Run k steps: greedily replay the largest captured graph <= remaining, eager tail.
+  void run(int k);
+  // Block until the stream drains; false on watchdog timeout (comm aborted).
+  bool sync(double timeout_s);
+  void invalidate_graphs();
+  int num_graphs() const { return (int)graphs_.size(); }
+
+ protected:
+  virtual void enqueue_one_step() = 0;
+  hipStream_t stream_ = nullptr;
+  RcclComm* comm_ = nullptr;
+  int device_;
+
+ private:
+  std::map<int, hipGraphExec_t> graphs_;
+};
+
+}  // namespace damd

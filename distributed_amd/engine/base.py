@@ -1,0 +1,55 @@
+"""Engine interface and selection."""
+from __future__ import annotations
+
+from ..utils import env
+from ..utils import logging as dlog
+
+
+class Engine:
+    """Executes training steps for one (model, strategy, batch) configuration."""
+
+    name = "base"
+
+    def __init__(self, model, strategy, per_replica_batch: int, global_batch: int):
+        self.model, self.strategy = model, strategy
+        self.per_replica, self.global_batch = per_replica_batch, global_batch
+        self.world, self.rank = strategy.num_replicas_in_sync, strategy.rank
+        self.device = strategy.device
+
+    def bind(self, x, y):  # -> DataFeed
+        raise NotImplementedError
+
+    def start_epoch(self, epoch: int, shuffle: bool):
+        raise NotImplementedError
+
+    def run(self, n_steps: int):
+        raise NotImplementedError
+
+    def metrics(self) -> dict:
+        """Global epoch-so-far averages, e.g. {'loss':..., 'accuracy':...} (syncs)."""
+        raise NotImplementedError
+
+    def end_epoch(self) -> dict:
+        return self.metrics()
+
+    def finish(self):
+        pass
+
+    def lr_changed(self):
+        pass
+
+    def sync(self):
+        pass
+
+
+def select_engine(model, strategy, per_replica: int, global_batch: int) -> Engine:
+    from .generic import GenericEngine
+
+    if env.get_bool("DAMD_FUSED", True):
+        from .fused_convnet import FusedConvNetEngine
+
+        ok, why = FusedConvNetEngine.eligible(model, strategy)
+        if ok:
+            return FusedConvNetEngine(model, strategy, per_replica, global_batch)
+        dlog.debug("fused ConvNet engine not used: %s", why)
+    return GenericEngine(model, strategy, per_replica, global_batch)

@@ -1,0 +1,238 @@
+"""Fused MI355X engine for the reference CNN family (reference README.md:58-73).
+
+Pattern: ``Conv2D(32, 3, relu, input (28,28,1)) -> MaxPooling2D(2) -> Flatten ->
+Dense(64, relu) -> Dense(10)`` + ``SparseCategoricalCrossentropy(from_logits=True)`` +
+``SGD`` (any lr / momentum / nesterov) + accuracy metric.
+
+Execution (csrc/kernels/convnet_fused.hip, csrc/runtime/step_executor.cpp): a step is
+three HIP launches plus one in-place RCCL SUM all-reduce of the flat gradient buffer
+(347,146 grads + [loss, correct, count] tail); the SGD update is deferred into the next
+step's consumer kernels; k steps are captured into one hipGraph and replayed.  Model
+variables are views of the fp32 master buffer, so ``get_weights``/checkpoints see the
+trained values after ``finish()`` (which applies the last pending update).
+"""
+from __future__ import annotations
+
+import struct
+
+import numpy as np
+import torch
+
+from ..utils import env
+from ..utils import logging as dlog
+from .base import Engine
+from .data import DataFeed
+
+NPARAM = 347146
+NGRAD = 347152
+HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
+REC = 716
+# ctrl word indices (csrc/include/damd_common.h struct Ctrl)
+C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP = range(14)
+SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
+
+
+def _f2i(f: float) -> int:
+    return struct.unpack("<i", struct.pack("<f", float(f)))[0]
+
+
+def _i2f(i: int) -> float:
+    return struct.unpack("<f", struct.pack("<i", int(i)))[0]
+
+
+class FusedConvNetEngine(Engine):
+    name = "fused_convnet"
+
+    @staticmethod
+    def eligible(model, strategy):
+        from ..keras import layers as L
+        from ..keras import losses, optimizers
+
+        if strategy.device.type != "cuda":
+            return False, "not on a GPU"
+        ls = [l for l in getattr(model, "layers", []) if not isinstance(l, L.InputLayer)]
+        if len(ls) != 5:
+            return False, "layer count"
+        c, p, f, d1, d2 = ls
+        if not (isinstance(c, L.Conv2D) and c.filters == 32 and c.kernel_size == (3, 3) and c.strides == (1, 1)
+                and c.padding == "valid" and c.dilation_rate == (1, 1) and c.use_bias
+                and c.activation.__name__ == "relu" and tuple(c.input_shape or ())[1:] == (28, 28, 1)):
+            return False, "conv layer"
+        if not (isinstance(p, L.MaxPooling2D) and p.pool_size == (2, 2) and p.strides == (2, 2)
+                and p.padding == "valid"):
+            return False, "pool layer"
+        if not isinstance(f, L.Flatten):
+            return False, "flatten"
+        if not (isinstance(d1, L.Dense) and d1.units == 64 and d1.use_bias and d1.activation.__name__ == "relu"):
+            return False, "dense"
+        if not (isinstance(d2, L.Dense) and d2.units == 10 and d2.use_bias and d2.activation.__name__ == "linear"):
+            return False, "dense_1"
+        if not (isinstance(model.loss, losses.SparseCategoricalCrossentropy) and model.loss.from_logits):
+            return False, "loss"
+        if type(model.optimizer) is not optimizers.SGD:
+            return False, "optimizer"
+        for m in model.compiled_metrics:
+            if m.name not in ("accuracy", "acc", "sparse_categorical_accuracy"):
+                return False, f"metric {m.name}"
+        return True, ""
+
+    def __init__(self, model, strategy, per_replica_batch, global_batch):
+        super().__init__(model, strategy, per_replica_batch, global_batch)
+        from ..native import require_C
+
+        C = require_C()
+        dev = self.device
+        B = per_replica_batch
+        self.PP = env.get_int("DAMD_PP", 4)
+        NS = (169 + self.PP - 1) // self.PP
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.P = torch.zeros(NGRAD, **f32)
+        self.G = torch.zeros(NGRAD, **f32)
+        self.V = torch.zeros(NGRAD, **f32)
+        self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
+        self.pooled = torch.zeros(B, FEAT, dtype=torch.bfloat16, device=dev)
+        self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
+        self.slabs = torch.zeros(NS, B, HID, **f32)
+        self.dh = torch.zeros(B, HID, **f32)
+        self.hpart = torch.zeros((B + 3) // 4, REC, **f32)
+        self.cpart = torch.zeros(NS, NCONV, **f32)
+        # model variables -> views of the fp32 master buffer (Keras weight order)
+        self.vars = model.trainable_weights
+        off = 0
+        for v, shp in zip(self.vars, SHAPES):
+            if tuple(v.shape) != shp:
+                raise RuntimeError(f"unexpected variable shape {v.shape} for {v.name}")
+            n = int(np.prod(shp))
+            v._rebind(self.P[off:off + n].view(shp))
+            off += n
+        opt = model.optimizer
+        if opt.momentum and "momentum" in opt.slots and opt.slots["momentum"].numel() == NPARAM:
+            self.V[:NPARAM].copy_(opt.slots["momentum"].to(dev))
+        if self.world > 1:
+            strategy.communicator.broadcast_(self.P, 0)  # mirrored variables start equal
+        c = self.ctrl.cpu()
+        c[C_IT] = int(opt.iterations)
+        self.ctrl.copy_(c.to(dev))
+        self._write_hparams()
+        torch.cuda.synchronize(dev)
+        bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
+                    ctrl=self.ctrl.data_ptr(), pooled=self.pooled.data_ptr(), code=self.code.data_ptr(),
+                    slabs=self.slabs.data_ptr(), dh=self.dh.data_ptr(), hpart=self.hpart.data_ptr(),
+                    cpart=self.cpart.data_ptr())
+        self.trainer = C.ConvNetTrainer(dev.index or 0, bufs, B, self.PP, 1)
+        native = strategy.communicator.native if self.world > 1 else None
+        if native is not None:
+            self.trainer.set_comm(native)
+        elif self.world > 1:
+            raise RuntimeError("fused engine needs the native RCCL communicator for world > 1 (DAMD_COMM=rccl)")
+        self.use_graph = env.get_bool("DAMD_GRAPH", True)
+        self.graph_steps = max(1, env.get_int("DAMD_GRAPH_STEPS", 20))
+        self.watchdog_s = env.get_float("DAMD_WATCHDOG_S", 0.0)
+        opt._iter_source = self._iterations
+        self.feed = None
+        self._pending = False
+        self.steps_done = 0
+        dlog.debug("fused ConvNet engine: B=%d, slices=%d, graph=%s", B, NS, self.use_graph)
+
+    # --- host <-> ctrl ---------------------------------------------------------------
+    def _ctrl_host(self):
+        self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        return self.ctrl.cpu().tolist()
+
+    def _ctrl_write(self, updates: dict):
+        self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        c = self.ctrl.cpu()
+        for k, v in updates.items():
+            c[k] = v
+        self.ctrl.copy_(c.to(self.device))
+        torch.cuda.synchronize(self.device)
+
+    def _write_hparams(self):
+        opt = self.model.optimizer
+        c = self.ctrl.cpu()
+        c[C_LR] = _f2i(opt.learning_rate)
+        c[C_MOM] = _f2i(opt.momentum)
+        c[C_NEST] = int(opt.nesterov)
+        c[C_ROW0] = self.rank * self.per_replica
+        c[C_GB] = self.global_batch
+        self.ctrl.copy_(c.to(self.device))
+
+    def _watchdog_fired(self):
+        raise RuntimeError(f"collective watchdog: step did not complete within {self.watchdog_s}s; "
+                           "RCCL communicator aborted")
+
+    def _iterations(self):
+        return self._ctrl_host()[C_IT]
+
+    def lr_changed(self):
+        self._flush()
+        c = {C_LR: _f2i(self.model.optimizer.learning_rate)}
+        self._ctrl_write(c)
+
+    # --- data / epochs ---------------------------------------------------------------
+    def bind(self, x, y):
+        x = np.asarray(x)
+        if tuple(x.shape[1:]) not in ((28, 28, 1), (28, 28), (784,)):
+            raise ValueError(f"fused ConvNet engine expects 28x28x1 inputs, got {x.shape[1:]}")
+        key = (id(x), id(y), len(x))
+        if self.feed is None or getattr(self, "_feed_key", None) != key:
+            self.trainer.sync(0.0)
+            self.feed = DataFeed(x, y, self.device, flatten=True)
+            self._feed_key = key
+            torch.cuda.synchronize(self.device)
+            self.trainer.set_data(self.feed.x.data_ptr(), self.feed.y.data_ptr(), self.feed.perm.data_ptr())
+            self._ctrl_write({C_NS: self.feed.n})
+        return self.feed
+
+    def start_epoch(self, epoch, shuffle, wrap_steps: int = 0):
+        """``wrap_steps > 0`` makes the device cursor wrap (benchmark runs longer than an
+        epoch without host round trips); fit() manages epochs on the host (wrap 0)."""
+        self._flush()
+        self.trainer.sync(0.0)
+        self.feed.set_epoch(epoch, shuffle)
+        opt = self.model.optimizer
+        self._ctrl_write({C_CUR: 0, C_AL: 0, C_AC: 0, C_AN: 0, C_WRAP: int(wrap_steps),
+                          C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
+
+    def run(self, n_steps):
+        if self.use_graph and n_steps >= self.graph_steps:
+            self.trainer.capture(self.graph_steps)
+        if self.use_graph:
+            self.trainer.run(n_steps)
+        else:
+            self.trainer.step(n_steps)
+        self._pending = True
+        self.steps_done += n_steps
+
+    def _flush(self):
+        if self._pending:
+            self.trainer.flush()
+            self._pending = False
+
+    def metrics(self):
+        c = self._ctrl_host()
+        tail = self.G[NPARAM:NPARAM + 3].cpu().tolist() if self._pending else [0.0, 0.0, 0.0]
+        loss = _i2f(c[C_AL]) + tail[0]
+        corr = _i2f(c[C_AC]) + tail[1]
+        cnt = _i2f(c[C_AN]) + tail[2]
+        d = max(cnt, 1.0)
+        out = {"loss": loss / d, "_count": cnt}
+        for m in self.model.compiled_metrics:
+            out[m.name] = corr / d
+        return out
+
+    def end_epoch(self):
+        self._flush()
+        return self.metrics()
+
+    def finish(self):
+        self._flush()
+        self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        opt = self.model.optimizer
+        if opt.momentum:
+            opt.ensure_slots(NPARAM, self.device)
+            opt.slots["momentum"].copy_(self.V[:NPARAM])
+        torch.cuda.synchronize(self.device)
+
+    def sync(self):
+        self.trainer.sync(self.watchdog_s) or self._watchdog_fired()

@@ -1,0 +1,113 @@
+"""Generic engine: any Keras model, per-layer ops, autograd backward, flat-bucket DP.
+
+Per step (per replica): gather the local rows of the global batch from the
+device-resident feed, forward, per-sample loss, ``sum / global_batch`` so that a SUM
+all-reduce gives the global-mean gradient, write all gradients into ONE
+flat fp32 buffer whose tail carries [loss_sum, count, metric sums...] (SURVEY.md D6:
+one collective per step for grads + metrics), all-reduce it, apply the optimizer on the
+flat master buffer, and accumulate the metric tail on device (no host sync per step).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .base import Engine
+from .data import DataFeed
+
+
+class GenericEngine(Engine):
+    name = "generic"
+
+    def __init__(self, model, strategy, per_replica_batch, global_batch):
+        super().__init__(model, strategy, per_replica_batch, global_batch)
+        self.vars = model.trainable_weights
+        self.sizes = [int(np.prod(v.shape)) for v in self.vars]
+        self.n = int(sum(self.sizes))
+        dev = self.device
+        self.P = torch.zeros(self.n, dtype=torch.float32, device=dev)
+        off = 0
+        self.leaves = []
+        for v, sz in zip(self.vars, self.sizes):
+            view = self.P[off:off + sz].view(v.shape)
+            with torch.no_grad():
+                view.copy_(v.value.detach().to(dev, torch.float32))
+            leaf = torch.empty(0, device=dev)
+            leaf.data = view
+            leaf.requires_grad_(True)
+            v._t = leaf
+            self.leaves.append(leaf)
+            off += sz
+        self.loss = model.loss
+        self.metric_objs = model.compiled_metrics
+        self.ntail = 2 + len(self.metric_objs)
+        self.G = torch.zeros(self.n + self.ntail, dtype=torch.float32, device=dev)
+        self.acc = torch.zeros(self.ntail, dtype=torch.float64, device=dev)
+        model.optimizer.ensure_slots(self.n, dev)
+        # mirrored variables: replicas start from worker 0's values
+        if self.world > 1:
+            comm = strategy.communicator
+            comm.broadcast_(self.P, 0)
+            for w in model.non_trainable_weights:
+                comm.broadcast_(w.value.data if w.value.requires_grad else w.value, 0)
+        self.feed = None
+        self.step_in_epoch = 0
+
+    def bind(self, x, y):
+        key = (id(x), id(y), len(x))
+        if self.feed is None or getattr(self, "_feed_key", None) != key:
+            self.feed = DataFeed(x, y, self.device)
+            self._feed_key = key
+        return self.feed
+
+    def start_epoch(self, epoch, shuffle):
+        self.feed.set_epoch(epoch, shuffle)
+        self.step_in_epoch = 0
+        self.acc.zero_()
+
+    def _one_step(self):
+        feed, model = self.feed, self.model
+        s = self.step_in_epoch
+        idx = feed.batch_indices(s, self.global_batch, self.rank * self.per_replica, self.per_replica)
+        gstart = s * self.global_batch
+        gcount = max(0, min(self.global_batch, feed.n - gstart))
+        G = self.G
+        G.zero_()
+        if idx.numel() > 0 and gcount > 0:
+            xb, yb = feed.x[idx], feed.y[idx]
+            out = model(xb, training=True)
+            ls = self.loss.per_sample(yb, out)
+            loss = ls.sum() * (1.0 / gcount)
+            grads = torch.autograd.grad(loss, self.leaves, allow_unused=True)
+            off = 0
+            for g, sz in zip(grads, self.sizes):
+                if g is not None:
+                    G[off:off + sz].copy_(g.reshape(-1))
+                off += sz
+            with torch.no_grad():
+                G[self.n] = ls.detach().sum()
+                G[self.n + 1] = float(idx.numel())
+                for i, m in enumerate(self.metric_objs):
+                    G[self.n + 2 + i] = m.per_sample(yb, out.detach()).sum()
+        if self.world > 1:
+            self.strategy.communicator.allreduce_(G, "sum")
+        self.model.optimizer.apply_flat(self.P, G[: self.n])
+        self.acc += G[self.n:].double()
+        self.step_in_epoch += 1
+
+    def run(self, n_steps):
+        for _ in range(n_steps):
+            self._one_step()
+
+    def metrics(self):
+        a = self.acc.cpu().tolist()
+        cnt = a[1] if a[1] else 1.0
+        out = {"loss": a[0] / cnt}
+        for i, m in enumerate(self.metric_objs):
+            out[m.name] = a[2 + i] / cnt
+        out["_count"] = a[1]
+        return out
+
+    def sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

@@ -1,0 +1,447 @@
+"""Keras ``Model`` / ``Sequential`` with ``compile`` / ``fit`` / ``evaluate`` / ``predict``.
+
+Training-loop contract (reference README.md:75, 304, 392 and SURVEY.md B10-B13, C3):
+
+* ``fit(x, y, batch_size=B)`` — ``B`` is the **global** batch; under
+  MultiWorkerMirroredStrategy each of the W replicas processes ``B / W`` rows per step;
+* ``steps_per_epoch`` truncates each epoch; the progbar target is the sample count
+  ("Train on 60000 samples", "320/60000 ... - loss: ... - accuracy: ...");
+* returns a :class:`~.callbacks.History` (``history.history['accuracy']``, and the R
+  accessor ``result$metrics$accuracy``, README.md:220);
+* loss and metrics are global across replicas (README.md:229-231).
+
+The model captures the strategy active at construction time (``with
+strategy.scope():``), like tf.keras.
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+
+import numpy as np
+import torch
+
+from ..parallel import runtime as _runtime
+from ..parallel.strategy import MultiWorkerMirroredStrategy, get_strategy
+from ..utils import logging as dlog
+from . import backend as K
+from . import callbacks as cbks
+from . import layers as L
+from . import losses as _losses
+from . import metrics as _metrics
+from . import optimizers as _opts
+
+KERAS_VERSION = "2.2.4-tf"
+
+
+class Model(L.Layer):
+    def __init__(self, inputs=None, outputs=None, name=None, **kw):
+        super().__init__(name=name or K.unique_name(K.to_snake_case(type(self).__name__)), **kw)
+        self._strategy = get_strategy()
+        self.optimizer = None
+        self.loss = None
+        self.compiled_metrics = []
+        self.stop_training = False
+        self._engine = None
+        self._engine_key = None
+        self._initial_epoch_override = None
+        self._inputs, self._outputs = None, None
+        self._nodes = []
+        if inputs is not None and outputs is not None:
+            self._init_graph(inputs, outputs)
+
+    # --- functional graph --------------------------------------------------------
+    def _init_graph(self, inputs, outputs):
+        self._inputs = list(inputs) if isinstance(inputs, (list, tuple)) else [inputs]
+        self._outputs = list(outputs) if isinstance(outputs, (list, tuple)) else [outputs]
+        order, seen = [], set()
+
+        def visit(t):
+            if id(t) in seen:
+                return
+            seen.add(id(t))
+            for i in t.inputs:
+                visit(i)
+            order.append(t)
+
+        for o in self._outputs:
+            visit(o)
+        self._nodes = [t for t in order if t.layer is not None and not isinstance(t.layer, L.InputLayer)]
+        self.built = True
+        self.input_shape = self._inputs[0].shape
+        self.output_shape = self._outputs[0].shape
+
+    @property
+    def layers(self):
+        if self._inputs is None:
+            return []
+        seen, out = set(), []
+        for t in self._inputs:
+            if id(t.layer) not in seen:
+                seen.add(id(t.layer))
+                out.append(t.layer)
+        for t in self._nodes:
+            if id(t.layer) not in seen:
+                seen.add(id(t.layer))
+                out.append(t.layer)
+        return out
+
+    def call(self, x, training=False):
+        vals = {id(self._inputs[0]): x}
+        for t in self._nodes:
+            args = [vals[id(i)] for i in t.inputs]
+            vals[id(t)] = t.layer(args if isinstance(t.layer, L.Add) else args[0], training=training)
+        return vals[id(self._outputs[0])]
+
+    def __call__(self, x, training=False):
+        if isinstance(x, L.KerasTensor):
+            return super().__call__(x, training)
+        return self.call(x, training=training)
+
+    def get_layer(self, name=None, index=None):
+        if index is not None:
+            return self.layers[index]
+        for l in self.layers:
+            if l.name == name:
+                return l
+        raise ValueError(f"no layer named {name}")
+
+    # --- weights -------------------------------------------------------------------
+    @property
+    def trainable_weights(self):
+        return [w for l in self.layers for w in l.trainable_weights]
+
+    @property
+    def non_trainable_weights(self):
+        return [w for l in self.layers for w in l.non_trainable_weights]
+
+    @property
+    def weights(self):
+        return [w for l in self.layers for w in l.weights]
+
+    def get_weights(self):
+        self._sync_engine()
+        return [w.numpy() for w in self.weights]
+
+    def set_weights(self, values):
+        self._sync_engine()
+        ws = self.weights
+        if len(values) != len(ws):
+            raise ValueError(f"model expects {len(ws)} weight arrays, got {len(values)}")
+        for w, v in zip(ws, values):
+            w.assign(v)
+
+    def count_params(self):
+        return int(sum(int(np.prod(w.shape)) for w in self.weights))
+
+    def _sync_engine(self):
+        if self._engine is not None:
+            self._engine.sync()
+
+    # --- compile -------------------------------------------------------------------
+    def compile(self, optimizer="rmsprop", loss=None, metrics=None, loss_weights=None, run_eagerly=None, **kw):
+        self.optimizer = _opts.get(optimizer)
+        self.loss = _losses.get(loss)
+        ms = metrics or []
+        if isinstance(ms, (str, _metrics.Metric)):
+            ms = [ms]
+        self.compiled_metrics = [_metrics.resolve(m, self.loss) for m in ms]
+        self._engine, self._engine_key = None, None
+
+    @property
+    def metrics_names(self):
+        return ["loss"] + [m.name for m in self.compiled_metrics]
+
+    # --- engine ----------------------------------------------------------------------
+    def _get_engine(self, per_replica, global_batch):
+        from ..engine import select_engine
+
+        key = (per_replica, global_batch, id(self._strategy), id(self.optimizer), id(self.loss))
+        if self._engine is None or self._engine_key != key:
+            if self._engine is not None:
+                self._engine.finish()
+            self._engine = select_engine(self, self._strategy, per_replica, global_batch)
+            self._engine_key = key
+        return self._engine
+
+    # --- fit -------------------------------------------------------------------------
+    def fit(self, x=None, y=None, batch_size=None, epochs=1, verbose=1, callbacks=None, validation_split=0.0,
+            validation_data=None, shuffle=True, class_weight=None, sample_weight=None, initial_epoch=0,
+            steps_per_epoch=None, validation_steps=None, validation_freq=1, **kw):
+        if self.optimizer is None or self.loss is None:
+            raise RuntimeError("You must compile your model before training/testing.")
+        if class_weight is not None or sample_weight is not None:
+            raise NotImplementedError("class_weight / sample_weight are not supported")
+        st = self._strategy
+        world = st.num_replicas_in_sync
+        batch_size = int(batch_size or 32)
+        if batch_size % world:
+            raise ValueError(f"global batch_size {batch_size} is not divisible by num_replicas_in_sync={world}")
+        per = batch_size // world
+        x = np.asarray(x)
+        y = np.asarray(y)
+        if validation_split and validation_data is None:
+            k = int(len(x) * (1 - validation_split))
+            validation_data = (x[k:], y[k:])
+            x, y = x[:k], y[:k]
+        n = len(x)
+        steps = int(steps_per_epoch) if steps_per_epoch else int(math.ceil(n / batch_size))
+        if isinstance(st, MultiWorkerMirroredStrategy):
+            dlog.info("Running Distribute Coordinator with mode = 'independent_worker', %s", _runtime.describe())
+            if not any(isinstance(c, (cbks.ModelCheckpoint, cbks.BackupAndRestore)) for c in (callbacks or [])):
+                dlog.warning("ModelCheckpoint callback is not provided. Workers will need to restart training if "
+                             "any fails.")
+        engine = self._get_engine(per, batch_size)
+        engine.bind(x, y)
+        hist = cbks.History()
+        cb_list = [hist]
+        if verbose:
+            cb_list.append(cbks.ProgbarLogger())
+        cb_list += list(callbacks or [])
+        params = {"batch_size": batch_size, "epochs": epochs, "steps": steps, "samples": n, "verbose": verbose,
+                  "metrics": self.metrics_names + (["val_" + m for m in self.metrics_names] if validation_data
+                                                   is not None else [])}
+        cl = cbks.CallbackList(cb_list, self, params)
+        self.stop_training = False
+        self._initial_epoch_override = None
+        cl.on_train_begin()
+        if self._initial_epoch_override is not None:
+            initial_epoch = max(initial_epoch, self._initial_epoch_override)
+        from ..parallel.runtime import fault_injection_step
+
+        fail_at = fault_injection_step()
+        if isinstance(st, MultiWorkerMirroredStrategy):
+            dlog.info("Collective batch_all_reduce: 1 all-reduces (%d grads + metric tail, %s), num_workers = %d",
+                      len(self.trainable_weights), engine.name, world)
+        per_hook = cl.needs_batch_hooks
+        refresh_s = 0.5
+        global_step = 0
+        try:
+            for epoch in range(initial_epoch, epochs):
+                cl.on_epoch_begin(epoch)
+                engine.start_epoch(epoch, shuffle)
+                done, last_ui = 0, time.time()
+                chunk = 1 if per_hook else max(1, min(steps, 200))
+                while done < steps:
+                    k = min(chunk, steps - done)
+                    if fail_at is not None and global_step <= fail_at < global_step + k:
+                        raise RuntimeError(f"DAMD_FAIL_AT: injected failure at step {fail_at}")
+                    engine.run(k)
+                    done += k
+                    global_step += k
+                    if per_hook or (verbose == 1 and time.time() - last_ui > refresh_s):
+                        logs = self._public(engine.metrics())
+                        logs["seen"] = min(done * batch_size, n) if steps_per_epoch is None else done * batch_size
+                        logs["size"] = batch_size
+                        cl.on_train_batch_end(done - 1, logs)
+                        last_ui = time.time()
+                logs = self._public(engine.end_epoch())
+                logs["seen"] = min(done * batch_size, n) if steps_per_epoch is None else done * batch_size
+                if validation_data is not None and (epoch + 1) % validation_freq == 0:
+                    vres = self.evaluate(validation_data[0], validation_data[1], batch_size=batch_size, verbose=0,
+                                         steps=validation_steps, _return_dict=True)
+                    logs.update({"val_" + k: v for k, v in vres.items()})
+                cl.on_epoch_end(epoch, {k: v for k, v in logs.items()})
+                if self.stop_training:
+                    break
+        except BaseException:
+            self._failed = True
+            raise
+        finally:
+            engine.finish()
+        self._failed = False
+        for c in cb_list:
+            if "seen" in getattr(c, "__dict__", {}):
+                pass
+        for k in list(hist.history):
+            if k == "seen":
+                hist.history.pop(k)
+        cl.on_train_end()
+        hist.params = params
+        hist.model = self
+        return hist
+
+    @staticmethod
+    def _public(d):
+        return {k: float(v) for k, v in d.items() if not k.startswith("_")}
+
+    # --- evaluate / predict ------------------------------------------------------------
+    @torch.no_grad()
+    def predict(self, x, batch_size=None, verbose=0, steps=None):
+        self._sync_engine()
+        x = np.asarray(x, dtype=np.float32)
+        bs = int(batch_size or 32)
+        dev = self._strategy.device
+        outs = []
+        for i in range(0, len(x), bs):
+            xb = torch.from_numpy(np.ascontiguousarray(x[i:i + bs])).to(dev)
+            outs.append(self(xb, training=False).float().cpu())
+        return torch.cat(outs).numpy() if outs else np.zeros((0,))
+
+    @torch.no_grad()
+    def evaluate(self, x=None, y=None, batch_size=None, verbose=1, steps=None, return_dict=False, _return_dict=False):
+        """Loss and metrics over (x, y).  Under a multi-worker strategy each worker
+        evaluates a disjoint shard and the sums are all-reduced."""
+        self._sync_engine()
+        st = self._strategy
+        x = np.asarray(x, dtype=np.float32)
+        y = np.asarray(y)
+        world, rank = st.num_replicas_in_sync, st.rank
+        bs = int(batch_size or 32)
+        n = len(x) if steps is None else min(len(x), int(steps) * bs)
+        dev = st.device
+        sums = torch.zeros(2 + len(self.compiled_metrics), dtype=torch.float64)
+        lo, hi = (n * rank) // world, (n * (rank + 1)) // world
+        for i in range(lo, hi, bs):
+            j = min(i + bs, hi)
+            xb = torch.from_numpy(np.ascontiguousarray(x[i:j])).to(dev)
+            yb = torch.from_numpy(np.ascontiguousarray(y[i:j])).to(dev)
+            out = self(xb, training=False)
+            sums[0] += float(self.loss.per_sample(yb, out).double().sum())
+            sums[1] += j - i
+            for k, m in enumerate(self.compiled_metrics):
+                sums[2 + k] += float(m.per_sample(yb, out).double().sum())
+        if world > 1:
+            st.communicator.allreduce_(sums, "sum")
+        cnt = max(float(sums[1]), 1.0)
+        res = {"loss": float(sums[0]) / cnt}
+        for k, m in enumerate(self.compiled_metrics):
+            res[m.name] = float(sums[2 + k]) / cnt
+        if verbose:
+            print(" - ".join(f"{k}: {v:.4f}" for k, v in res.items()))
+        if return_dict or _return_dict:
+            return res
+        vals = list(res.values())
+        return vals[0] if len(vals) == 1 else vals
+
+    # --- summary / config ----------------------------------------------------------------
+    def summary(self, line_length=65, print_fn=print):
+        print_fn(f'Model: "{self.name}"')
+        print_fn("_" * line_length)
+        print_fn(f"{'Layer (type)':<29}{'Output Shape':<22}{'Param #':<10}")
+        print_fn("=" * line_length)
+        for i, l in enumerate(self.layers):
+            if isinstance(l, L.InputLayer):
+                continue
+            shp = str(tuple(l.output_shape)).replace("None", "None") if l.output_shape is not None else "?"
+            print_fn(f"{l.name + ' (' + type(l).__name__ + ')':<29}{shp:<22}{l.count_params():<10}")
+            print_fn(("=" if i == len(self.layers) - 1 else "_") * line_length)
+        tp = sum(int(np.prod(w.shape)) for w in self.trainable_weights)
+        ntp = sum(int(np.prod(w.shape)) for w in self.non_trainable_weights)
+        print_fn(f"Total params: {tp + ntp:,}")
+        print_fn(f"Trainable params: {tp:,}")
+        print_fn(f"Non-trainable params: {ntp:,}")
+        print_fn("_" * line_length)
+
+    def _layer_configs(self):
+        return [{"class_name": type(l).__name__, "config": l.get_config()} for l in self.layers
+                if not isinstance(l, L.InputLayer)]
+
+    def get_config(self):
+        return {"name": self.name, "layers": self._layer_configs()}
+
+    def to_json(self, **kw):
+        return json.dumps({"class_name": type(self).__name__, "config": self.get_config(),
+                           "keras_version": KERAS_VERSION, "backend": "tensorflow"}, **kw)
+
+    # --- persistence -------------------------------------------------------------------------
+    def save(self, filepath, overwrite=True, include_optimizer=True, save_format=None):
+        from . import saving
+
+        self._sync_engine()
+        saving.save_model(self, str(filepath), include_optimizer=include_optimizer)
+
+    def save_weights(self, filepath, overwrite=True, save_format=None):
+        from . import saving
+
+        self._sync_engine()
+        saving.save_weights(self, str(filepath))
+
+    def load_weights(self, filepath, by_name=False):
+        from . import saving
+
+        self._sync_engine()
+        saving.load_weights_into(self, str(filepath), with_optimizer=False)
+
+
+class Sequential(Model):
+    def __init__(self, layers=None, name=None):
+        super().__init__(name=name or K.unique_name("sequential"))
+        self._layers = []
+        for l in layers or []:
+            self.add(l)
+
+    @property
+    def layers(self):
+        return list(self._layers)
+
+    def add(self, layer):
+        if not isinstance(layer, L.Layer):
+            raise TypeError(f"{layer!r} is not a Layer")
+        if self._layers:
+            prev = self._layers[-1]
+            if prev.built and prev.output_shape is not None and not layer.built:
+                layer._maybe_build(prev.output_shape)
+        elif layer._batch_input_shape is not None and not layer.built:
+            layer._maybe_build(layer._batch_input_shape)
+        self._layers.append(layer)
+        if layer.built:
+            self.built = True
+            self.output_shape = layer.output_shape
+            self.input_shape = self._layers[0].input_shape
+        self._engine, self._engine_key = None, None
+        return self
+
+    def pop(self):
+        self._layers.pop()
+        self._engine = None
+
+    def build(self, input_shape=None):
+        shp = tuple(input_shape)
+        for l in self._layers:
+            l._maybe_build(shp)
+            shp = l.output_shape
+        self.built = True
+        self.input_shape = tuple(input_shape)
+        self.output_shape = shp
+
+    def call(self, x, training=False):
+        for l in self._layers:
+            x = l(x, training=training)
+        return x
+
+    def __call__(self, x, training=False):
+        if not self.built:
+            self.build((None,) + tuple(x.shape[1:]))
+        return self.call(x, training=training)
+
+    def get_config(self):
+        return {"name": self.name, "layers": self._layer_configs()}
+
+
+def model_from_config(config: dict) -> Model:
+    if config["class_name"] != "Sequential":
+        raise NotImplementedError("only Sequential model configs can be rebuilt from JSON")
+    m = Sequential(name=config["config"].get("name"))
+    for lc in config["config"]["layers"]:
+        cls = L.LAYER_CLASSES[lc["class_name"]]
+        cfg = dict(lc["config"])
+        cfg.pop("dtype", None)
+        for k in ("kernel_regularizer", "bias_regularizer", "activity_regularizer", "kernel_constraint",
+                  "bias_constraint", "noise_shape", "seed"):
+            cfg.pop(k, None)
+        if "batch_input_shape" in cfg:
+            cfg["input_shape"] = tuple(cfg.pop("batch_input_shape")[1:])
+        m.add(cls(**cfg))
+    return m
+
+
+def model_from_json(s: str) -> Model:
+    return model_from_config(json.loads(s))
+
+
+def load_model(filepath, compile=True):
+    from . import saving
+
+    return saving.load_model(str(filepath), compile=compile)

@@ -1,0 +1,221 @@
+"""Communicators: the collective layer under MultiWorkerMirroredStrategy.
+
+Reference: TF CollectiveAllReduce over gRPC between CPU workers
+(reference README.md:395 ``rpc_layer='grpc'``, :398 ``CollectiveCommunication.AUTO``,
+:403-412 "Collective batch_all_reduce").  MI355X design:
+
+* :class:`RcclCommunicator` — native RCCL communicator (``_C.RcclComm``) for device
+  tensors, enqueued on the caller's HIP stream (capturable into hipGraphs); the
+  unique id is exchanged once over the control-plane process group.
+* :class:`TorchCommunicator` — ``torch.distributed`` (gloo on CPU; nccl=RCCL on GPU
+  when ``DAMD_COMM=torch``).
+* :class:`LoopbackCommunicator` — world size 1, every collective is a no-op.
+
+All communicators expose the same in-place tensor API.
+"""
+from __future__ import annotations
+
+import datetime
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..utils import logging as dlog
+
+_OPS = {"sum": 0, "max": 1, "min": 2, "avg": 3}
+_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.float64: 4}
+
+
+class Communicator:
+    name = "base"
+    world_size = 1
+    rank = 0
+
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        raise NotImplementedError
+
+    def allgather(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    def allgather_object(self, obj: Any) -> List[Any]:
+        raise NotImplementedError
+
+    def broadcast_object(self, obj: Any, root: int = 0) -> Any:
+        raise NotImplementedError
+
+    @property
+    def native(self):
+        """Native RCCL handle usable inside captured graphs (None if not RCCL)."""
+        return None
+
+    def shutdown(self) -> None:
+        pass
+
+
+class LoopbackCommunicator(Communicator):
+    name = "loopback"
+
+    def allreduce_(self, t, op="sum"):
+        return t
+
+    def broadcast_(self, t, root=0):
+        return t
+
+    def allgather(self, t):
+        return t.unsqueeze(0).clone()
+
+    def barrier(self):
+        pass
+
+    def allgather_object(self, obj):
+        return [obj]
+
+    def broadcast_object(self, obj, root=0):
+        return obj
+
+
+_TORCH_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
+class TorchCommunicator(Communicator):
+    """torch.distributed process group (gloo control plane; optional data-plane group)."""
+
+    name = "torch"
+
+    def __init__(self, world_size: int, rank: int, data_group=None):
+        self.world_size, self.rank = world_size, rank
+        self._data_group = data_group  # None -> default (gloo) group
+
+    def allreduce_(self, t, op="sum"):
+        if op == "avg":
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self._group_for(t))
+            t.div_(self.world_size)
+            return t
+        dist.all_reduce(t, op=_TORCH_OPS[op], group=self._group_for(t))
+        return t
+
+    def broadcast_(self, t, root=0):
+        dist.broadcast(t, src=root, group=self._group_for(t))
+        return t
+
+    def allgather(self, t):
+        out = [torch.empty_like(t) for _ in range(self.world_size)]
+        dist.all_gather(out, t.contiguous(), group=self._group_for(t))
+        return torch.stack(out)
+
+    def barrier(self):
+        dist.barrier()
+
+    def allgather_object(self, obj):
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj)
+        return out
+
+    def broadcast_object(self, obj, root=0):
+        box = [obj]
+        dist.broadcast_object_list(box, src=root)
+        return box[0]
+
+    def _group_for(self, t):
+        if t.is_cuda and self._data_group is not None:
+            return self._data_group
+        if t.is_cuda:
+            raise RuntimeError("device tensor on a gloo-only communicator; use RcclCommunicator")
+        return None
+
+    def shutdown(self):
+        pass
+
+
+class RcclCommunicator(TorchCommunicator):
+    """Native RCCL data plane + gloo control plane."""
+
+    name = "rccl"
+
+    def __init__(self, world_size: int, rank: int, device: int):
+        super().__init__(world_size, rank)
+        from ..native import require_C
+
+        C = require_C()
+        uid = C.rccl_unique_id() if rank == 0 else None
+        uid = self.broadcast_object(uid, root=0) if world_size > 1 else uid
+        self._comm = C.RcclComm(world_size, rank, uid, device)
+        self.device = device
+        dlog.debug("RCCL communicator up: rank %d/%d on hip device %d (RCCL %s)", rank, world_size, device,
+                   C.rccl_version())
+
+    @property
+    def native(self):
+        return self._comm
+
+    def _stream(self):
+        return torch.cuda.current_stream().cuda_stream
+
+    def allreduce_(self, t, op="sum"):
+        if not t.is_cuda:
+            return super().allreduce_(t, op)
+        if not t.is_contiguous():
+            raise ValueError("allreduce_ needs a contiguous tensor")
+        self._comm.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), _DTYPES[t.dtype], _OPS[op], self._stream())
+        return t
+
+    def broadcast_(self, t, root=0):
+        if not t.is_cuda:
+            return super().broadcast_(t, root)
+        self._comm.broadcast(t.data_ptr(), t.numel(), _DTYPES[t.dtype], root, self._stream())
+        return t
+
+    def allgather(self, t):
+        if not t.is_cuda:
+            return super().allgather(t)
+        t = t.contiguous()
+        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self._comm.allgather(t.data_ptr(), out.data_ptr(), t.numel(), _DTYPES[t.dtype], self._stream())
+        return out
+
+    def shutdown(self):
+        self._comm = None
+
+
+def init_process_group(world_size: int, rank: int, init_method: str, timeout_s: float = 600.0) -> None:
+    if dist.is_initialized():
+        return
+    dist.init_process_group(
+        backend="gloo",
+        init_method=init_method,
+        world_size=world_size,
+        rank=rank,
+        timeout=datetime.timedelta(seconds=timeout_s),
+    )
+
+
+def make_communicator(world_size: int, rank: int, device: torch.device, kind: Optional[str] = None) -> Communicator:
+    if world_size == 1 and kind in (None, "auto", "loopback"):
+        if device.type == "cuda" and kind not in ("loopback",):
+            # a size-1 RCCL comm keeps the world=1 run on exactly the same code path
+            # (BASELINE.json:8 "single-replica MirroredStrategy path") without a PG.
+            try:
+                from ..native import require_C
+
+                C = require_C()
+                c = RcclCommunicator.__new__(RcclCommunicator)
+                TorchCommunicator.__init__(c, 1, 0)
+                c._comm = C.RcclComm(1, 0, C.rccl_unique_id(), device.index or 0)
+                c.device = device.index or 0
+                return c
+            except Exception as e:  # pragma: no cover
+                dlog.warning("size-1 RCCL communicator unavailable (%s); using loopback", e)
+        return LoopbackCommunicator()
+    if device.type == "cuda":
+        if kind == "torch":
+            grp = dist.new_group(backend="nccl")
+            return TorchCommunicator(world_size, rank, data_group=grp)
+        return RcclCommunicator(world_size, rank, device.index or 0)
+    return TorchCommunicator(world_size, rank)

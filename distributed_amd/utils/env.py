@@ -1,0 +1,45 @@
+"""Environment flags (SURVEY.md §5 config/flag system).
+
+TF_CONFIG keeps the reference schema (reference README.md:84-113, 319-357); framework
+knobs use the ``DAMD_`` prefix.  NCCL_* / RCCL_* pass through untouched to RCCL.
+"""
+from __future__ import annotations
+
+import os
+
+
+def get_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return default if v in (None, "") else int(v)
+
+
+def get_float(name: str, default: float) -> float:
+    v = os.environ.get(name)
+    return default if v in (None, "") else float(v)
+
+
+def get_bool(name: str, default: bool) -> bool:
+    v = os.environ.get(name)
+    if v in (None, ""):
+        return default
+    return v.strip().lower() not in ("0", "false", "no", "off")
+
+
+def get_str(name: str, default: str) -> str:
+    v = os.environ.get(name)
+    return default if v in (None, "") else v
+
+
+# Documented knobs (README "Configuration"):
+#   DAMD_DEVICE            cpu | cuda          force the compute device
+#   DAMD_FUSED             0/1                 allow the fused native ConvNet engine (default 1)
+#   DAMD_GRAPH             0/1                 capture steps into hipGraphs (default 1)
+#   DAMD_GRAPH_STEPS       int                 steps per captured graph (default 20)
+#   DAMD_PP                1..4                pooled positions per fused slice (default 4)
+#   DAMD_COMM              rccl | torch | auto data-plane communicator on GPU (default auto=rccl)
+#   DAMD_BUCKET_MB         float               gradient bucket size for the generic engine
+#   DAMD_WATCHDOG_S        float               collective watchdog deadline (0 = off)
+#   DAMD_FAIL_AT           "rank:step"         fault injection (raise inside fit)
+#   DAMD_CHECK_MIRRORS     int                 mirror-divergence check every N epochs (0=off)
+#   DAMD_DEBUG             0/1                 synchronous launches + extra checks
+#   DAMD_LOCAL_RANK        int                 local GPU index (set by the launcher)

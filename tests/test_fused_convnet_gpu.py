@@ -1,0 +1,161 @@
+"""Fused MNIST-CNN HIP kernels vs a plain PyTorch fp32 reference of the same step."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def _model(lr=0.1, momentum=0.0, nesterov=False, seed=3):
+    import distributed_amd as tf
+
+    tf.set_seed(seed)
+    m = tf.models.mnist_cnn()
+    m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tf.keras.optimizers.SGD(learning_rate=lr, momentum=momentum, nesterov=nesterov),
+              metrics=["accuracy"])
+    return m
+
+
+def _data(n=512, seed=0):
+    rng = np.random.default_rng(seed)
+    x = rng.random((n, 28, 28, 1), dtype=np.float32)
+    y = rng.integers(0, 10, n).astype(np.int64)
+    return x, y
+
+
+def _ref_step(ws, xb, yb, gcount):
+    """fp32 torch reference: returns (grads list, loss_sum, correct)."""
+    from distributed_amd.ops import reference as R
+
+    ts = [torch.tensor(w, dtype=torch.float64, requires_grad=True) for w in ws]
+    x = torch.tensor(xb, dtype=torch.float64)
+    h = torch.relu(R.conv2d(x, ts[0], ts[1]))
+    p = R.maxpool2d(h)
+    f = p.reshape(p.shape[0], -1)
+    d = torch.relu(f @ ts[2] + ts[3])
+    z = d @ ts[4] + ts[5]
+    ls = torch.nn.functional.cross_entropy(z, torch.tensor(yb), reduction="none")
+    (ls.sum() / gcount).backward()
+    corr = float((z.argmax(-1) == torch.tensor(yb)).sum())
+    return [t.grad.numpy() for t in ts], float(ls.sum()), corr
+
+
+def _engine(model, B):
+    from distributed_amd.parallel.strategy import get_strategy
+
+    eng = model._get_engine(B, B)
+    assert eng.name == "fused_convnet", "fused engine must be selected on GPU"
+    return eng
+
+
+@pytest.mark.parametrize("B", [64, 40, 100])
+def test_one_step_matches_reference(B, monkeypatch):
+    _need_gpu()
+    monkeypatch.setenv("DAMD_GRAPH", "0")
+    lr = 0.5
+    m = _model(lr=lr)
+    x, y = _data(300)
+    w0 = m.get_weights()
+    eng = _engine(m, B)
+    eng.bind(x, y)
+    eng.start_epoch(0, shuffle=False)
+    eng.run(1)
+    met = eng.end_epoch()
+    eng.finish()
+    w1 = m.get_weights()
+    grads, lsum, corr = _ref_step(w0, x[:B], y[:B], B)
+    for a, b, g, name in zip(w0, w1, grads, ["wc", "bc", "w1", "b1", "w2", "b2"]):
+        est = (a - b) / lr
+        err = np.linalg.norm(est - g) / (np.linalg.norm(g) + 1e-12)
+        assert err < 3e-2, f"{name}: rel err {err:.3e}"
+    assert abs(met["loss"] - lsum / B) < 2e-2
+    assert abs(met["accuracy"] - corr / B) < 1.5 / B
+
+
+def test_graph_replay_bitwise_equals_eager(monkeypatch):
+    _need_gpu()
+    x, y = _data(2000)
+    res = []
+    for graph in ("0", "1"):
+        monkeypatch.setenv("DAMD_GRAPH", graph)
+        monkeypatch.setenv("DAMD_GRAPH_STEPS", "4")
+        m = _model(lr=0.05, momentum=0.9, seed=11)
+        eng = _engine(m, 64)
+        eng.bind(x, y)
+        eng.start_epoch(0, shuffle=True)
+        eng.run(10)
+        met = eng.end_epoch()
+        eng.finish()
+        res.append((np.concatenate([w.ravel() for w in m.get_weights()]), met))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert res[0][1]["loss"] == res[1][1]["loss"]
+
+
+def test_momentum_three_steps(monkeypatch):
+    _need_gpu()
+    monkeypatch.setenv("DAMD_GRAPH", "0")
+    lr, mom = 0.1, 0.9
+    m = _model(lr=lr, momentum=mom, nesterov=True, seed=5)
+    x, y = _data(256)
+    w = [a.astype(np.float64) for a in m.get_weights()]
+    v = [np.zeros_like(a) for a in w]
+    eng = _engine(m, 64)
+    eng.bind(x, y)
+    eng.start_epoch(0, shuffle=False)
+    eng.run(3)
+    eng.end_epoch()
+    eng.finish()
+    for s in range(3):
+        g, _, _ = _ref_step(w, x[s * 64:(s + 1) * 64], y[s * 64:(s + 1) * 64], 64)
+        for i in range(6):
+            v[i] = mom * v[i] - lr * g[i]
+            w[i] = w[i] + mom * v[i] - lr * g[i]
+    for a, b in zip(m.get_weights(), w):
+        err = np.linalg.norm(a - b) / (np.linalg.norm(b) + 1e-12)
+        assert err < 5e-3
+
+
+def test_fit_reference_script_on_gpu(capsys):
+    _need_gpu()
+    import distributed_amd as tf
+
+    (x, y), _ = tf.keras.datasets.mnist.load_data()
+    x = x.reshape(len(x), 28, 28, 1) / 255.0
+    m = _model(lr=0.001)
+    h = m.fit(x, y, batch_size=64, epochs=3, steps_per_epoch=5)
+    assert m._engine.name == "fused_convnet"
+    assert len(h.history["loss"]) == 3
+    assert all(abs(l - 2.30) < 0.1 for l in h.history["loss"])
+    out = capsys.readouterr().out
+    assert "Train on 60000 samples" in out and "320/60000" in out
+
+
+def test_fit_learns_synthetic(monkeypatch):
+    _need_gpu()
+    import distributed_amd as tf
+
+    (x, y), _ = tf.keras.datasets.mnist.load_data()
+    x = x.reshape(len(x), 28, 28, 1) / 255.0
+    m = _model(lr=0.05, momentum=0.9)
+    h = m.fit(x, y, batch_size=64, epochs=2, steps_per_epoch=300, verbose=0)
+    assert h.history["loss"][-1] < 1.0
+    assert h.history["accuracy"][-1] > 0.6
+    ev = m.evaluate(x[:2000], y[:2000], verbose=0)
+    assert ev[1] > 0.6
+
+
+def test_native_module_loaded():
+    _need_gpu()
+    import sys
+
+    import distributed_amd.native as n
+
+    C = n.require_C()
+    assert C.__file__.endswith(".so")
+    assert any(k.startswith("distributed_amd._C") for k in sys.modules)
