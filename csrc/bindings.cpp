@@ -38,7 +38,7 @@ class ConvNetTrainer : public StepExecutor {
     if (B <= 0) throw std::invalid_argument("batch must be > 0");
     if (PP < 1 || PP > 4) throw std::invalid_argument("positions per slice must be in [1,4]");
     auto g = [&](const char* k) -> uintptr_t { return bufs[k].cast<uintptr_t>(); };
-    b_.X = nullptr; b_.labels = nullptr; b_.perm = nullptr;
+    b_.X = nullptr; b_.labels = nullptr;
     b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
     b_.ctrl = P_<Ctrl>(g("ctrl"));
     b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
@@ -46,8 +46,9 @@ class ConvNetTrainer : public StepExecutor {
     b_.hpart = P_<float>(g("hpart")); b_.cpart = P_<float>(g("cpart"));
     HIP_CHECK(convnet_set_lds_limits());
   }
-  void set_data(uintptr_t X, uintptr_t labels, uintptr_t perm) {
-    b_.X = P_<const float>(X); b_.labels = P_<const int>(labels); b_.perm = P_<const int>(perm);
+  // X [n][784] fp32 and labels [n] int32: epoch-permuted copies (stable pointers).
+  void set_data(uintptr_t X, uintptr_t labels) {
+    b_.X = P_<const float>(X); b_.labels = P_<const int>(labels);
     invalidate_graphs();
   }
   void flush() { HIP_CHECK(convnet_launch_flush(b_, stream_)); }
@@ -71,6 +72,10 @@ PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_amd native runtime (HIP/gfx950 kernels, RCCL, hipGraph executor)";
   m.attr("CONVNET_NPARAM") = kConvNetNParam;
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
+  m.attr("CONVNET_REC") = kConvNetRec;
+  m.def("convnet_num_slices", &convnet_num_slices);
+  m.def("convnet_cpart_pitch", &convnet_cpart_pitch);
+  m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP), convnet_f3_lds(PP)); });
 
   m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) n = 0; return n; });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });

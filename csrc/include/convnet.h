@@ -5,14 +5,17 @@
 
 namespace damd {
 struct Ctrl;
+// X / labels are the epoch-permuted copies of the dataset (row g = global sample g).
 struct ConvNetBuffers {
-  const float* X; const int* labels; const int* perm;
+  const float* X; const int* labels;
   float* P; float* G; float* V; Ctrl* ctrl;
   uint16_t* pooled; uint8_t* code; float* slabs; float* dh; float* hpart; float* cpart;
 };
 constexpr int kConvNetNParam = 347146;
 constexpr int kConvNetNGrad = 347152;
+constexpr int kConvNetRec = 716;  // F2 record columns (hpart is [kConvNetRec][B])
 int convnet_num_slices(int PP);
+int convnet_cpart_pitch(int PP);  // cpart is [320][pitch]
 size_t convnet_f1_lds(int PP);
 size_t convnet_f3_lds(int PP);
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);

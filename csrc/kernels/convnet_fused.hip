@@ -6,31 +6,39 @@
 //   optimizer: SGD(lr, momentum, nesterov) on fp32 master weights.
 //
 // One training step = 3 launches (+ one RCCL all-reduce of the flat gradient between
-// steps when world > 1).  The optimizer update of step t is *deferred* into the kernels of
-// step t+1 that first consume each parameter, so no separate SGD launch exists in the
-// steady state (mnist_flush applies the last pending update before weights are read by
-// the host):
+// steps when world > 1).  At this size (183 MFLOP/step) every kernel is bound by its
+// chain of dependent memory round trips, so each kernel issues all of its independent
+// global loads up front and keeps reductions wide.  The optimizer update of step t is
+// *deferred* into the kernels of step t+1 that first consume each parameter, so there
+// is no separate SGD launch (flush_pending applies the last pending update before the
+// host reads weights):
 //
-//   F1 (grid NS, 512 thr): W1-slice SGD apply, conv SGD apply (registers), gather batch
-//       rows from the device-resident dataset, conv+bias+ReLU+maxpool on VALU, keep the
-//       pooled tile in LDS and multiply it by the matching W1 K-slice on MFMA
-//       (16x16x32 bf16, one pooled position == one K step) -> split-K slab.
-//   F2 (grid B/4, 256 thr, one wave per sample row, lane == hidden unit): split-K slab
-//       reduction + b1 + ReLU, Dense(10), softmax-xent + accuracy, dz, dh, per-block
-//       partials of dW2/db2/db1/metrics.  Last arriving block writes back the small
-//       parameters (applying their deferred update) and reduces the partials into the
-//       flat gradient buffer in a fixed order (deterministic).
-//   F3 (grid NS, 512 thr): dW1 = P^T dh (MFMA, written straight into the gradient
-//       buffer), dP = dh W1^T (MFMA, kept in LDS), MaxPool/ReLU backward via the stored
-//       argmax code, conv weight/bias gradient partials; last arriver reduces them.
+//   F1 (grid NS slices of PP pooled positions, 512 thr): apply the pending SGD update to
+//       this slice's W1 rows (owned by exactly one block) and to the conv weights (in
+//       registers), conv on MFMA (16x16x32 bf16, K = 9 taps padded): the 4 pixels of
+//       one 2x2 pool window are the 4 accumulator rows of one lane, so bias+ReLU+max+
+//       argmax happen in registers; the pooled tile stays in LDS and is multiplied by the
+//       W1 K-slice on MFMA (one pooled position == one K step) -> split-K slab.
+//   F2 (grid B, 256 thr, one sample row per block): slab reduction (4 waves split the
+//       slices) + b1 + ReLU, Dense(10), softmax-xent + accuracy, dz, dh, and the row's
+//       contributions to dW2/db2/db1/loss/correct (column-major records).
+//   F3 (grid NS, 512 thr): dW1 = P^T dh (MFMA, straight into the gradient buffer),
+//       dP = dh W1^T (MFMA into LDS), MaxPool/ReLU backward through the stored argmax
+//       code, conv weight/bias gradient partials; every block also applies the pending
+//       update of a slice of the small parameters (conv, b1, W2, b2) and reduces that
+//       slice's new gradient from F2's records; the last arriving block reduces the conv
+//       partials (deterministic fixed order).
+//   dh enters both backward MFMAs as a hi+lo pair of bf16 (~16-bit mantissa) because
+//   the conv weight gradient sums 43k terms with heavy cancellation.
 //
-// Flat parameter / gradient layout = Keras weight order (so views of the master buffer
-// are the Keras variables): conv2d/kernel (3,3,1,32), conv2d/bias, dense/kernel
-// (5408,64), dense/bias, dense_1/kernel (64,10), dense_1/bias; gradient buffer tail
-// carries [loss_sum, correct, count] so one all-reduce per step moves grads + metrics
-// (SURVEY.md D5/D6).
-#include "damd_common.h"
+// Flat parameter / gradient layout = Keras weight order (views of the master buffer are
+// the Keras variables): conv2d/kernel (3,3,1,32), conv2d/bias, dense/kernel (5408,64),
+// dense/bias, dense_1/kernel (64,10), dense_1/bias; the gradient buffer tail carries
+// [loss_sum, correct, count] so ONE all-reduce per step moves grads + metrics
+// (SURVEY.md D5/D6).  Inputs are epoch-permuted copies of the dataset (row g of the
+// epoch = global sample g), so batch rows are read directly, without an index gather.
 #include "convnet.h"
+#include "damd_common.h"
 
 namespace damd {
 namespace convnet {
@@ -47,70 +55,116 @@ constexpr int NPARAM = OFF_B2 + NCLS;        // 347146
 constexpr int OFF_LOSS = NPARAM, OFF_CORR = NPARAM + 1, OFF_CNT = NPARAM + 2;
 constexpr int NGRAD = NPARAM + 6;            // padded to 16 B: 347152
 constexpr int NSMALL = HID + HID * NCLS + NCLS;  // b1, W2, b2 contiguous: 714
-constexpr int REC = NSMALL + 2;              // F2 partial record: dW2, db2, db1 order below
+constexpr int REC = NSMALL + 2;              // F2 record columns: dW2[640] db2[10] db1[64] loss corr
+constexpr int NAUX = NCONV + NSMALL + 3;     // per-step "aux" elements spread over F3 blocks
 constexpr int CH = 64;                       // images per chunk
 constexpr int XR = 6;                        // staged input rows per image
 constexpr int MAXPP = 4;                     // max pooled positions per F1/F3 block
-static_assert(NPARAM == kConvNetNParam && NGRAD == kConvNetNGrad, "param count");
-
-// ---------------------------------------------------------------------------------
-// LDS budgets (bytes)
 constexpr int XS_BYTES = CH * XR * IMG * 4;  // 43008
-__host__ __device__ constexpr int kpitch(int pp) { return pp * 32 + 8; }
+constexpr int HP = 72;                       // bf16 pitch of 64-wide tiles (conflict-free)
+static_assert(NPARAM == kConvNetNParam && NGRAD == kConvNetNGrad, "param count");
+static_assert(REC == kConvNetRec, "record count");
 
-// Stage input rows [r0, r0+nrows) of the CH images of chunk `chunk` into xs[b][r][28].
-__device__ __forceinline__ void stage_rows(float* xs, const float* __restrict__ X,
-                                           const int* __restrict__ perm, const Ctrl& c,
-                                           int B, int chunk, int r0, int nrows) {
-  const long gstart = (long)c.cursor * c.global_batch + c.row0;
-  const int per_img = nrows * 7;  // float4 per image
-  for (int i = threadIdx.x; i < CH * per_img; i += blockDim.x) {
-    const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-    const int lb = chunk * CH + b;
-    const long g = gstart + lb;
+__host__ __device__ constexpr int kpitch(int pp) { return pp * 32 + 8; }
+__host__ __device__ constexpr int nsp(int ns) { return (ns + 3) & ~3; }
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint16_t bf16_hi(float v) { return f2bf(v); }
+__device__ __forceinline__ uint16_t bf16_lo(float v, uint16_t hi) { return f2bf(v - bf2f(hi)); }
+
+// ---- staged input rows: registers first (loads in flight early), LDS later ------------
+struct XStage {
+  float4 v[6];
+};
+__device__ __forceinline__ void x_load(XStage& st, const float* __restrict__ X, long row_base, int nsamples,
+                                       int B, int chunk, int r0, int nrows) {
+  const int per_img = nrows * 7, total = CH * per_img;
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const int i = threadIdx.x + u * 512;
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (lb < B && g < c.nsamples) {
-      const int sidx = perm[g];
-      v = reinterpret_cast<const float4*>(X + (long)sidx * NPIX + (r0 + r) * IMG)[q];
+    if (i < total) {
+      const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
+      const int lb = chunk * CH + b;
+      const long g = row_base + lb;
+      if (lb < B && g < nsamples) v = reinterpret_cast<const float4*>(X + g * NPIX + (r0 + r) * IMG)[q];
     }
-    reinterpret_cast<float4*>(xs + (b * XR + r) * IMG)[q] = v;
+    st.v[u] = v;
+  }
+}
+__device__ __forceinline__ void x_store(const XStage& st, float* xs, int nrows) {
+  const int per_img = nrows * 7, total = CH * per_img;
+#pragma unroll
+  for (int u = 0; u < 6; ++u) {
+    const int i = threadIdx.x + u * 512;
+    if (i < total) {
+      const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
+      reinterpret_cast<float4*>(xs + (b * XR + r) * IMG)[q] = st.v[u];
+    }
   }
 }
 
 // =================================================================================
-// F1: deferred SGD on W1 slice + conv, conv/ReLU/pool fwd, dense-1 split-K partial.
+// F1
 // =================================================================================
 __global__ __launch_bounds__(512) void f1_forward(
-    const float* __restrict__ X, const int* __restrict__ perm, float* __restrict__ P,
-    const float* __restrict__ G, float* __restrict__ V, const Ctrl* __restrict__ ctrl,
-    uint16_t* __restrict__ pooled, uint8_t* __restrict__ code, float* __restrict__ slabs,
-    int B, int PP) {
+    const float* __restrict__ X, float* __restrict__ P, const float* __restrict__ G,
+    float* __restrict__ V, const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
+    uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int s = blockIdx.x, tid = threadIdx.x;
+  const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
   float* xs = reinterpret_cast<float*>(smem);
-  uint16_t* as = reinterpret_cast<uint16_t*>(smem + XS_BYTES);   // [CH][KP]
-  uint16_t* w1t = as + CH * KP;                                    // [HID][KP]
-  float* cw = reinterpret_cast<float*>(w1t + HID * KP);            // [320]
+  uint16_t* as = reinterpret_cast<uint16_t*>(smem + XS_BYTES);   // [CH][KP] pooled tile
+  uint16_t* w1t = as + CH * KP;                                    // [HID][KP] W1 slice^T
+  float* cw = reinterpret_cast<float*>(w1t + HID * KP);            // [320] conv params
   const Ctrl c = *ctrl;
+  const long row_base = (long)c.cursor * c.global_batch + c.row0;
+  const int r0 = 2 * (p0 / PO);
+  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
+  const bool mom = c.momentum != 0.f;
 
-  // 1. deferred SGD of this block's W1 rows (each row owned by exactly one block).
-  {
-    const int n4 = K * HID / 4;
-    float4* P4 = reinterpret_cast<float4*>(P + OFF_W1 + p0 * 32 * HID);
-    const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
-    float4* V4 = reinterpret_cast<float4*>(V + OFF_W1 + p0 * 32 * HID);
-    const bool mom = c.momentum != 0.f;
-    for (int i = tid; i < n4; i += blockDim.x) {
-      float4 w = P4[i], g = G4[i], v = mom ? V4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  // ---- issue every independent load of the prologue ----
+  XStage xst;
+  x_load(xst, X, row_base, c.nsamples, B, 0, r0, nrows);
+  const int n4 = K * HID / 4;  // <= 2048
+  float4 wv[4], gv[4], vv[4];
+  const float4* P4 = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID);
+  const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
+  const float4* V4 = reinterpret_cast<const float4*>(V + OFF_W1 + p0 * 32 * HID);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 512;
+    // (if/else, not ?: -- a select between a global load and a local zero makes hipcc
+    //  emit flat loads through scratch)
+    wv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    gv[u] = wv[u];
+    vv[u] = wv[u];
+    if (i < n4) {
+      wv[u] = P4[i];
+      gv[u] = G4[i];
+      if (mom) vv[u] = V4[i];
+    }
+  }
+  float cp = 0.f, cg = 0.f, cv = 0.f;
+  if (tid < NCONV) { cp = P[tid]; cg = G[tid]; cv = V[tid]; }
+
+  // ---- pending SGD update: W1 rows of this slice (owner block) + conv (registers) ----
+  float4* P4w = reinterpret_cast<float4*>(P + OFF_W1 + p0 * 32 * HID);
+  float4* V4w = reinterpret_cast<float4*>(V + OFF_W1 + p0 * 32 * HID);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 512;
+    if (i < n4) {
       float4 wn, vn;
-      sgd_update(w.x, g.x, v.x, c.lr, c.momentum, c.nesterov, wn.x, vn.x);
-      sgd_update(w.y, g.y, v.y, c.lr, c.momentum, c.nesterov, wn.y, vn.y);
-      sgd_update(w.z, g.z, v.z, c.lr, c.momentum, c.nesterov, wn.z, vn.z);
-      sgd_update(w.w, g.w, v.w, c.lr, c.momentum, c.nesterov, wn.w, vn.w);
-      P4[i] = wn;
-      if (mom) V4[i] = vn;
+      sgd_update(wv[u].x, gv[u].x, vv[u].x, c.lr, c.momentum, c.nesterov, wn.x, vn.x);
+      sgd_update(wv[u].y, gv[u].y, vv[u].y, c.lr, c.momentum, c.nesterov, wn.y, vn.y);
+      sgd_update(wv[u].z, gv[u].z, vv[u].z, c.lr, c.momentum, c.nesterov, wn.z, vn.z);
+      sgd_update(wv[u].w, gv[u].w, vv[u].w, c.lr, c.momentum, c.nesterov, wn.w, vn.w);
+      P4w[i] = wn;
+      if (mom) V4w[i] = vn;
       const int e = i * 4, kr = e >> 6, n = e & 63;
       w1t[(n + 0) * KP + kr] = f2bf(wn.x);
       w1t[(n + 1) * KP + kr] = f2bf(wn.y);
@@ -118,79 +172,82 @@ __global__ __launch_bounds__(512) void f1_forward(
       w1t[(n + 3) * KP + kr] = f2bf(wn.w);
     }
   }
-  // 2. conv parameters after their deferred update (not written back here: F2 does it).
-  for (int i = tid; i < NCONV; i += blockDim.x) {
+  if (tid < NCONV) {
     float wn, vn;
-    sgd_update(P[i], G[i], V[i], c.lr, c.momentum, c.nesterov, wn, vn);
-    cw[i] = wn;
+    sgd_update(cp, cg, cv, c.lr, c.momentum, c.nesterov, wn, vn);
+    cw[tid] = wn;
   }
+  x_store(xst, xs, nrows);
   __syncthreads();
 
-  const int cb = tid >> 3, cg = tid & 7;  // conv mapping: image, 4-channel group
-  float wr[9][4], br[4];
+  // conv weights as MFMA B fragments: B[k = tap][col = channel], taps >= 9 are zero
+  bf16x8 wfrag[2];
+  float bias[2];
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int nt = 0; nt < 2; ++nt) {
+    s16x8 t;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) wr[t][j] = cw[t * NF + cg * 4 + j];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) br[j] = cw[OFF_BC + cg * 4 + j];
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * (lane >> 4) + j;
+      t[j] = (short)(k < 9 ? f2bf(cw[k * NF + 16 * nt + (lane & 15)]) : 0);
+    }
+    wfrag[nt] = __builtin_bit_cast(bf16x8, t);
+    bias[nt] = cw[OFF_BC + 16 * nt + (lane & 15)];
+  }
 
-  const int r0 = 2 * (p0 / PO);
-  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
-  const int wave = tid >> 6, lane = tid & 63;
   const int mt = wave & 3, nt0 = (wave >> 2) * 2;
   const int nchunks = (B + CH - 1) / CH;
-
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    if (chunk) __syncthreads();
-    stage_rows(xs, X, perm, c, B, chunk, r0, nrows);
-    __syncthreads();
-    // conv 3x3 + bias + ReLU + 2x2 max-pool for (image cb, channels 4cg..4cg+3)
-    {
-      const float* xb = xs + cb * XR * IMG;
-      const int lb = chunk * CH + cb;
-      for (int pl = 0; pl < np; ++pl) {
-        const int pos = p0 + pl, py = pos / PO, px = pos - py * PO;
-        const int ry = 2 * py - r0, cx = 2 * px;
-        float pt[4][4];
+    if (chunk) {
+      __syncthreads();
+      x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
+      x_store(xst, xs, nrows);
+      __syncthreads();
+    }
+    // ---- conv + bias + ReLU + 2x2 max-pool on MFMA ----
+    // row tile rt = 4 pool windows x 4 sub-pixels; window wi = pl*64 + image
+    const int nrt = 16 * np;
+    for (int rt = wave; rt < nrt; rt += 8) {
+      s16x8 at;
+      {
+        const int r = lane & 15, wi = 4 * rt + (r >> 2), sub = r & 3;
+        const int pl = wi >> 6, b = wi & 63, pos = p0 + pl, py = pos / PO, px = pos - py * PO;
+        const float* base = xs + (b * XR + 2 * py - r0 + (sub >> 1)) * IMG + 2 * px + (sub & 1);
+        const int kg = lane >> 4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pt[i][j] = xb[(ry + i) * IMG + cx + j];
-        float best[4];
-        int arg[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int dy = q >> 1, dx = q & 1;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            float a = br[j];
-#pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-              for (int kx = 0; kx < 3; ++kx) a = fmaf(pt[dy + ky][dx + kx], wr[ky * 3 + kx][j], a);
-            a = fmaxf(a, 0.f);
-            if (q == 0 || a > best[j]) { best[j] = a; arg[j] = q; }
-          }
+        for (int j = 0; j < 8; ++j) {
+          const int k = 8 * kg + j;
+          const float v = (k < 9) ? base[(k / 3) * IMG + (k % 3)] : 0.f;
+          at[j] = (short)f2bf(v);
         }
-        uint16_t hb[4];
-        uint32_t cd = 0;
+      }
+      const bf16x8 a = __builtin_bit_cast(bf16x8, at);
+      const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+      const f32x4 c0 = mfma16(a, wfrag[0], zero);
+      const f32x4 c1 = mfma16(a, wfrag[1], zero);
+      const int wo = 4 * rt + (lane >> 4), plo = wo >> 6, bo = wo & 63, lb = chunk * CH + bo;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          hb[j] = f2bf(best[j]);
-          cd |= (uint32_t)(arg[j] | ((best[j] > 0.f) ? 4 : 0)) << (8 * j);
+      for (int nt = 0; nt < 2; ++nt) {
+        const f32x4 cc = nt ? c1 : c0;
+        float best = fmaxf(cc[0] + bias[nt], 0.f);
+        int arg = 0;
+#pragma unroll
+        for (int j = 1; j < 4; ++j) {
+          const float v = fmaxf(cc[j] + bias[nt], 0.f);
+          if (v > best) { best = v; arg = j; }
         }
-        uint2 packed = make_uint2((uint32_t)hb[0] | ((uint32_t)hb[1] << 16),
-                                  (uint32_t)hb[2] | ((uint32_t)hb[3] << 16));
-        *reinterpret_cast<uint2*>(as + cb * KP + pl * 32 + cg * 4) = packed;
+        const int ch = 16 * nt + (lane & 15);
+        const uint16_t hb = f2bf(best);
+        as[bo * KP + plo * 32 + ch] = hb;
         if (lb < B) {
-          *reinterpret_cast<uint2*>(pooled + (long)lb * FEAT + pos * NF + cg * 4) = packed;
-          *reinterpret_cast<uint32_t*>(code + (long)lb * FEAT + pos * NF + cg * 4) = cd;
+          const long o = (long)lb * FEAT + (p0 + plo) * NF + ch;
+          pooled[o] = hb;
+          code[o] = (uint8_t)(arg | (best > 0.f ? 4 : 0));
         }
       }
     }
     __syncthreads();
-    // dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n]
+    // ---- dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n] ----
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int ar = 16 * mt + (lane & 15), ko = 8 * (lane >> 4);
     const int bn0 = 16 * nt0 + (lane & 15), bn1 = bn0 + 16;
@@ -214,73 +271,83 @@ __global__ __launch_bounds__(512) void f1_forward(
 }
 
 // =================================================================================
-// F2: dense-1 epilogue, dense-2, softmax-xent, dz / dh, small-param partials.
+// F2: one sample row per block
 // =================================================================================
 __global__ __launch_bounds__(256) void f2_head(
-    const int* __restrict__ perm, const int* __restrict__ labels, float* __restrict__ P,
-    float* __restrict__ G, float* __restrict__ V, Ctrl* __restrict__ ctrl,
-    const float* __restrict__ slabs, float* __restrict__ dh, float* __restrict__ hpart, int B,
-    int NS) {
-  __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 4 * 16 + 4 * REC + 4];
-  float* sp = lds;                      // updated b1[64], W2[640], b2[10]
-  float* hs = sp + NSMALL + 2;          // [4][64]
-  float* zs = hs + 4 * 64;              // [4][16]
-  float* part = zs + 4 * 16;            // [4][REC]
-  int* flag = reinterpret_cast<int*>(part + 4 * REC);
+    const int* __restrict__ labels, const float* __restrict__ P, const float* __restrict__ G,
+    const float* __restrict__ V, const Ctrl* __restrict__ ctrl, const float* __restrict__ slabs,
+    float* __restrict__ dh, float* __restrict__ rec, int B, int NS) {
+  __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 64 + 16 + 16];
+  float* sp = lds;                 // updated b1[64], W2[640], b2[10]
+  float* hw = sp + NSMALL + 2;     // [4][64] per-wave partial slab sums
+  float* hs = hw + 4 * 64;         // [64] h
+  float* zs = hs + 64;             // [16] logits
   const Ctrl c = *ctrl;
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, b = blockIdx.x;
+  const long g = (long)c.cursor * c.global_batch + c.row0 + b;
+  const bool valid = g < c.nsamples;
+  const long gstart = (long)c.cursor * c.global_batch;
+  const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
+  const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
 
-  for (int i = tid; i < NSMALL; i += blockDim.x) {
-    float wn, vn;
-    sgd_update(P[OFF_B1 + i], G[OFF_B1 + i], V[OFF_B1 + i], c.lr, c.momentum, c.nesterov, wn, vn);
-    sp[i] = wn;
+  // issue: label, small params (3 per thread), this wave's slab slices
+  const int y = valid ? labels[g] : 0;
+  float pv[3], gvv[3], vv[3];
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int i = tid + u * 256;
+    pv[u] = i < NSMALL ? P[OFF_B1 + i] : 0.f;
+    gvv[u] = i < NSMALL ? G[OFF_B1 + i] : 0.f;
+    vv[u] = i < NSMALL ? V[OFF_B1 + i] : 0.f;
   }
+  float hsum = 0.f;
+  {
+    const float* src = slabs + (long)b * HID + l;
+    const long stride = (long)B * HID;
+    float t[16];
+    for (int s0 = w; s0 < NS; s0 += 64) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int sj = s0 + 4 * j;
+        t[j] = sj < NS ? src[sj * stride] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 16; ++j) hsum += t[j];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int i = tid + u * 256;
+    if (i < NSMALL) {
+      float wn, vn;
+      sgd_update(pv[u], gvv[u], vv[u], c.lr, c.momentum, c.nesterov, wn, vn);
+      sp[i] = wn;
+    }
+  }
+  hw[w * 64 + l] = hsum;
   __syncthreads();
   const float* b1n = sp;
   const float* w2n = sp + HID;
   const float* b2n = sp + HID + HID * NCLS;
-
-  const long gstart = (long)c.cursor * c.global_batch;
-  const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
-  const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
-  const int b = blockIdx.x * 4 + w;
-  const long g = gstart + c.row0 + b;
-  const bool valid = (b < B) && (g < c.nsamples);
-
-  float h = 0.f;
-  if (b < B) {
-    const float* src = slabs + (long)b * HID + l;
-    const long stride = (long)B * HID;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-    int sidx = 0;
-    for (; sidx + 4 <= NS; sidx += 4) {
-      a0 += src[(sidx + 0) * stride];
-      a1 += src[(sidx + 1) * stride];
-      a2 += src[(sidx + 2) * stride];
-      a3 += src[(sidx + 3) * stride];
-    }
-    for (; sidx < NS; ++sidx) a0 += src[sidx * stride];
-    h = (a0 + a1) + (a2 + a3);
-  }
-  h = fmaxf(h + b1n[l], 0.f);
-  hs[w * 64 + l] = h;
+  const float h = fmaxf(((hw[l] + hw[64 + l]) + (hw[128 + l] + hw[192 + l])) + b1n[l], 0.f);
+  if (w == 0) hs[l] = h;
   __syncthreads();
-  if (l < 16) {
+  if (tid < 16) {
     float z = -INFINITY;
-    if (l < NCLS) {
-      z = b2n[l];
-      for (int k = 0; k < HID; ++k) z = fmaf(hs[w * 64 + k], w2n[k * NCLS + l], z);
+    if (tid < NCLS) {
+      z = b2n[tid];
+#pragma unroll 8
+      for (int k = 0; k < HID; ++k) z = fmaf(hs[k], w2n[k * NCLS + tid], z);
     }
-    zs[w * 16 + l] = z;
+    zs[tid] = z;
   }
   __syncthreads();
-  const int y = valid ? labels[perm[g]] : 0;
   float z[NCLS];
   float m = -INFINITY;
   int am = 0;
 #pragma unroll
   for (int k = 0; k < NCLS; ++k) {
-    z[k] = zs[w * 16 + k];
+    z[k] = zs[k];
     if (z[k] > m) { m = z[k]; am = k; }
   }
   float se = 0.f;
@@ -290,143 +357,198 @@ __global__ __launch_bounds__(256) void f2_head(
   float zy = z[0];
 #pragma unroll
   for (int k = 1; k < NCLS; ++k) zy = (k == y) ? z[k] : zy;
-  const float loss = lse - zy;
   float dz[NCLS];
 #pragma unroll
-  for (int k = 0; k < NCLS; ++k)
-    dz[k] = valid ? (__expf(z[k] - lse) - (k == y ? 1.f : 0.f)) * inv : 0.f;
-  float dhl = 0.f;
-  if (h > 0.f) {
+  for (int k = 0; k < NCLS; ++k) dz[k] = valid ? (__expf(z[k] - lse) - (k == y ? 1.f : 0.f)) * inv : 0.f;
+  if (w == 0) {
+    float dhl = 0.f;
+    if (h > 0.f) {
 #pragma unroll
-    for (int k = 0; k < NCLS; ++k) dhl = fmaf(dz[k], w2n[l * NCLS + k], dhl);
+      for (int k = 0; k < NCLS; ++k) dhl = fmaf(dz[k], w2n[l * NCLS + k], dhl);
+    }
+    dh[(long)b * HID + l] = dhl;
+    rec[(long)(650 + l) * B + b] = dhl;  // db1 contribution
   }
-  if (b < B) dh[(long)b * HID + l] = dhl;
-  // per-row partial record: [0,640) dW2 (row-major [64][10]), [640,650) db2, [650,714) db1,
-  // 714 loss, 715 correct
-  float* pr = part + w * REC;
-#pragma unroll
-  for (int k = 0; k < NCLS; ++k) pr[l * NCLS + k] = h * dz[k];
-  if (l < NCLS) {
+  // dW2[k][c] = h_k dz_c   (column-major records: rec[col][row])
+  for (int i = tid; i < HID * NCLS; i += 256) {
+    const int k = i / NCLS, cc = i - k * NCLS;
     float d = 0.f;
 #pragma unroll
-    for (int k = 0; k < NCLS; ++k) d = (k == l) ? dz[k] : d;
-    pr[640 + l] = d;
+    for (int q = 0; q < NCLS; ++q) d = (q == cc) ? dz[q] : d;
+    rec[(long)i * B + b] = hs[k] * d;
   }
-  pr[650 + l] = dhl;
-  if (l == 0) {
-    pr[714] = valid ? loss : 0.f;
-    pr[715] = (valid && am == y) ? 1.f : 0.f;
-  }
-  __syncthreads();
-  for (int i = tid; i < REC; i += blockDim.x)
-    hpart[(long)blockIdx.x * REC + i] = (part[i] + part[REC + i]) + (part[2 * REC + i] + part[3 * REC + i]);
-
-  if (!last_arriver(&ctrl->cnt_a, gridDim.x, flag)) return;
-
-  // ---- last arriving block: write back deferred updates of small + conv params ----
-  const bool mom = c.momentum != 0.f;
-  for (int i = tid; i < NSMALL + NCONV; i += blockDim.x) {
-    const int idx = i < NSMALL ? OFF_B1 + i : i - NSMALL;
-    float wn, vn;
-    sgd_update(P[idx], G[idx], V[idx], c.lr, c.momentum, c.nesterov, wn, vn);
-    P[idx] = wn;
-    if (mom) V[idx] = vn;
-  }
-  if (tid == 0) {  // fold previous step's all-reduced metrics into the epoch accumulators
-    ctrl->acc_loss = c.acc_loss + G[OFF_LOSS];
-    ctrl->acc_correct = c.acc_correct + G[OFF_CORR];
-    ctrl->acc_count = c.acc_count + G[OFF_CNT];
-  }
-  __syncthreads();
-  const int nb = gridDim.x;
-  for (int i = tid; i < REC; i += blockDim.x) {
-    float a = 0.f;
-    for (int r = 0; r < nb; ++r) a += hpart[(long)r * REC + i];
-    int dst;
-    if (i < 640) dst = OFF_W2 + i;
-    else if (i < 650) dst = OFF_B2 + (i - 640);
-    else if (i < 714) dst = OFF_B1 + (i - 650);
-    else dst = (i == 714) ? OFF_LOSS : OFF_CORR;
-    G[dst] = a;
+  if (tid < NCLS) {
+    float d = 0.f;
+#pragma unroll
+    for (int q = 0; q < NCLS; ++q) d = (q == tid) ? dz[q] : d;
+    rec[(long)(640 + tid) * B + b] = d;
   }
   if (tid == 0) {
-    const int nv = max(0, min(B, gcount - c.row0));
-    G[OFF_CNT] = (float)nv;
-    __hip_atomic_store(&ctrl->cnt_a, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    rec[(long)714 * B + b] = valid ? (lse - zy) : 0.f;
+    rec[(long)715 * B + b] = (valid && am == y) ? 1.f : 0.f;
   }
 }
 
 // =================================================================================
-// F3: dense-1 backward (dW1, dP), maxpool/ReLU backward, conv weight gradient.
+// F3
 // =================================================================================
+// aux element e: [0,320) conv param, [320,1034) b1/W2/b2, [1034,1037) metric tail.
+__device__ __forceinline__ int aux_param(int e) { return e < NCONV ? e : OFF_B1 + (e - NCONV); }
+__device__ __forceinline__ int aux_rec_col(int e) {  // record column of a small param
+  const int j = e - NCONV;
+  if (j < HID) return 650 + j;                 // db1
+  if (j < HID + HID * NCLS) return j - HID;    // dW2
+  return 640 + (j - HID - HID * NCLS);         // db2
+}
+
 __global__ __launch_bounds__(512) void f3_backward(
-    const float* __restrict__ X, const int* __restrict__ perm, const float* __restrict__ P,
-    float* __restrict__ G, Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled,
-    const uint8_t* __restrict__ code, const float* __restrict__ dh, float* __restrict__ cpart,
-    int B, int PP) {
+    const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
+    Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
+    const float* __restrict__ dh, const float* __restrict__ rec, float* __restrict__ cpart, int B, int PP) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int s = blockIdx.x, tid = threadIdx.x;
+  const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x, NSP = nsp(gridDim.x);
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
-  const int KD = PP * 32 + 4;      // dps pitch (f32)
-  constexpr int HP = 72;           // bf16 pitch of 64-wide tiles
+  const int KD = PP * 32 + 4;   // dps pitch (f32)
+  const int KC = PP * 32;       // code pitch (bytes)
   float* xs = reinterpret_cast<float*>(smem);                              // [CH][XR][28]
   float* dps = reinterpret_cast<float*>(smem + XS_BYTES);                  // [CH][KD]
   uint16_t* pt = reinterpret_cast<uint16_t*>(dps + CH * KD);               // [PP*32][HP]
-  uint16_t* dht = pt + PP * 32 * HP;                                       // [HID][HP]
-  uint16_t* dhs = dht + HID * HP;                                          // [CH][HP]
-  uint16_t* w1s = dhs + CH * HP;                                           // [PP*32][HP]
-  float* red = reinterpret_cast<float*>(w1s + PP * 32 * HP);               // [16][320]
-  int* flag = reinterpret_cast<int*>(red + 16 * NCONV);
+  uint16_t* dht = pt + PP * 32 * HP;                                       // [2][HID][HP] hi, lo
+  uint16_t* dhs = dht + 2 * HID * HP;                                      // [2][CH][HP]  hi, lo
+  uint16_t* w1s = dhs + 2 * CH * HP;                                       // [PP*32][HP]
+  uint8_t* cs = reinterpret_cast<uint8_t*>(w1s + PP * 32 * HP);            // [CH][KC]
+  int* flag = reinterpret_cast<int*>(cs + CH * KC);
+  float* red = reinterpret_cast<float*>(pt);  // [16][320] reduction scratch, after the MFMAs
   const Ctrl c = *ctrl;
-
-  // W1 rows of this slice (already updated by F1 of this step) -> bf16 [k][n]
-  for (int i = tid; i < K * HID / 4; i += blockDim.x) {
-    const float4 v = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID)[i];
-    const int e = i * 4, kr = e >> 6, n = e & 63;
-    uint2 pk = make_uint2((uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
-                          (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
-    *reinterpret_cast<uint2*>(w1s + kr * HP + n) = pk;
-  }
-
+  const long row_base = (long)c.cursor * c.global_batch + c.row0;
+  const int r0 = 2 * (p0 / PO);
+  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const int wave = tid >> 6, lane = tid & 63;
   const int ko = 8 * (lane >> 4), lr16 = lane & 15;
-  // dW1 tiles: rows (k) 16*mt, cols (n) 16*nt; wave owns nt = wave&3, mt = (wave>>2) + 2i
+
+  // ---- aux work of this block (loads issued now, consumed at the end) ----
+  const int chunk_aux = (NAUX + NS - 1) / NS;
+  const int tpe = max(1, min(512 / chunk_aux, 64));  // threads per aux element
+  const int ae_local = tid / tpe, aq = tid - ae_local * tpe;
+  const int ae = s * chunk_aux + ae_local;
+  const bool aux_on = ae_local < chunk_aux && ae < NAUX;
+  float ap = 0.f, ag = 0.f, av = 0.f, arsum = 0.f;
+  if (aux_on) {
+    if (ae < NCONV + NSMALL) {
+      const int idx = aux_param(ae);
+      if (aq == 0) { ap = P[idx]; ag = G[idx]; av = V[idx]; }
+      if (ae >= NCONV) {
+        const float* rc = rec + (long)aux_rec_col(ae) * B;
+        for (int r = aq; r < B; r += tpe) arsum += rc[r];
+      }
+    } else {
+      const int m = ae - NCONV - NSMALL;  // 0 loss, 1 correct, 2 count
+      if (aq == 0) ag = G[OFF_LOSS + m];
+      if (m < 2) {
+        const float* rc = rec + (long)(714 + m) * B;
+        for (int r = aq; r < B; r += tpe) arsum += rc[r];
+      }
+    }
+  }
+
+  // ---- prologue loads: W1 slice, dh, pooled slice, code slice, input rows ----
+  const int n4 = K * HID / 4;
+  float4 wv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 512;
+    wv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n4) wv[u] = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID)[i];
+  }
+  XStage xst;
+  float4 dv[2];
+  uint4 pv[2];
+  uint4 cv;
+  const int kq = K / 8;   // uint4 (8 bf16) per image row of the pooled slice
+  const int kc = K / 16;  // uint4 of code bytes per image
+  auto load_chunk = [&](int chunk) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {  // dh: 64x64 fp32 = 1024 float4
+      const int i = tid + u * 512, bb = i >> 4, lb = chunk * CH + bb;
+      dv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (lb < B) dv[u] = reinterpret_cast<const float4*>(dh + (long)lb * HID)[i & 15];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 512, bb = i / kq, q = i - bb * kq, lb = chunk * CH + bb;
+      pv[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (i < CH * kq && lb < B) pv[u] = *reinterpret_cast<const uint4*>(pooled + (long)lb * FEAT + p0 * NF + q * 8);
+    }
+    {
+      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
+      cv = make_uint4(0u, 0u, 0u, 0u);
+      if (i < CH * kc && lb < B) cv = *reinterpret_cast<const uint4*>(code + (long)lb * FEAT + p0 * NF + q * 16);
+    }
+    x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 512, bb = i >> 4, n = (i & 15) * 4;
+      const float e[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint16_t hi = bf16_hi(e[j]), lo = bf16_lo(e[j], hi);
+        dhs[bb * HP + n + j] = hi;
+        dhs[CH * HP + bb * HP + n + j] = lo;
+        dht[(n + j) * HP + bb] = hi;
+        dht[HID * HP + (n + j) * HP + bb] = lo;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 512;
+      if (i < CH * kq) {
+        const int bb = i / kq, q = i - bb * kq;
+        const uint32_t w4[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pt[(q * 8 + 2 * j) * HP + bb] = (uint16_t)(w4[j] & 0xffff);
+          pt[(q * 8 + 2 * j + 1) * HP + bb] = (uint16_t)(w4[j] >> 16);
+        }
+      }
+    }
+    if (tid < CH * kc) {
+      const int bb = tid / kc, q = tid - bb * kc;
+      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
+    }
+    x_store(xst, xs, nrows);
+  };
+  load_chunk(0);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 512;
+    if (i < n4) {
+      const int e = i * 4, kr = e >> 6, n = e & 63;
+      uint2 pk = make_uint2((uint32_t)f2bf(wv[u].x) | ((uint32_t)f2bf(wv[u].y) << 16),
+                            (uint32_t)f2bf(wv[u].z) | ((uint32_t)f2bf(wv[u].w) << 16));
+      *reinterpret_cast<uint2*>(w1s + kr * HP + n) = pk;
+    }
+  }
+
   const int dn = wave & 3, dm0 = wave >> 2;
   f32x4 accw[MAXPP];
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) accw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // conv-grad mapping: channel ch, image group grp (4 images)
   const int ch = tid & 31, grp = tid >> 5;
   float gw[9], gb = 0.f;
 #pragma unroll
   for (int t = 0; t < 9; ++t) gw[t] = 0.f;
-  const int r0 = 2 * (p0 / PO);
-  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const int nchunks = (B + CH - 1) / CH;
 
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    if (chunk) __syncthreads();
-    // dh chunk -> dhs [b][n] and dht [n][b] (bf16)
-    for (int i = tid; i < CH * HID; i += blockDim.x) {
-      const int bb = i >> 6, n = i & 63, lb = chunk * CH + bb;
-      const float v = lb < B ? dh[(long)lb * HID + n] : 0.f;
-      const uint16_t hv = f2bf(v);
-      dhs[bb * HP + n] = hv;
-      dht[n * HP + bb] = hv;
+    if (chunk) {
+      __syncthreads();
+      load_chunk(chunk);
     }
-    // pooled slice -> pt [k][b]
-    for (int i = tid; i < CH * K / 4; i += blockDim.x) {
-      const int bb = i / (K / 4), kq = i - bb * (K / 4), lb = chunk * CH + bb;
-      uint2 v = make_uint2(0u, 0u);
-      if (lb < B) v = *reinterpret_cast<const uint2*>(pooled + (long)lb * FEAT + p0 * NF + kq * 4);
-      pt[(kq * 4 + 0) * HP + bb] = (uint16_t)(v.x & 0xffff);
-      pt[(kq * 4 + 1) * HP + bb] = (uint16_t)(v.x >> 16);
-      pt[(kq * 4 + 2) * HP + bb] = (uint16_t)(v.y & 0xffff);
-      pt[(kq * 4 + 3) * HP + bb] = (uint16_t)(v.y >> 16);
-    }
-    stage_rows(xs, X, perm, c, B, chunk, r0, nrows);
+    store_chunk();
     __syncthreads();
-    // dW1[k][n] += sum_b P[b][k] dh[b][n]   (static accumulator indices: no scratch)
+    // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
 #pragma unroll
     for (int i = 0; i < MAXPP; ++i) {
       if (i >= np) break;
@@ -434,11 +556,13 @@ __global__ __launch_bounds__(512) void f3_backward(
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         const bf16x8 a = ld_frag(pt + (16 * mt + lr16) * HP + kk * 32 + ko);
-        const bf16x8 bb = ld_frag(dht + (16 * dn + lr16) * HP + kk * 32 + ko);
-        accw[i] = mfma16(a, bb, accw[i]);
+        const bf16x8 bh = ld_frag(dht + (16 * dn + lr16) * HP + kk * 32 + ko);
+        const bf16x8 bl = ld_frag(dht + HID * HP + (16 * dn + lr16) * HP + kk * 32 + ko);
+        accw[i] = mfma16(a, bh, accw[i]);
+        accw[i] = mfma16(a, bl, accw[i]);
       }
     }
-    // dP[b][k] = sum_n dh[b][n] W1[k][n]   (row tile = wave&3, col tiles (wave>>2)+2i)
+    // dP[b][k] = sum_n (dh_hi + dh_lo)[b][n] W1[k][n]
     {
       const int pm = wave & 3;
 #pragma unroll
@@ -448,36 +572,40 @@ __global__ __launch_bounds__(512) void f3_backward(
         f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          const bf16x8 a = ld_frag(dhs + (16 * pm + lr16) * HP + kk * 32 + ko);
+          const bf16x8 ah = ld_frag(dhs + (16 * pm + lr16) * HP + kk * 32 + ko);
+          const bf16x8 al = ld_frag(dhs + CH * HP + (16 * pm + lr16) * HP + kk * 32 + ko);
           const bf16x8 bb = ld_frag(w1s + (16 * nt + lr16) * HP + kk * 32 + ko);
-          a4 = mfma16(a, bb, a4);
+          a4 = mfma16(ah, bb, a4);
+          a4 = mfma16(al, bb, a4);
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) dps[(16 * pm + 4 * (lane >> 4) + j) * KD + 16 * nt + lr16] = a4[j];
       }
     }
     __syncthreads();
-    // maxpool + ReLU backward fused into the conv weight-gradient accumulation
+    // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
+#pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
       const int bb = grp * 4 + ii, lb = chunk * CH + bb;
-      if (lb >= B) break;
-      for (int pl = 0; pl < np; ++pl) {
-        const int pos = p0 + pl, py = pos / PO, px = pos - py * PO;
-        const int cd = code[(long)lb * FEAT + pos * NF + ch];
-        if (cd & 4) {
-          const float d = dps[bb * KD + pl * 32 + ch];
-          const int y0 = 2 * py + ((cd >> 1) & 1) - r0, x0 = 2 * px + (cd & 1);
-          const float* xp = xs + (bb * XR + y0) * IMG + x0;
+      if (lb < B) {
+        for (int pl = 0; pl < np; ++pl) {
+          const int cd = cs[bb * KC + pl * 32 + ch];
+          if (cd & 4) {
+            const int pos = p0 + pl, py = pos / PO, px = pos - py * PO;
+            const float d = dps[bb * KD + pl * 32 + ch];
+            const int y0 = 2 * py + ((cd >> 1) & 1) - r0, x0 = 2 * px + (cd & 1);
+            const float* xp = xs + (bb * XR + y0) * IMG + x0;
 #pragma unroll
-          for (int ky = 0; ky < 3; ++ky)
+            for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-            for (int kx = 0; kx < 3; ++kx) gw[ky * 3 + kx] = fmaf(d, xp[ky * IMG + kx], gw[ky * 3 + kx]);
-          gb += d;
+              for (int kx = 0; kx < 3; ++kx) gw[ky * 3 + kx] = fmaf(d, xp[ky * IMG + kx], gw[ky * 3 + kx]);
+            gb += d;
+          }
         }
       }
     }
   }
-  // dW1 straight into the flat gradient buffer (this block owns these rows)
+  // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
     if (i >= np) break;
@@ -488,22 +616,55 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_W1 + (long)(p0 * 32 + k) * HID + 16 * dn + lr16] = accw[i][j];
     }
   }
-  // conv partial: reduce 16 image groups in LDS
+  __syncthreads();  // pt/dht region becomes `red`, dps becomes `ared`
 #pragma unroll
   for (int t = 0; t < 9; ++t) red[grp * NCONV + t * NF + ch] = gw[t];
   red[grp * NCONV + OFF_BC + ch] = gb;
+  float* ared = dps;
+  ared[tid] = arsum;
   __syncthreads();
-  for (int i = tid; i < NCONV; i += blockDim.x) {
+  for (int i = tid; i < NCONV; i += 512) {
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
-    cpart[(long)s * NCONV + i] = a;
+    cpart[(long)i * NSP + s] = a;
   }
-  if (!last_arriver(&ctrl->cnt_b, gridDim.x, flag)) return;
-  const int nb = gridDim.x;
-  for (int i = tid; i < NCONV; i += blockDim.x) {
+  // ---- aux: pending update of conv/small params, new small-param grads, metrics ----
+  if (aux_on && aq == 0) {
+    float tot = 0.f;
+    for (int q = 0; q < tpe; ++q) tot += ared[ae_local * tpe + q];
+    if (ae < NCONV + NSMALL) {
+      const int idx = aux_param(ae);
+      float wn, vn;
+      sgd_update(ap, ag, av, c.lr, c.momentum, c.nesterov, wn, vn);
+      P[idx] = wn;
+      if (c.momentum != 0.f) V[idx] = vn;
+      if (ae >= NCONV) G[idx] = tot;  // new gradient of b1/W2/b2 (old one consumed above)
+    } else {
+      const int m = ae - NCONV - NSMALL;
+      float* accp = m == 0 ? &ctrl->acc_loss : (m == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
+      const float old = m == 0 ? c.acc_loss : (m == 1 ? c.acc_correct : c.acc_count);
+      *accp = old + ag;  // fold the previous step's all-reduced metric into the epoch total
+      const long gstart = (long)c.cursor * c.global_batch;
+      const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
+      G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
+    }
+  }
+  if (!last_arriver(&ctrl->cnt_b, NS, flag)) return;
+  // ---- last arriver: conv gradient = fixed-order sum of the per-block partials ----
+  for (int i = tid; i < NCONV; i += 512) {
+    const float4* src = reinterpret_cast<const float4*>(cpart + (long)i * NSP);
     float a = 0.f;
-    for (int r = 0; r < nb; ++r) a += cpart[(long)r * NCONV + i];
+    float4 t[12];
+    for (int q0 = 0; q0 < NSP / 4; q0 += 12) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) {
+        t[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q0 + q < NSP / 4) t[q] = src[q0 + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 12; ++q) a += (t[q].x + t[q].y) + (t[q].z + t[q].w);
+    }
     G[i] = a;
   }
   if (tid == 0) {
@@ -539,30 +700,31 @@ __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, floa
 }  // namespace convnet
 
 // ---------------------------------------------------------------------------------
-// Host-side launchers (called from the C++ runtime; never allocate / sync here so the
-// sequence can be captured into a hipGraph).
+// Host-side launchers (no allocation / sync: capturable into a hipGraph).
 // ---------------------------------------------------------------------------------
 int convnet_num_slices(int PP) { return (convnet::NPOS + PP - 1) / PP; }
+int convnet_cpart_pitch(int PP) { return convnet::nsp(convnet_num_slices(PP)); }
 
 size_t convnet_f1_lds(int PP) {
   const int KP = convnet::kpitch(PP);
   return convnet::XS_BYTES + (size_t)(convnet::CH + convnet::HID) * KP * 2 + convnet::NCONV * 4;
 }
 size_t convnet_f3_lds(int PP) {
-  const int KD = PP * 32 + 4, HP = 72;
-  return convnet::XS_BYTES + (size_t)convnet::CH * KD * 4 + (size_t)PP * 32 * HP * 2 * 2 +
-         (size_t)(convnet::HID + convnet::CH) * HP * 2 + 16 * convnet::NCONV * 4 + 16;
+  using namespace convnet;
+  const int KD = PP * 32 + 4;
+  return XS_BYTES + (size_t)CH * KD * 4 + (size_t)PP * 32 * HP * 2 * 2 + (size_t)2 * (HID + CH) * HP * 2 +
+         (size_t)CH * PP * 32 + 16;
 }
 
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
-  hipLaunchKernelGGL(f1_forward, dim3(NS), dim3(512), convnet_f1_lds(PP), st, b.X, b.perm, b.P, b.G,
-                     b.V, b.ctrl, b.pooled, b.code, b.slabs, B, PP);
-  hipLaunchKernelGGL(f2_head, dim3((B + 3) / 4), dim3(256), 0, st, b.perm, b.labels, b.P, b.G, b.V,
-                     b.ctrl, b.slabs, b.dh, b.hpart, B, NS);
-  hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.perm, b.P, b.G,
-                     b.ctrl, b.pooled, b.code, b.dh, b.cpart, B, PP);
+  hipLaunchKernelGGL(f1_forward, dim3(NS), dim3(512), convnet_f1_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
+                     b.pooled, b.code, b.slabs, B, PP);
+  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dh, b.hpart,
+                     B, NS);
+  hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
+                     b.pooled, b.code, b.dh, b.hpart, b.cpart, B, PP);
   return hipGetLastError();
 }
 
@@ -572,12 +734,11 @@ hipError_t convnet_launch_flush(const ConvNetBuffers& b, hipStream_t st) {
 }
 
 hipError_t convnet_set_lds_limits() {
-  // F3 needs > 64 KiB of dynamic LDS.
   hipError_t e = hipFuncSetAttribute((const void*)convnet::f3_backward,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)convnet::f1_forward,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  return hipFuncSetAttribute((const void*)convnet::f1_forward, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             160 * 1024);
 }
 
 }  // namespace damd

@@ -84,7 +84,10 @@ class FusedConvNetEngine(Engine):
         dev = self.device
         B = per_replica_batch
         self.PP = env.get_int("DAMD_PP", 4)
-        NS = (169 + self.PP - 1) // self.PP
+        if not 1 <= self.PP <= 4:
+            raise ValueError("DAMD_PP must be in [1, 4]")
+        NS = C.convnet_num_slices(self.PP)
+        NSP = C.convnet_cpart_pitch(self.PP)
         f32 = dict(dtype=torch.float32, device=dev)
         self.P = torch.zeros(NGRAD, **f32)
         self.G = torch.zeros(NGRAD, **f32)
@@ -94,8 +97,8 @@ class FusedConvNetEngine(Engine):
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
         self.slabs = torch.zeros(NS, B, HID, **f32)
         self.dh = torch.zeros(B, HID, **f32)
-        self.hpart = torch.zeros((B + 3) // 4, REC, **f32)
-        self.cpart = torch.zeros(NS, NCONV, **f32)
+        self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
+        self.cpart = torch.zeros(NCONV, NSP, **f32)
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
         off = 0
@@ -180,7 +183,10 @@ class FusedConvNetEngine(Engine):
             self.feed = DataFeed(x, y, self.device, flatten=True)
             self._feed_key = key
             torch.cuda.synchronize(self.device)
-            self.trainer.set_data(self.feed.x.data_ptr(), self.feed.y.data_ptr(), self.feed.perm.data_ptr())
+            self.x_ep = torch.empty_like(self.feed.x)
+            self.y_ep = torch.empty_like(self.feed.y)
+            torch.cuda.synchronize(self.device)
+            self.trainer.set_data(self.x_ep.data_ptr(), self.y_ep.data_ptr())
             self._ctrl_write({C_NS: self.feed.n})
         return self.feed
 
@@ -190,6 +196,11 @@ class FusedConvNetEngine(Engine):
         self._flush()
         self.trainer.sync(0.0)
         self.feed.set_epoch(epoch, shuffle)
+        # materialise the epoch order once (one gather per epoch instead of an index
+        # indirection on every step's critical path)
+        perm = self.feed.perm.long()
+        torch.index_select(self.feed.x, 0, perm, out=self.x_ep)
+        torch.index_select(self.feed.y, 0, perm, out=self.y_ep)
         opt = self.model.optimizer
         self._ctrl_write({C_CUR: 0, C_AL: 0, C_AC: 0, C_AN: 0, C_WRAP: int(wrap_steps),
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})

@@ -1,0 +1,237 @@
+"""Keras API parity on the CPU reference path (README.md:58-75, 282-304)."""
+import io
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+os.environ.setdefault("DAMD_DEVICE", "cpu")
+
+import distributed_amd as tf  # noqa: E402
+
+
+def _ref_model():
+    return tf.keras.Sequential([
+        tf.keras.layers.Conv2D(32, 3, activation="relu", input_shape=(28, 28, 1)),
+        tf.keras.layers.MaxPooling2D(),
+        tf.keras.layers.Flatten(),
+        tf.keras.layers.Dense(64, activation="relu"),
+        tf.keras.layers.Dense(10),
+    ])
+
+
+def test_names_shapes_params():
+    m = _ref_model()
+    assert [l.name for l in m.layers] == ["conv2d", "max_pooling2d", "flatten", "dense", "dense_1"]
+    assert m.count_params() == 347146
+    assert [w.name for w in m.weights] == ["conv2d/kernel:0", "conv2d/bias:0", "dense/kernel:0", "dense/bias:0",
+                                           "dense_1/kernel:0", "dense_1/bias:0"]
+    assert [l.output_shape for l in m.layers] == [(None, 26, 26, 32), (None, 13, 13, 32), (None, 5408),
+                                                  (None, 64), (None, 10)]
+    m2 = _ref_model()
+    assert m2.layers[0].name == "conv2d_1" and m2.name == "sequential_1"
+
+
+def test_glorot_uniform_limits_and_zero_bias():
+    tf.set_seed(1)
+    m = _ref_model()
+    k = m.layers[3].kernel.numpy()
+    lim = math.sqrt(6.0 / (5408 + 64))
+    assert np.abs(k).max() <= lim and np.abs(k).max() > 0.95 * lim
+    assert abs(k.std() - lim / math.sqrt(3)) < 0.02 * lim
+    ck = m.layers[0].kernel.numpy()
+    clim = math.sqrt(6.0 / (9 * 1 + 9 * 32))
+    assert np.abs(ck).max() <= clim
+    assert not m.layers[0].bias.numpy().any()
+
+
+def test_set_seed_reproducible():
+    tf.set_seed(7)
+    a = _ref_model().get_weights()
+    tf.set_seed(7)
+    b = _ref_model().get_weights()
+    assert all(np.array_equal(x, y) for x, y in zip(a, b))
+
+
+def test_forward_matches_manual_nhwc():
+    tf.set_seed(0)
+    m = _ref_model()
+    x = torch.rand(3, 28, 28, 1)
+    y = m(x)
+    w = [torch.tensor(a) for a in m.get_weights()]
+    # manual conv in NHWC via unfold, Keras flatten order
+    xc = x.permute(0, 3, 1, 2)
+    conv = torch.nn.functional.conv2d(xc, w[0].permute(3, 2, 0, 1), w[1]).relu()
+    pool = torch.nn.functional.max_pool2d(conv, 2).permute(0, 2, 3, 1).reshape(3, -1)
+    ref = (pool @ w[2] + w[3]).relu() @ w[4] + w[5]
+    assert torch.allclose(y, ref, atol=1e-5)
+
+
+def test_sparse_xent_and_accuracy_math():
+    logits = torch.tensor([[2.0, 1.0, 0.1], [0.5, 2.5, 0.0]])
+    y = np.array([0, 2])
+    l = tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True)
+    lse = torch.logsumexp(logits, -1)
+    expect = ((lse[0] - 2.0) + (lse[1] - 0.0)) / 2
+    assert abs(float(l(y, logits)) - float(expect)) < 1e-6
+    lp = tf.keras.losses.SparseCategoricalCrossentropy()
+    assert abs(float(lp(y, torch.softmax(logits, -1))) - float(expect)) < 1e-5
+    acc = tf.keras.metrics.resolve("accuracy", l)
+    acc.update_state(y, logits)
+    assert acc.result() == 0.5
+
+
+def test_sgd_exact_and_momentum():
+    p = torch.tensor([1.0, -2.0])
+    g = torch.tensor([0.5, 0.25])
+    o = tf.keras.optimizers.SGD(learning_rate=0.1)
+    o.apply_flat(p, g)
+    assert torch.allclose(p, torch.tensor([0.95, -2.025]))
+    o = tf.keras.optimizers.SGD(learning_rate=0.1, momentum=0.9, nesterov=True)
+    o.ensure_slots(2, "cpu")
+    p = torch.tensor([1.0, -2.0])
+    o.apply_flat(p, g)
+    v = -0.1 * g
+    assert torch.allclose(p, torch.tensor([1.0, -2.0]) + 0.9 * v - 0.1 * g)
+    assert o.iterations == 1
+    assert tf.keras.optimizers.SGD(lr=0.3).learning_rate == pytest.approx(0.3)
+
+
+def test_adam_step_matches_formula():
+    p = torch.tensor([1.0])
+    g = torch.tensor([0.2])
+    o = tf.keras.optimizers.Adam(learning_rate=0.01)
+    o.ensure_slots(1, "cpu")
+    o.apply_flat(p, g)
+    m, v = 0.1 * 0.2, 0.001 * 0.04
+    lr_t = 0.01 * math.sqrt(1 - 0.999) / (1 - 0.9)
+    assert abs(float(p) - (1 - lr_t * m / (math.sqrt(v) + 1e-7))) < 1e-6
+
+
+def test_readme_python_local_snippet_runs(capsys):
+    """README.md:282-304 verbatim, except `import distributed_amd as tf`."""
+    batch_size = 64
+    mnist = tf.keras.datasets.mnist
+    (x_train, y_train), (x_test, y_test) = mnist.load_data()
+    x_train = x_train.reshape(len(x_train), 28, 28, 1)
+    x_train, x_test = x_train / 255.0, x_test / 255.0
+    model = tf.keras.Sequential([
+        tf.keras.layers.Conv2D(32, 3, activation='relu', input_shape=(28, 28, 1)),
+        tf.keras.layers.MaxPooling2D(),
+        tf.keras.layers.Flatten(),
+        tf.keras.layers.Dense(64, activation='relu'),
+        tf.keras.layers.Dense(10)
+    ])
+    model.compile(
+        loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+        optimizer=tf.keras.optimizers.SGD(learning_rate=0.001), metrics=['accuracy'])
+    h = model.fit(x_train, y_train, batch_size=batch_size, epochs=3, steps_per_epoch=5)
+    out = capsys.readouterr().out
+    assert "Train on 60000 samples" in out
+    assert "Epoch 1/3" in out and "Epoch 3/3" in out
+    assert "320/60000 [..............................] - ETA:" in out
+    assert set(h.history) == {"loss", "accuracy"} and len(h.history["loss"]) == 3
+    # the reference runs at chance: loss ~ ln(10) after 15 SGD steps at lr 1e-3
+    assert all(abs(l - math.log(10)) < 0.08 for l in h.history["loss"])
+    assert h.metrics is h.history
+
+
+def test_progbar_format():
+    buf = io.StringIO()
+    pb = tf.keras.utils.Progbar(60000, stream=buf)
+    line = pb.format_line(320, [("loss", 2.2995), ("accuracy", 0.2062)], now=pb._start + 0.78)
+    assert line.startswith("  320/60000 [..............................] - ETA: ")
+    assert line.endswith(" - loss: 2.2995 - accuracy: 0.2062")
+    done = pb.format_line(60000, [("loss", 1.0)], now=pb._start + 5)
+    assert done.startswith("60000/60000 [==============================] - 5s")
+
+
+def test_fit_learns_on_cpu():
+    tf.set_seed(2)
+    (x, y), _ = tf.keras.datasets.mnist.load_data()
+    x = x[:4096].reshape(-1, 28, 28, 1) / 255.0
+    y = y[:4096]
+    m = _ref_model()
+    m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9), metrics=["accuracy"])
+    h = m.fit(x, y, batch_size=64, epochs=2, verbose=0)
+    assert h.history["loss"][1] < h.history["loss"][0] and h.history["accuracy"][1] > 0.5
+    loss, acc = m.evaluate(x[:512], y[:512], verbose=0)
+    assert acc > 0.5
+    p = m.predict(x[:10])
+    assert p.shape == (10, 10)
+
+
+def test_functional_api_and_callbacks():
+    tf.set_seed(3)
+    inp = tf.keras.Input((8,))
+    h = tf.keras.layers.Dense(16, activation="relu")(inp)
+    h2 = tf.keras.layers.Dense(16)(h)
+    s = tf.keras.layers.Add()([h, h2])
+    out = tf.keras.layers.Dense(3)(s)
+    m = tf.keras.Model(inp, out)
+    m.compile(optimizer="adam", loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              metrics=["accuracy"])
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((256, 8)).astype(np.float32)
+    y = (x[:, 0] > 0).astype(np.int64) + (x[:, 1] > 1)
+    lrs = []
+
+    class Rec(tf.keras.callbacks.Callback):
+        def on_epoch_end(self, epoch, logs=None):
+            lrs.append(self.model.optimizer.learning_rate)
+
+    sched = tf.keras.callbacks.LearningRateScheduler(lambda e: 0.01 / (1 + e))
+    h = m.fit(x, y, batch_size=32, epochs=3, verbose=0, callbacks=[sched, Rec()], validation_split=0.25)
+    assert lrs == pytest.approx([0.01, 0.005, 0.01 / 3])
+    assert "val_loss" in h.history and "val_accuracy" in h.history
+    assert h.history["loss"][-1] < h.history["loss"][0]
+
+
+def test_batchnorm_and_global_pool():
+    tf.set_seed(4)
+    m = tf.keras.Sequential([tf.keras.layers.Conv2D(4, 3, padding="same", input_shape=(8, 8, 2)),
+                             tf.keras.layers.BatchNormalization(), tf.keras.layers.ReLU(),
+                             tf.keras.layers.GlobalAveragePooling2D(), tf.keras.layers.Dense(2)])
+    names = [w.name for w in m.weights]
+    assert names[2:6] == ["batch_normalization/gamma:0", "batch_normalization/beta:0",
+                          "batch_normalization/moving_mean:0", "batch_normalization/moving_variance:0"]
+    m.compile(optimizer=tf.keras.optimizers.SGD(0.1), loss="sparse_categorical_crossentropy")
+    x = np.random.default_rng(0).standard_normal((64, 8, 8, 2)).astype(np.float32)
+    y = np.zeros(64, dtype=np.int64)
+    mm0 = m.layers[1].moving_mean.numpy().copy()
+    m.fit(x, y, batch_size=16, epochs=1, verbose=0)
+    assert not np.allclose(m.layers[1].moving_mean.numpy(), mm0)
+
+
+def test_same_padding_matches_tf_convention():
+    from distributed_amd.ops import reference as R
+
+    x = torch.arange(2 * 5 * 5 * 1, dtype=torch.float32).reshape(2, 5, 5, 1)
+    w = torch.ones(2, 2, 1, 1)
+    y = R.conv2d(x, w, None, (2, 2), "same")
+    assert y.shape == (2, 3, 3, 1)
+    # TF pads bottom/right: output[0,0] sums x[0:2,0:2]
+    assert float(y[0, 0, 0, 0]) == float(x[0, 0:2, 0:2, 0].sum())
+    assert float(y[0, 2, 2, 0]) == float(x[0, 4, 4, 0])
+
+
+def test_r_style_verbs_and_history_metrics():
+    from distributed_amd import r_api as k
+
+    model = k.keras_model_sequential()
+    model = k.pipe(model,
+                   lambda m: k.layer_conv_2d(m, filters=32, kernel_size=3, activation="relu",
+                                             input_shape=k.c(28, 28, 1)),
+                   k.layer_max_pooling_2d, k.layer_flatten,
+                   lambda m: k.layer_dense(m, units=64, activation="relu"),
+                   lambda m: k.layer_dense(m, units=10))
+    k.compile(model, loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tf.keras.optimizers.SGD(learning_rate=0.001), metrics="accuracy")
+    mnist = k.dataset_mnist()
+    x = k.array_reshape(mnist["train"]["x"][:640], k.c(640, 28, 28, 1)) / 255
+    res = k.fit(model, x, mnist["train"]["y"][:640], batch_size=64, epochs=2, steps_per_epoch=3, verbose=0)
+    assert len(res.metrics["accuracy"]) == 2
+    assert model.count_params() == 347146
