@@ -44,6 +44,7 @@ class ConvNetTrainer : public StepExecutor {
     b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
     b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
     b_.hpart = P_<float>(g("hpart")); b_.cpart = P_<float>(g("cpart"));
+    b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
     HIP_CHECK(convnet_set_lds_limits());
   }
   // X [n][784] fp32 and labels [n] int32: epoch-permuted copies (stable pointers).

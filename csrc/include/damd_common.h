@@ -88,4 +88,11 @@ __device__ __forceinline__ bool last_arriver(int* counter, int nblocks, int* fla
   return *flag != 0;
 }
 
+// Diagnostic phase stamps (s_memrealtime, 100 MHz): thread 0 of each block writes
+// st[block * 16 + idx].  `st` is null unless DAMD_STAMPS is set on the host, so the
+// production path pays one uniform scalar branch per stamp point.
+__device__ __forceinline__ void stamp(unsigned long long* st, int idx) {
+  if (st != nullptr && threadIdx.x == 0) st[blockIdx.x * 16 + idx] = __builtin_amdgcn_s_memrealtime();
+}
+
 }  // namespace damd

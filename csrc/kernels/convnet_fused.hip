@@ -111,9 +111,10 @@ __device__ __forceinline__ void x_store(const XStage& st, float* xs, int nrows) 
 __global__ __launch_bounds__(512) void f1_forward(
     const float* __restrict__ X, float* __restrict__ P, const float* __restrict__ G,
     float* __restrict__ V, const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
-    uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP) {
+    uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  stamp(st, 0);
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
   float* xs = reinterpret_cast<float*>(smem);
@@ -125,6 +126,7 @@ __global__ __launch_bounds__(512) void f1_forward(
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const bool mom = c.momentum != 0.f;
+  stamp(st, 1);
 
   // ---- issue every independent load of the prologue ----
   XStage xst;
@@ -177,8 +179,10 @@ __global__ __launch_bounds__(512) void f1_forward(
     sgd_update(cp, cg, cv, c.lr, c.momentum, c.nesterov, wn, vn);
     cw[tid] = wn;
   }
+  stamp(st, 2);
   x_store(xst, xs, nrows);
   __syncthreads();
+  stamp(st, 3);
 
   // conv weights as MFMA B fragments: B[k = tap][col = channel], taps >= 9 are zero
   bf16x8 wfrag[2];
@@ -247,6 +251,7 @@ __global__ __launch_bounds__(512) void f1_forward(
       }
     }
     __syncthreads();
+    stamp(st, 4);
     // ---- dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n] ----
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int ar = 16 * mt + (lane & 15), ko = 8 * (lane >> 4);
@@ -268,6 +273,7 @@ __global__ __launch_bounds__(512) void f1_forward(
       }
     }
   }
+  stamp(st, 5);
 }
 
 // =================================================================================
@@ -276,7 +282,8 @@ __global__ __launch_bounds__(512) void f1_forward(
 __global__ __launch_bounds__(256) void f2_head(
     const int* __restrict__ labels, const float* __restrict__ P, const float* __restrict__ G,
     const float* __restrict__ V, const Ctrl* __restrict__ ctrl, const float* __restrict__ slabs,
-    float* __restrict__ dh, float* __restrict__ rec, int B, int NS) {
+    float* __restrict__ dh, float* __restrict__ rec, int B, int NS, unsigned long long* st) {
+  stamp(st, 0);
   __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 64 + 16 + 16];
   float* sp = lds;                 // updated b1[64], W2[640], b2[10]
   float* hw = sp + NSMALL + 2;     // [4][64] per-wave partial slab sums
@@ -326,6 +333,7 @@ __global__ __launch_bounds__(256) void f2_head(
   }
   hw[w * 64 + l] = hsum;
   __syncthreads();
+  stamp(st, 1);
   const float* b1n = sp;
   const float* w2n = sp + HID;
   const float* b2n = sp + HID + HID * NCLS;
@@ -387,6 +395,7 @@ __global__ __launch_bounds__(256) void f2_head(
     rec[(long)714 * B + b] = valid ? (lse - zy) : 0.f;
     rec[(long)715 * B + b] = (valid && am == y) ? 1.f : 0.f;
   }
+  stamp(st, 2);
 }
 
 // =================================================================================
@@ -404,8 +413,10 @@ __device__ __forceinline__ int aux_rec_col(int e) {  // record column of a small
 __global__ __launch_bounds__(512) void f3_backward(
     const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
     Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
-    const float* __restrict__ dh, const float* __restrict__ rec, float* __restrict__ cpart, int B, int PP) {
+    const float* __restrict__ dh, const float* __restrict__ rec, float* __restrict__ cpart, int B, int PP,
+    unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  stamp(st, 0);
   const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x, NSP = nsp(gridDim.x);
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KD = PP * 32 + 4;   // dps pitch (f32)
@@ -548,6 +559,7 @@ __global__ __launch_bounds__(512) void f3_backward(
     }
     store_chunk();
     __syncthreads();
+    stamp(st, 1);
     // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
 #pragma unroll
     for (int i = 0; i < MAXPP; ++i) {
@@ -583,6 +595,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
     __syncthreads();
+    stamp(st, 2);
     // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
@@ -616,6 +629,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_W1 + (long)(p0 * 32 + k) * HID + 16 * dn + lr16] = accw[i][j];
     }
   }
+  stamp(st, 3);
   __syncthreads();  // pt/dht region becomes `red`, dps becomes `ared`
 #pragma unroll
   for (int t = 0; t < 9; ++t) red[grp * NCONV + t * NF + ch] = gw[t];
@@ -650,7 +664,10 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
   }
-  if (!last_arriver(&ctrl->cnt_b, NS, flag)) return;
+  stamp(st, 4);
+  const bool is_last = last_arriver(&ctrl->cnt_b, NS, flag);
+  stamp(st, 5);
+  if (!is_last) return;
   // ---- last arriver: conv gradient = fixed-order sum of the per-block partials ----
   for (int i = tid; i < NCONV; i += 512) {
     const float4* src = reinterpret_cast<const float4*>(cpart + (long)i * NSP);
@@ -672,6 +689,7 @@ __global__ __launch_bounds__(512) void f3_backward(
     ctrl->cursor = (c.wrap > 0 && c.cursor + 1 >= c.wrap) ? 0 : c.cursor + 1;
     __hip_atomic_store(&ctrl->cnt_b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  stamp(st, 6);
 }
 
 // =================================================================================
@@ -720,11 +738,12 @@ hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   hipLaunchKernelGGL(f1_forward, dim3(NS), dim3(512), convnet_f1_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.pooled, b.code, b.slabs, B, PP);
+                     b.pooled, b.code, b.slabs, B, PP, b.stamps);
   hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dh, b.hpart,
-                     B, NS);
+                     B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
   hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.pooled, b.code, b.dh, b.hpart, b.cpart, B, PP);
+                     b.pooled, b.code, b.dh, b.hpart, b.cpart, B, PP,
+                     b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   return hipGetLastError();
 }
 

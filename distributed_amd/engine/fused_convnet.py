@@ -122,6 +122,10 @@ class FusedConvNetEngine(Engine):
                     ctrl=self.ctrl.data_ptr(), pooled=self.pooled.data_ptr(), code=self.code.data_ptr(),
                     slabs=self.slabs.data_ptr(), dh=self.dh.data_ptr(), hpart=self.hpart.data_ptr(),
                     cpart=self.cpart.data_ptr())
+        self.stamps = None
+        if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
+            self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)
+            bufs["stamps"] = self.stamps.data_ptr()
         self.trainer = C.ConvNetTrainer(dev.index or 0, bufs, B, self.PP, 1)
         native = strategy.communicator.native if self.world > 1 else None
         if native is not None:

@@ -20,6 +20,7 @@ if [ "$STAGE" = all ] || [ "$STAGE" = test ]; then
   step smoke 300 python __graft_entry__.py smoke
 fi
 if [ "$STAGE" = all ] || [ "$STAGE" = bench ]; then
+  step stamps 300 python scripts/stamps.py 64
   step bench_n1 300 python bench.py --gpus 1 --steps 3000 --warmup 300
   step bench_n1_generic 300 python bench.py --gpus 1 --steps 200 --warmup 20 --engine generic
 fi

@@ -1,0 +1,54 @@
+"""Phase-stamp diagnostics of the fused ConvNet step (DAMD_STAMPS=1).
+
+Runs warm steps, then one more step, and prints per kernel / per phase the median
+(over blocks) time since that kernel's earliest block start, in microseconds
+(s_memrealtime ticks at 100 MHz)."""
+import os
+import statistics
+import sys
+
+os.environ["DAMD_STAMPS"] = "1"
+os.environ.setdefault("DAMD_GRAPH", "0")
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import distributed_amd as tf  # noqa: E402
+
+
+def main():
+    B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    (x, y), _ = tf.keras.datasets.mnist.load_data()
+    x = x.reshape(len(x), 28, 28, 1) / 255.0
+    m = tf.models.mnist_cnn()
+    tf.models.compile_reference(m)
+    eng = m._get_engine(B, B)
+    eng.bind(x, y)
+    eng.start_epoch(0, True, wrap_steps=len(x) // B)
+    eng.run(50)
+    eng.sync()
+    eng.stamps.zero_()
+    eng.run(1)
+    eng.sync()
+    st = eng.stamps.cpu().numpy()
+    NS = eng.trainer.num_slices
+    grids = {"F1": NS, "F2": B, "F3": NS}
+    names = {"F1": ["start", "ctrl", "sgd+loads", "xs staged", "conv done", "end"],
+             "F2": ["start", "slabs+params", "end"],
+             "F3": ["start", "loads staged", "mfma", "convgrad", "aux", "elected", "last end"]}
+    t0 = None
+    for k, (kn, n) in enumerate(grids.items()):
+        a = st[k, :n].astype(np.int64)
+        base = a[:, 0][a[:, 0] > 0].min()
+        t0 = base if t0 is None else t0
+        print(f"{kn}: grid {n}, first block start at +{(base - t0) / 100:.2f} us")
+        for j, nm in enumerate(names[kn]):
+            col = a[:, j]
+            col = col[col > 0]
+            if len(col) == 0:
+                continue
+            d = (col - base) / 100.0
+            print(f"   {j} {nm:14s} median {statistics.median(d):7.2f}  min {d.min():7.2f}  max {d.max():7.2f} us")
+
+
+if __name__ == "__main__":
+    main()

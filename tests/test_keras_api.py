@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-os.environ.setdefault("DAMD_DEVICE", "cpu")
+
 
 import distributed_amd as tf  # noqa: E402
 
