@@ -45,6 +45,8 @@ class ConvNetTrainer : public StepExecutor {
     b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
     b_.hpart = P_<float>(g("hpart")); b_.cpart = P_<float>(g("cpart"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
+    if (b_.cpart != b_.G + kConvNetNGrad)
+      throw std::invalid_argument("cpart must directly follow the gradient buffer (one all-reduce)");
     HIP_CHECK(convnet_set_lds_limits());
   }
   // X [n][784] fp32 and labels [n] int32: epoch-permuted copies (stable pointers).
@@ -52,7 +54,7 @@ class ConvNetTrainer : public StepExecutor {
     b_.X = P_<const float>(X); b_.labels = P_<const int>(labels);
     invalidate_graphs();
   }
-  void flush() { HIP_CHECK(convnet_launch_flush(b_, stream_)); }
+  void flush() { HIP_CHECK(convnet_launch_flush(b_, PP_, stream_)); }
   int num_slices() const { return convnet_num_slices(PP_); }
   int batch() const { return B_; }
 
@@ -61,7 +63,7 @@ class ConvNetTrainer : public StepExecutor {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
     if (grad_allreduce_ && comm_ && comm_->nranks() > 1)
-      comm_->allreduce(b_.G, b_.G, kConvNetNGrad, 0, 0, stream_);
+      comm_->allreduce(b_.G, b_.G, convnet_grad_count(PP_), 0, 0, stream_);
   }
 
  private:
@@ -76,6 +78,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CONVNET_REC") = kConvNetRec;
   m.def("convnet_num_slices", &convnet_num_slices);
   m.def("convnet_cpart_pitch", &convnet_cpart_pitch);
+  m.def("convnet_grad_count", &convnet_grad_count);
   m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP), convnet_f3_lds(PP)); });
 
   m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) n = 0; return n; });

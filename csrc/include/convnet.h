@@ -5,6 +5,7 @@
 
 namespace damd {
 struct Ctrl;
+// cpart must directly follow G in memory (one all-reduce covers both).
 // X / labels are the epoch-permuted copies of the dataset (row g = global sample g).
 struct ConvNetBuffers {
   const float* X; const int* labels;
@@ -20,6 +21,8 @@ int convnet_cpart_pitch(int PP);  // cpart is [320][pitch]
 size_t convnet_f1_lds(int PP);
 size_t convnet_f3_lds(int PP);
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
-hipError_t convnet_launch_flush(const ConvNetBuffers& b, hipStream_t st);
+hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st);
+// elements of the all-reduced gradient buffer: G[kConvNetNGrad] followed by cpart[320][pitch]
+size_t convnet_grad_count(int PP);
 hipError_t convnet_set_lds_limits();
 }  // namespace damd

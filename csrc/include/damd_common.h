@@ -13,17 +13,21 @@ namespace damd {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  // NaN stays NaN (quiet), otherwise RNE.
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
+// f32 -> bf16 (RNE, NaN-preserving) on the gfx950 hardware converter (v_cvt_pk_bf16_f32).
+// A software version with a NaN branch turns into divergent control flow that
+// serialises the surrounding LDS reads (measured: 16 us vs ~1 us for the conv loop).
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for its
+// outstanding global stores (__syncthreads() also drains vmcnt, i.e. waits for every
+// prior global store to be acknowledged -- a full memory round trip per barrier).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // Load 8 consecutive bf16 (16 B, must be 16-B aligned) from LDS / global as an MFMA fragment.
@@ -48,7 +52,9 @@ struct Ctrl {
   float acc_correct;        // 11
   float acc_count;          // 12
   int   wrap;               // 13 if > 0: cursor wraps modulo `wrap` (benchmark epochs)
-  int   pad[18];
+  int   cur2;               // 14 step index as seen by the 2nd kernel of a step (set by the 1st)
+  int   cur3;               // 15 step index as seen by the 3rd kernel (set by the 2nd)
+  int   pad[16];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

@@ -5,38 +5,47 @@
 //   -> Dense(64)+bias+ReLU -> Dense(10) logits -> SparseCategoricalCrossentropy(from_logits)
 //   optimizer: SGD(lr, momentum, nesterov) on fp32 master weights.
 //
-// One training step = 3 launches (+ one RCCL all-reduce of the flat gradient between
-// steps when world > 1).  At this size (183 MFLOP/step) every kernel is bound by its
-// chain of dependent memory round trips, so each kernel issues all of its independent
-// global loads up front and keeps reductions wide.  The optimizer update of step t is
-// *deferred* into the kernels of step t+1 that first consume each parameter, so there
-// is no separate SGD launch (flush_pending applies the last pending update before the
-// host reads weights):
+// One training step = 3 launches (+ one RCCL all-reduce of the flat gradient buffer
+// between steps when world > 1).  At this size (183 MFLOP/step) every kernel is bound
+// by its chain of dependent memory round trips, so each kernel issues all of its
+// independent global loads up front, loads are unconditional (clamped index + value
+// mask: a guarded load becomes a branch + vmcnt(0)), workgroup barriers are LDS-only
+// (lds_barrier: no wait for outstanding global stores), and no kernel has a grid-wide
+// reduction on its critical path.  The optimizer update of step t is *deferred* into
+// the kernels of step t+1 that first consume each parameter, so there is no separate
+// SGD launch (flush_pending applies the last pending update before the host reads
+// weights):
 //
-//   F1 (grid NS slices of PP pooled positions, 512 thr): apply the pending SGD update to
-//       this slice's W1 rows (owned by exactly one block) and to the conv weights (in
-//       registers), conv on MFMA (16x16x32 bf16, K = 9 taps padded): the 4 pixels of
-//       one 2x2 pool window are the 4 accumulator rows of one lane, so bias+ReLU+max+
-//       argmax happen in registers; the pooled tile stays in LDS and is multiplied by the
-//       W1 K-slice on MFMA (one pooled position == one K step) -> split-K slab.
+//   F1 (grid NS slices of PP pooled positions, 512 thr): pending SGD update of this
+//       slice's W1 rows (owned by exactly one block) and of the conv weights (in
+//       registers; their gradient = sum of F3's per-slice partials), conv on MFMA
+//       (16x16x32 bf16 with a split-precision K packing): the 4 pixels of one 2x2 pool
+//       window are the 4 accumulator rows of one lane, so bias+ReLU+max+argmax happen
+//       in registers; the pooled tile stays in LDS and is multiplied by the W1 K-slice
+//       on MFMA (one pooled position == one K step) -> split-K slab.
 //   F2 (grid B, 256 thr, one sample row per block): slab reduction (4 waves split the
-//       slices) + b1 + ReLU, Dense(10), softmax-xent + accuracy, dz, dh, and the row's
-//       contributions to dW2/db2/db1/loss/correct (column-major records).
+//       slices) + b1 + ReLU, Dense(10), softmax-xent + accuracy, dz, dh, the row's
+//       contributions to dW2/db2/db1/loss/correct (column-major records), and the
+//       write-back of the conv parameters' pending update (spread over blocks).
 //   F3 (grid NS, 512 thr): dW1 = P^T dh (MFMA, straight into the gradient buffer),
 //       dP = dh W1^T (MFMA into LDS), MaxPool/ReLU backward through the stored argmax
-//       code, conv weight/bias gradient partials; every block also applies the pending
-//       update of a slice of the small parameters (conv, b1, W2, b2) and reduces that
-//       slice's new gradient from F2's records; the last arriving block reduces the conv
-//       partials (deterministic fixed order).
+//       code, this slice's conv weight/bias gradient partial (a column of `cpart`,
+//       which is all-reduced with the gradient buffer); every block also applies the
+//       pending update of a slice of b1/W2/b2 and reduces that slice's new gradient
+//       from F2's records (fixed order: deterministic, no atomics).
 //   dh enters both backward MFMAs as a hi+lo pair of bf16 (~16-bit mantissa) because
 //   the conv weight gradient sums 43k terms with heavy cancellation.
+//
+// Step counter without intra-kernel races: F1 reads ctrl.cursor and its block 0 copies
+// it to cur2, F2 reads cur2 and copies it to cur3, F3 reads cur3 and its block 0
+// advances cursor / iterations -- no kernel writes a field it reads.
 //
 // Flat parameter / gradient layout = Keras weight order (views of the master buffer are
 // the Keras variables): conv2d/kernel (3,3,1,32), conv2d/bias, dense/kernel (5408,64),
 // dense/bias, dense_1/kernel (64,10), dense_1/bias; the gradient buffer tail carries
-// [loss_sum, correct, count] so ONE all-reduce per step moves grads + metrics
-// (SURVEY.md D5/D6).  Inputs are epoch-permuted copies of the dataset (row g of the
-// epoch = global sample g), so batch rows are read directly, without an index gather.
+// [loss_sum, correct, count] and is followed by cpart[320][NSP], so ONE all-reduce per
+// step moves grads + metrics.  Inputs are epoch-permuted copies of
+// the dataset (row g of the epoch = global sample g), read without an index gather.
 #include "convnet.h"
 #include "damd_common.h"
 
@@ -56,7 +65,7 @@ constexpr int OFF_LOSS = NPARAM, OFF_CORR = NPARAM + 1, OFF_CNT = NPARAM + 2;
 constexpr int NGRAD = NPARAM + 6;            // padded to 16 B: 347152
 constexpr int NSMALL = HID + HID * NCLS + NCLS;  // b1, W2, b2 contiguous: 714
 constexpr int REC = NSMALL + 2;              // F2 record columns: dW2[640] db2[10] db1[64] loss corr
-constexpr int NAUX = NCONV + NSMALL + 3;     // per-step "aux" elements spread over F3 blocks
+constexpr int NAUX = NSMALL + 3;             // F3 "aux" elements: b1/W2/b2 + metric tail
 constexpr int CH = 64;                       // images per chunk
 constexpr int XR = 6;                        // staged input rows per image
 constexpr int MAXPP = 4;                     // max pooled positions per F1/F3 block
@@ -70,8 +79,29 @@ __host__ __device__ constexpr int nsp(int ns) { return (ns + 3) & ~3; }
 
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint16_t bf16_hi(float v) { return f2bf(v); }
 __device__ __forceinline__ uint16_t bf16_lo(float v, uint16_t hi) { return f2bf(v - bf2f(hi)); }
+
+// next step index (wraps for benchmark epochs)
+__device__ __forceinline__ int next_cursor(const Ctrl& c, int cur) {
+  return (c.wrap > 0 && cur + 1 >= c.wrap) ? 0 : cur + 1;
+}
+
+// Sum of one cpart row (NSP floats, 16-B aligned) with every load in flight at once.
+__device__ __forceinline__ float cpart_row_sum(const float* __restrict__ row, int nsp4) {
+  const float4* r4 = reinterpret_cast<const float4*>(row);
+  float4 t[12];
+  float a = 0.f;
+  for (int q0 = 0; q0 < nsp4; q0 += 12) {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const float4 v = r4[min(q0 + q, nsp4 - 1)];
+      t[q] = (q0 + q < nsp4) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < 12; ++q) a += (t[q].x + t[q].y) + (t[q].z + t[q].w);
+  }
+  return a;
+}
 
 // ---- staged input rows: registers first (loads in flight early), LDS later ------------
 struct XStage {
@@ -82,15 +112,14 @@ __device__ __forceinline__ void x_load(XStage& st, const float* __restrict__ X, 
   const int per_img = nrows * 7, total = CH * per_img;
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
-    const int i = threadIdx.x + u * 512;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < total) {
-      const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-      const int lb = chunk * CH + b;
-      const long g = row_base + lb;
-      if (lb < B && g < nsamples) v = reinterpret_cast<const float4*>(X + g * NPIX + (r0 + r) * IMG)[q];
-    }
-    st.v[u] = v;
+    const int i = min((int)threadIdx.x + u * 512, total - 1);
+    const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
+    const int lb = chunk * CH + b;
+    const long g = row_base + lb;
+    const bool ok = ((int)threadIdx.x + u * 512 < total) && lb < B && g < nsamples;
+    const long gs = max(0L, min(g, (long)nsamples - 1));
+    const float4 v = reinterpret_cast<const float4*>(X + gs * NPIX + (r0 + r) * IMG)[q];
+    st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 __device__ __forceinline__ void x_store(const XStage& st, float* xs, int nrows) {
@@ -110,18 +139,21 @@ __device__ __forceinline__ void x_store(const XStage& st, float* xs, int nrows) 
 // =================================================================================
 __global__ __launch_bounds__(512) void f1_forward(
     const float* __restrict__ X, float* __restrict__ P, const float* __restrict__ G,
-    float* __restrict__ V, const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
-    uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP, unsigned long long* st) {
+    float* __restrict__ V, Ctrl* __restrict__ ctrl, const float* __restrict__ cpart,
+    uint16_t* __restrict__ pooled, uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP,
+    unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   stamp(st, 0);
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
+  const int nsp4 = nsp(gridDim.x) / 4;
   float* xs = reinterpret_cast<float*>(smem);
   uint16_t* as = reinterpret_cast<uint16_t*>(smem + XS_BYTES);   // [CH][KP] pooled tile
   uint16_t* w1t = as + CH * KP;                                    // [HID][KP] W1 slice^T
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);            // [320] conv params
   const Ctrl c = *ctrl;
+  if (s == 0 && tid == 0) ctrl->cur2 = c.cursor;
   const long row_base = (long)c.cursor * c.global_batch + c.row0;
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
@@ -138,20 +170,14 @@ __global__ __launch_bounds__(512) void f1_forward(
   const float4* V4 = reinterpret_cast<const float4*>(V + OFF_W1 + p0 * 32 * HID);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const int i = tid + u * 512;
-    // (if/else, not ?: -- a select between a global load and a local zero makes hipcc
-    //  emit flat loads through scratch)
-    wv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    gv[u] = wv[u];
-    vv[u] = wv[u];
-    if (i < n4) {
-      wv[u] = P4[i];
-      gv[u] = G4[i];
-      if (mom) vv[u] = V4[i];
-    }
+    const int ic = min(tid + u * 512, n4 - 1);
+    wv[u] = P4[ic];
+    gv[u] = G4[ic];
+    vv[u] = V4[ic];
   }
-  float cp = 0.f, cg = 0.f, cv = 0.f;
-  if (tid < NCONV) { cp = P[tid]; cg = G[tid]; cv = V[tid]; }
+  const int tcl = min(tid, NCONV - 1);
+  const float cp = P[tcl], cv = V[tcl];
+  const float cg = cpart_row_sum(cpart + (long)tcl * nsp4 * 4, nsp4);
 
   // ---- pending SGD update: W1 rows of this slice (owner block) + conv (registers) ----
   float4* P4w = reinterpret_cast<float4*>(P + OFF_W1 + p0 * 32 * HID);
@@ -181,10 +207,25 @@ __global__ __launch_bounds__(512) void f1_forward(
   }
   stamp(st, 2);
   x_store(xst, xs, nrows);
-  __syncthreads();
+  lds_barrier();
   stamp(st, 3);
 
-  // conv weights as MFMA B fragments: B[k = tap][col = channel], taps >= 9 are zero
+  // Conv as one 16x16x32 bf16 MFMA per tile with a split-precision K packing:
+  //   k in [0,9): x_hi*w_hi   [9,18): x_lo*w_hi   [18,27): x_hi*w_lo   [27,32): 0
+  // (x = hi + lo, w = hi + lo in bf16) -> ~16-bit-mantissa conv outputs, so the pool
+  // argmax / ReLU mask match an fp32 conv; the 23 spare K slots of a 9-tap conv pay it.
+  // Per-lane tap offsets and bit masks: branch-free selects (a ?: on the value becomes
+  // divergent control flow that serialises the LDS reads).
+  int toff[8];
+  uint32_t lomask[8], zmask[8];
+  const int kg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
+    toff[j] = (tap / 3) * IMG + (tap % 3);
+    lomask[j] = part == 1 ? 0xffffu : 0u;
+    zmask[j] = k >= 27 ? 0u : 0xffffu;
+  }
   bf16x8 wfrag[2];
   float bias[2];
 #pragma unroll
@@ -192,8 +233,11 @@ __global__ __launch_bounds__(512) void f1_forward(
     s16x8 t;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 8 * (lane >> 4) + j;
-      t[j] = (short)(k < 9 ? f2bf(cw[k * NF + 16 * nt + (lane & 15)]) : 0);
+      const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
+      const float w32 = cw[min(tap, 8) * NF + 16 * nt + (lane & 15)];
+      const uint32_t hi = f2bf(w32), lo = bf16_lo(w32, (uint16_t)hi);
+      const uint32_t wlomask = part == 2 ? 0xffffu : 0u;
+      t[j] = (short)((hi ^ ((hi ^ lo) & wlomask)) & zmask[j]);
     }
     wfrag[nt] = __builtin_bit_cast(bf16x8, t);
     bias[nt] = cw[OFF_BC + 16 * nt + (lane & 15)];
@@ -203,10 +247,10 @@ __global__ __launch_bounds__(512) void f1_forward(
   const int nchunks = (B + CH - 1) / CH;
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     if (chunk) {
-      __syncthreads();
+      lds_barrier();
       x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
       x_store(xst, xs, nrows);
-      __syncthreads();
+      lds_barrier();
     }
     // ---- conv + bias + ReLU + 2x2 max-pool on MFMA ----
     // row tile rt = 4 pool windows x 4 sub-pixels; window wi = pl*64 + image
@@ -217,12 +261,13 @@ __global__ __launch_bounds__(512) void f1_forward(
         const int r = lane & 15, wi = 4 * rt + (r >> 2), sub = r & 3;
         const int pl = wi >> 6, b = wi & 63, pos = p0 + pl, py = pos / PO, px = pos - py * PO;
         const float* base = xs + (b * XR + 2 * py - r0 + (sub >> 1)) * IMG + 2 * px + (sub & 1);
-        const int kg = lane >> 4;
+        float v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = base[toff[j]];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const int k = 8 * kg + j;
-          const float v = (k < 9) ? base[(k / 3) * IMG + (k % 3)] : 0.f;
-          at[j] = (short)f2bf(v);
+          const uint32_t hi = f2bf(v[j]), lo = bf16_lo(v[j], (uint16_t)hi);
+          at[j] = (short)((hi ^ ((hi ^ lo) & lomask[j])) & zmask[j]);
         }
       }
       const bf16x8 a = __builtin_bit_cast(bf16x8, at);
@@ -238,7 +283,8 @@ __global__ __launch_bounds__(512) void f1_forward(
 #pragma unroll
         for (int j = 1; j < 4; ++j) {
           const float v = fmaxf(cc[j] + bias[nt], 0.f);
-          if (v > best) { best = v; arg = j; }
+          arg = v > best ? j : arg;
+          best = fmaxf(best, v);
         }
         const int ch = 16 * nt + (lane & 15);
         const uint16_t hb = f2bf(best);
@@ -250,7 +296,7 @@ __global__ __launch_bounds__(512) void f1_forward(
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     stamp(st, 4);
     // ---- dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n] ----
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -280,33 +326,42 @@ __global__ __launch_bounds__(512) void f1_forward(
 // F2: one sample row per block
 // =================================================================================
 __global__ __launch_bounds__(256) void f2_head(
-    const int* __restrict__ labels, const float* __restrict__ P, const float* __restrict__ G,
-    const float* __restrict__ V, const Ctrl* __restrict__ ctrl, const float* __restrict__ slabs,
+    const int* __restrict__ labels, float* __restrict__ P, const float* __restrict__ G, float* __restrict__ V,
+    Ctrl* __restrict__ ctrl, const float* __restrict__ cpart, const float* __restrict__ slabs,
     float* __restrict__ dh, float* __restrict__ rec, int B, int NS, unsigned long long* st) {
   stamp(st, 0);
-  __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 64 + 16 + 16];
+  __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 64 + 16];
   float* sp = lds;                 // updated b1[64], W2[640], b2[10]
   float* hw = sp + NSMALL + 2;     // [4][64] per-wave partial slab sums
   float* hs = hw + 4 * 64;         // [64] h
   float* zs = hs + 64;             // [16] logits
   const Ctrl c = *ctrl;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, b = blockIdx.x;
-  const long g = (long)c.cursor * c.global_batch + c.row0 + b;
+  if (b == 0 && tid == 0) ctrl->cur3 = c.cur2;
+  const long gstart = (long)c.cur2 * c.global_batch;
+  const long g = gstart + c.row0 + b;
   const bool valid = g < c.nsamples;
-  const long gstart = (long)c.cursor * c.global_batch;
   const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
   const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
+  const int nsp4 = nsp(NS) / 4;
 
-  // issue: label, small params (3 per thread), this wave's slab slices
-  const int y = valid ? labels[g] : 0;
+  // ---- issue: label, small params (3 per thread), slab slices, conv write-back inputs ----
+  const int yl = labels[max(0L, min(g, (long)c.nsamples - 1))];
+  const int y = valid ? yl : 0;
   float pv[3], gvv[3], vv[3];
 #pragma unroll
   for (int u = 0; u < 3; ++u) {
-    const int i = tid + u * 256;
-    pv[u] = i < NSMALL ? P[OFF_B1 + i] : 0.f;
-    gvv[u] = i < NSMALL ? G[OFF_B1 + i] : 0.f;
-    vv[u] = i < NSMALL ? V[OFF_B1 + i] : 0.f;
+    const int i = min(tid + u * 256, NSMALL - 1);
+    pv[u] = P[OFF_B1 + i];
+    gvv[u] = G[OFF_B1 + i];
+    vv[u] = V[OFF_B1 + i];
   }
+  // conv parameters' pending update is written back here, spread over the B blocks
+  const int cpb = (NCONV + gridDim.x - 1) / gridDim.x;
+  const int ci = min(b * cpb + tid, NCONV - 1);
+  const bool c_on = tid < cpb && b * cpb + tid < NCONV;
+  const float cpp = P[ci], cvv = V[ci];
+  const float cgg = cpart_row_sum(cpart + (long)ci * nsp4 * 4, nsp4);
   float hsum = 0.f;
   {
     const float* src = slabs + (long)b * HID + l;
@@ -316,7 +371,8 @@ __global__ __launch_bounds__(256) void f2_head(
 #pragma unroll
       for (int j = 0; j < 16; ++j) {
         const int sj = s0 + 4 * j;
-        t[j] = sj < NS ? src[sj * stride] : 0.f;
+        const float v = src[min(sj, NS - 1) * stride];
+        t[j] = sj < NS ? v : 0.f;
       }
 #pragma unroll
       for (int j = 0; j < 16; ++j) hsum += t[j];
@@ -331,15 +387,21 @@ __global__ __launch_bounds__(256) void f2_head(
       sp[i] = wn;
     }
   }
+  if (c_on) {
+    float wn, vn;
+    sgd_update(cpp, cgg, cvv, c.lr, c.momentum, c.nesterov, wn, vn);
+    P[ci] = wn;
+    if (c.momentum != 0.f) V[ci] = vn;
+  }
   hw[w * 64 + l] = hsum;
-  __syncthreads();
+  lds_barrier();
   stamp(st, 1);
   const float* b1n = sp;
   const float* w2n = sp + HID;
   const float* b2n = sp + HID + HID * NCLS;
   const float h = fmaxf(((hw[l] + hw[64 + l]) + (hw[128 + l] + hw[192 + l])) + b1n[l], 0.f);
   if (w == 0) hs[l] = h;
-  __syncthreads();
+  lds_barrier();
   if (tid < 16) {
     float z = -INFINITY;
     if (tid < NCLS) {
@@ -349,14 +411,15 @@ __global__ __launch_bounds__(256) void f2_head(
     }
     zs[tid] = z;
   }
-  __syncthreads();
+  lds_barrier();
   float z[NCLS];
   float m = -INFINITY;
   int am = 0;
 #pragma unroll
   for (int k = 0; k < NCLS; ++k) {
     z[k] = zs[k];
-    if (z[k] > m) { m = z[k]; am = k; }
+    am = z[k] > m ? k : am;
+    m = fmaxf(m, z[k]);
   }
   float se = 0.f;
 #pragma unroll
@@ -370,10 +433,9 @@ __global__ __launch_bounds__(256) void f2_head(
   for (int k = 0; k < NCLS; ++k) dz[k] = valid ? (__expf(z[k] - lse) - (k == y ? 1.f : 0.f)) * inv : 0.f;
   if (w == 0) {
     float dhl = 0.f;
-    if (h > 0.f) {
 #pragma unroll
-      for (int k = 0; k < NCLS; ++k) dhl = fmaf(dz[k], w2n[l * NCLS + k], dhl);
-    }
+    for (int k = 0; k < NCLS; ++k) dhl = fmaf(dz[k], w2n[l * NCLS + k], dhl);
+    dhl = h > 0.f ? dhl : 0.f;
     dh[(long)b * HID + l] = dhl;
     rec[(long)(650 + l) * B + b] = dhl;  // db1 contribution
   }
@@ -401,13 +463,27 @@ __global__ __launch_bounds__(256) void f2_head(
 // =================================================================================
 // F3
 // =================================================================================
-// aux element e: [0,320) conv param, [320,1034) b1/W2/b2, [1034,1037) metric tail.
-__device__ __forceinline__ int aux_param(int e) { return e < NCONV ? e : OFF_B1 + (e - NCONV); }
-__device__ __forceinline__ int aux_rec_col(int e) {  // record column of a small param
-  const int j = e - NCONV;
+// aux element e: [0,714) b1/W2/b2 (P index OFF_B1 + e), [714,717) metric tail.
+__device__ __forceinline__ int aux_rec_col(int j) {  // record column of small param j
   if (j < HID) return 650 + j;                 // db1
   if (j < HID + HID * NCLS) return j - HID;    // dW2
   return 640 + (j - HID - HID * NCLS);         // db2
+}
+
+// sum of rc[r] for r = q, q + stride, ... < n with 8 independent loads in flight.
+__device__ __forceinline__ float rec_sum(const float* __restrict__ rc, int q, int stride, int n) {
+  float a = 0.f;
+  for (int r0 = q; r0 < n; r0 += 8 * stride) {
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = rc[min(r0 + j * stride, n - 1)];
+      t[j] = (r0 + j * stride < n) ? v : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a += t[j];
+  }
+  return a;
 }
 
 __global__ __launch_bounds__(512) void f3_backward(
@@ -428,10 +504,14 @@ __global__ __launch_bounds__(512) void f3_backward(
   uint16_t* dhs = dht + 2 * HID * HP;                                      // [2][CH][HP]  hi, lo
   uint16_t* w1s = dhs + 2 * CH * HP;                                       // [PP*32][HP]
   uint8_t* cs = reinterpret_cast<uint8_t*>(w1s + PP * 32 * HP);            // [CH][KC]
-  int* flag = reinterpret_cast<int*>(cs + CH * KC);
   float* red = reinterpret_cast<float*>(pt);  // [16][320] reduction scratch, after the MFMAs
   const Ctrl c = *ctrl;
-  const long row_base = (long)c.cursor * c.global_batch + c.row0;
+  if (s == 0 && tid == 0) {
+    ctrl->cursor = next_cursor(c, c.cur3);
+    ctrl->iterations = c.iterations + 1;
+  }
+  const long gstart = (long)c.cur3 * c.global_batch;
+  const long row_base = gstart + c.row0;
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const int wave = tid >> 6, lane = tid & 63;
@@ -443,34 +523,24 @@ __global__ __launch_bounds__(512) void f3_backward(
   const int ae_local = tid / tpe, aq = tid - ae_local * tpe;
   const int ae = s * chunk_aux + ae_local;
   const bool aux_on = ae_local < chunk_aux && ae < NAUX;
-  float ap = 0.f, ag = 0.f, av = 0.f, arsum = 0.f;
-  if (aux_on) {
-    if (ae < NCONV + NSMALL) {
-      const int idx = aux_param(ae);
-      if (aq == 0) { ap = P[idx]; ag = G[idx]; av = V[idx]; }
-      if (ae >= NCONV) {
-        const float* rc = rec + (long)aux_rec_col(ae) * B;
-        for (int r = aq; r < B; r += tpe) arsum += rc[r];
-      }
-    } else {
-      const int m = ae - NCONV - NSMALL;  // 0 loss, 1 correct, 2 count
-      if (aq == 0) ag = G[OFF_LOSS + m];
-      if (m < 2) {
-        const float* rc = rec + (long)(714 + m) * B;
-        for (int r = aq; r < B; r += tpe) arsum += rc[r];
-      }
-    }
+  const int aec = min(ae, NAUX - 1);
+  float ap, ag, av, arsum;
+  if (aec < NSMALL) {
+    ap = P[OFF_B1 + aec]; ag = G[OFF_B1 + aec]; av = V[OFF_B1 + aec];
+    arsum = rec_sum(rec + (long)aux_rec_col(aec) * B, aq, tpe, B);
+  } else {
+    const int m = aec - NSMALL;  // 0 loss, 1 correct, 2 count
+    ap = 0.f; av = 0.f;
+    ag = G[OFF_LOSS + m];
+    arsum = rec_sum(rec + (long)(714 + min(m, 1)) * B, aq, tpe, B);
   }
 
   // ---- prologue loads: W1 slice, dh, pooled slice, code slice, input rows ----
   const int n4 = K * HID / 4;
   float4 wv[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int i = tid + u * 512;
-    wv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < n4) wv[u] = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID)[i];
-  }
+  for (int u = 0; u < 4; ++u)
+    wv[u] = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID)[min(tid + u * 512, n4 - 1)];
   XStage xst;
   float4 dv[2];
   uint4 pv[2];
@@ -481,19 +551,23 @@ __global__ __launch_bounds__(512) void f3_backward(
 #pragma unroll
     for (int u = 0; u < 2; ++u) {  // dh: 64x64 fp32 = 1024 float4
       const int i = tid + u * 512, bb = i >> 4, lb = chunk * CH + bb;
-      dv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (lb < B) dv[u] = reinterpret_cast<const float4*>(dh + (long)lb * HID)[i & 15];
+      const float4 v = reinterpret_cast<const float4*>(dh + (long)min(lb, B - 1) * HID)[i & 15];
+      dv[u] = lb < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int i = tid + u * 512, bb = i / kq, q = i - bb * kq, lb = chunk * CH + bb;
-      pv[u] = make_uint4(0u, 0u, 0u, 0u);
-      if (i < CH * kq && lb < B) pv[u] = *reinterpret_cast<const uint4*>(pooled + (long)lb * FEAT + p0 * NF + q * 8);
+      const bool ok = i < CH * kq && lb < B;
+      const uint4 v = *reinterpret_cast<const uint4*>(pooled + (long)min(lb, B - 1) * FEAT + p0 * NF +
+                                                      min(q, kq - 1) * 8);
+      pv[u] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
     {
       const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
-      cv = make_uint4(0u, 0u, 0u, 0u);
-      if (i < CH * kc && lb < B) cv = *reinterpret_cast<const uint4*>(code + (long)lb * FEAT + p0 * NF + q * 16);
+      const bool ok = i < CH * kc && lb < B;
+      const uint4 v = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF +
+                                                      min(q, kc - 1) * 16);
+      cv = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
     x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
   };
@@ -504,7 +578,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       const float e[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint16_t hi = bf16_hi(e[j]), lo = bf16_lo(e[j], hi);
+        const uint16_t hi = f2bf(e[j]), lo = bf16_lo(e[j], hi);
         dhs[bb * HP + n + j] = hi;
         dhs[CH * HP + bb * HP + n + j] = lo;
         dht[(n + j) * HP + bb] = hi;
@@ -554,11 +628,11 @@ __global__ __launch_bounds__(512) void f3_backward(
 
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     if (chunk) {
-      __syncthreads();
+      lds_barrier();
       load_chunk(chunk);
     }
     store_chunk();
-    __syncthreads();
+    lds_barrier();
     stamp(st, 1);
     // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
 #pragma unroll
@@ -594,30 +668,30 @@ __global__ __launch_bounds__(512) void f3_backward(
         for (int j = 0; j < 4; ++j) dps[(16 * pm + 4 * (lane >> 4) + j) * KD + 16 * nt + lr16] = a4[j];
       }
     }
-    __syncthreads();
+    lds_barrier();
     stamp(st, 2);
     // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
+    // (branch-free: the gradient is masked, the reads always hit staged LDS rows)
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
-      const int bb = grp * 4 + ii, lb = chunk * CH + bb;
-      if (lb < B) {
-        for (int pl = 0; pl < np; ++pl) {
-          const int cd = cs[bb * KC + pl * 32 + ch];
-          if (cd & 4) {
-            const int pos = p0 + pl, py = pos / PO, px = pos - py * PO;
-            const float d = dps[bb * KD + pl * 32 + ch];
-            const int y0 = 2 * py + ((cd >> 1) & 1) - r0, x0 = 2 * px + (cd & 1);
-            const float* xp = xs + (bb * XR + y0) * IMG + x0;
+      const int bb = grp * 4 + ii;
+      for (int pl = 0; pl < np; ++pl) {
+        const int cd = cs[bb * KC + pl * 32 + ch];
+        const int pos = p0 + pl, py = pos / PO, px = pos - py * PO;
+        const float dv0 = dps[bb * KD + pl * 32 + ch];
+        const float d = (cd & 4) ? dv0 : 0.f;
+        const int y0 = 2 * py + ((cd >> 1) & 1) - r0, x0 = 2 * px + (cd & 1);
+        const float* xp = xs + (bb * XR + y0) * IMG + x0;
+        float xv[9];
 #pragma unroll
-            for (int ky = 0; ky < 3; ++ky)
+        for (int t = 0; t < 9; ++t) xv[t] = xp[(t / 3) * IMG + (t % 3)];
 #pragma unroll
-              for (int kx = 0; kx < 3; ++kx) gw[ky * 3 + kx] = fmaf(d, xp[ky * IMG + kx], gw[ky * 3 + kx]);
-            gb += d;
-          }
-        }
+        for (int t = 0; t < 9; ++t) gw[t] = fmaf(d, xv[t], gw[t]);
+        gb += d;
       }
     }
   }
+  stamp(st, 3);
   // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
@@ -629,80 +703,61 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_W1 + (long)(p0 * 32 + k) * HID + 16 * dn + lr16] = accw[i][j];
     }
   }
-  stamp(st, 3);
-  __syncthreads();  // pt/dht region becomes `red`, dps becomes `ared`
+  lds_barrier();  // pt/dht region becomes `red`, dps becomes `ared`
 #pragma unroll
   for (int t = 0; t < 9; ++t) red[grp * NCONV + t * NF + ch] = gw[t];
   red[grp * NCONV + OFF_BC + ch] = gb;
   float* ared = dps;
   ared[tid] = arsum;
-  __syncthreads();
+  lds_barrier();
+  // this slice's conv-gradient partial: column s of cpart (all-reduced with G)
   for (int i = tid; i < NCONV; i += 512) {
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
     cpart[(long)i * NSP + s] = a;
   }
-  // ---- aux: pending update of conv/small params, new small-param grads, metrics ----
+  // ---- aux: pending update of b1/W2/b2, their new gradients, metrics ----
   if (aux_on && aq == 0) {
     float tot = 0.f;
     for (int q = 0; q < tpe; ++q) tot += ared[ae_local * tpe + q];
-    if (ae < NCONV + NSMALL) {
-      const int idx = aux_param(ae);
+    if (ae < NSMALL) {
       float wn, vn;
       sgd_update(ap, ag, av, c.lr, c.momentum, c.nesterov, wn, vn);
-      P[idx] = wn;
-      if (c.momentum != 0.f) V[idx] = vn;
-      if (ae >= NCONV) G[idx] = tot;  // new gradient of b1/W2/b2 (old one consumed above)
+      P[OFF_B1 + ae] = wn;
+      if (c.momentum != 0.f) V[OFF_B1 + ae] = vn;
+      G[OFF_B1 + ae] = tot;  // new gradient (the old one was consumed above)
     } else {
-      const int m = ae - NCONV - NSMALL;
+      const int m = ae - NSMALL;
       float* accp = m == 0 ? &ctrl->acc_loss : (m == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
       const float old = m == 0 ? c.acc_loss : (m == 1 ? c.acc_correct : c.acc_count);
       *accp = old + ag;  // fold the previous step's all-reduced metric into the epoch total
-      const long gstart = (long)c.cursor * c.global_batch;
       const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
       G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
   }
   stamp(st, 4);
-  const bool is_last = last_arriver(&ctrl->cnt_b, NS, flag);
-  stamp(st, 5);
-  if (!is_last) return;
-  // ---- last arriver: conv gradient = fixed-order sum of the per-block partials ----
-  for (int i = tid; i < NCONV; i += 512) {
-    const float4* src = reinterpret_cast<const float4*>(cpart + (long)i * NSP);
-    float a = 0.f;
-    float4 t[12];
-    for (int q0 = 0; q0 < NSP / 4; q0 += 12) {
-#pragma unroll
-      for (int q = 0; q < 12; ++q) {
-        t[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (q0 + q < NSP / 4) t[q] = src[q0 + q];
-      }
-#pragma unroll
-      for (int q = 0; q < 12; ++q) a += (t[q].x + t[q].y) + (t[q].z + t[q].w);
-    }
-    G[i] = a;
-  }
-  if (tid == 0) {
-    ctrl->iterations = c.iterations + 1;
-    ctrl->cursor = (c.wrap > 0 && c.cursor + 1 >= c.wrap) ? 0 : c.cursor + 1;
-    __hip_atomic_store(&ctrl->cnt_b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  stamp(st, 6);
 }
 
 // =================================================================================
 // flush: apply the pending (deferred) update to every parameter, zero the gradient
-// buffer and fold the pending metrics into the epoch accumulators.
+// buffers and fold the pending metrics into the epoch accumulators.
 // =================================================================================
 __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, float* __restrict__ G,
-                                                     float* __restrict__ V, Ctrl* __restrict__ ctrl) {
+                                                     float* __restrict__ V, Ctrl* __restrict__ ctrl,
+                                                     float* __restrict__ cpart, int NSP) {
   const Ctrl c = *ctrl;
   const bool mom = c.momentum != 0.f;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NPARAM; i += gridDim.x * blockDim.x) {
+    float g;
+    if (i < NCONV) {
+      g = cpart_row_sum(cpart + (long)i * NSP, NSP / 4);
+      for (int q = 0; q < NSP; ++q) cpart[(long)i * NSP + q] = 0.f;
+    } else {
+      g = G[i];
+    }
     float wn, vn;
-    sgd_update(P[i], G[i], V[i], c.lr, c.momentum, c.nesterov, wn, vn);
+    sgd_update(P[i], g, V[i], c.lr, c.momentum, c.nesterov, wn, vn);
     P[i] = wn;
     if (mom) V[i] = vn;
     G[i] = 0.f;
@@ -722,6 +777,9 @@ __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, floa
 // ---------------------------------------------------------------------------------
 int convnet_num_slices(int PP) { return (convnet::NPOS + PP - 1) / PP; }
 int convnet_cpart_pitch(int PP) { return convnet::nsp(convnet_num_slices(PP)); }
+size_t convnet_grad_count(int PP) {
+  return (size_t)convnet::NGRAD + (size_t)convnet::NCONV * convnet_cpart_pitch(PP);
+}
 
 size_t convnet_f1_lds(int PP) {
   const int KP = convnet::kpitch(PP);
@@ -738,17 +796,18 @@ hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   hipLaunchKernelGGL(f1_forward, dim3(NS), dim3(512), convnet_f1_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.pooled, b.code, b.slabs, B, PP, b.stamps);
-  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dh, b.hpart,
-                     B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
+                     b.cpart, b.pooled, b.code, b.slabs, B, PP, b.stamps);
+  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.cpart, b.slabs, b.dh,
+                     b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
   hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
                      b.pooled, b.code, b.dh, b.hpart, b.cpart, B, PP,
                      b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   return hipGetLastError();
 }
 
-hipError_t convnet_launch_flush(const ConvNetBuffers& b, hipStream_t st) {
-  hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.ctrl);
+hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st) {
+  hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.ctrl, b.cpart,
+                     convnet_cpart_pitch(PP));
   return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 REC = 716
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
-C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP = range(14)
+C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3 = range(16)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -90,7 +90,10 @@ class FusedConvNetEngine(Engine):
         NSP = C.convnet_cpart_pitch(self.PP)
         f32 = dict(dtype=torch.float32, device=dev)
         self.P = torch.zeros(NGRAD, **f32)
-        self.G = torch.zeros(NGRAD, **f32)
+        # one all-reduced buffer: flat gradient (+ metric tail) followed by the per-slice
+        # conv-gradient partials cpart[320][NSP]
+        self.gbuf = torch.zeros(C.convnet_grad_count(self.PP), **f32)
+        self.G = self.gbuf[:NGRAD]
         self.V = torch.zeros(NGRAD, **f32)
         self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
         self.pooled = torch.zeros(B, FEAT, dtype=torch.bfloat16, device=dev)
@@ -98,7 +101,7 @@ class FusedConvNetEngine(Engine):
         self.slabs = torch.zeros(NS, B, HID, **f32)
         self.dh = torch.zeros(B, HID, **f32)
         self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
-        self.cpart = torch.zeros(NCONV, NSP, **f32)
+        self.cpart = self.gbuf[NGRAD:].view(NCONV, NSP)
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
         off = 0

@@ -7,6 +7,7 @@ import os
 import statistics
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["DAMD_STAMPS"] = "1"
 os.environ.setdefault("DAMD_GRAPH", "0")
 import numpy as np  # noqa: E402

@@ -29,8 +29,17 @@ def _data(n=512, seed=0):
     return x, y
 
 
-def _ref_step(ws, xb, yb, gcount):
-    """fp32 torch reference: returns (grads list, loss_sum, correct)."""
+def _bf16(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+def _ref_step(ws, xb, yb, gcount, quant=False):
+    """fp64 torch reference of one step: returns (grads, loss_sum, correct).
+
+    ``quant=True`` mirrors the kernels' deliberate bf16 quantisation points (the pooled
+    activations and W1 enter the dense-1 MFMAs as bf16, with straight-through
+    gradients), so what remains is accumulation-order noise; ``quant=False`` is the
+    plain fp64 model."""
     from distributed_amd.ops import reference as R
 
     ts = [torch.tensor(w, dtype=torch.float64, requires_grad=True) for w in ws]
@@ -38,12 +47,16 @@ def _ref_step(ws, xb, yb, gcount):
     h = torch.relu(R.conv2d(x, ts[0], ts[1]))
     p = R.maxpool2d(h)
     f = p.reshape(p.shape[0], -1)
-    d = torch.relu(f @ ts[2] + ts[3])
+    w1 = ts[2]
+    if quant:
+        f = f + (_bf16(f) - f).detach()
+        w1 = w1 + (_bf16(w1) - w1).detach()
+    d = torch.relu(f @ w1 + ts[3])
     z = d @ ts[4] + ts[5]
     ls = torch.nn.functional.cross_entropy(z, torch.tensor(yb), reduction="none")
     (ls.sum() / gcount).backward()
     corr = float((z.argmax(-1) == torch.tensor(yb)).sum())
-    return [t.grad.numpy() for t in ts], float(ls.sum()), corr
+    return [t.grad.numpy() for t in ts], float(ls.detach().sum()), corr
 
 
 def _engine(model, B):
@@ -69,11 +82,25 @@ def test_one_step_matches_reference(B, monkeypatch):
     met = eng.end_epoch()
     eng.finish()
     w1 = m.get_weights()
-    grads, lsum, corr = _ref_step(w0, x[:B], y[:B], B)
-    for a, b, g, name in zip(w0, w1, grads, ["wc", "bc", "w1", "b1", "w2", "b2"]):
-        est = (a - b) / lr
-        err = np.linalg.norm(est - g) / (np.linalg.norm(g) + 1e-12)
-        assert err < 3e-2, f"{name}: rel err {err:.3e}"
+    names = ["wc", "bc", "w1", "b1", "w2", "b2"]
+
+    def rel_errs(grads):
+        out = {}
+        for a, b, g, name in zip(w0, w1, grads, names):
+            est = (a - b) / lr
+            out[name] = float(np.linalg.norm(est - g) / (np.linalg.norm(g) + 1e-12))
+        return out
+
+    # (1) vs a reference with the same bf16 quantisation points: the kernels' math
+    gq, lsum, corr = _ref_step(w0, x[:B], y[:B], B, quant=True)
+    eq = rel_errs(gq)
+    print("vs bf16-mirrored reference:", {k: f"{v:.2e}" for k, v in eq.items()})
+    assert max(eq.values()) < 5e-3, eq
+    # (2) vs plain fp64: the cost of bf16 dense compute (documented tolerance)
+    g64, _, _ = _ref_step(w0, x[:B], y[:B], B, quant=False)
+    e64 = rel_errs(g64)
+    print("vs fp64 reference:", {k: f"{v:.2e}" for k, v in e64.items()})
+    assert max(e64.values()) < 1e-1, e64
     assert abs(met["loss"] - lsum / B) < 2e-2
     assert abs(met["accuracy"] - corr / B) < 1.5 / B
 
