@@ -41,7 +41,6 @@ class ConvNetTrainer : public StepExecutor {
     b_.X = nullptr; b_.labels = nullptr;
     b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
     b_.ctrl = P_<Ctrl>(g("ctrl"));
-    b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
     b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
     b_.hpart = P_<float>(g("hpart")); b_.cpart = P_<float>(g("cpart"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;

@@ -10,7 +10,7 @@ struct Ctrl;
 struct ConvNetBuffers {
   const float* X; const int* labels;
   float* P; float* G; float* V; Ctrl* ctrl;
-  uint16_t* pooled; uint8_t* code; float* slabs; float* dh; float* hpart; float* cpart;
+  float* slabs; float* dh; float* hpart; float* cpart;
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
 };
 constexpr int kConvNetNParam = 347146;

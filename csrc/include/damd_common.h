@@ -94,11 +94,18 @@ __device__ __forceinline__ bool last_arriver(int* counter, int nblocks, int* fla
   return *flag != 0;
 }
 
-// Diagnostic phase stamps (s_memrealtime, 100 MHz): thread 0 of each block writes
-// st[block * 16 + idx].  `st` is null unless DAMD_STAMPS is set on the host, so the
-// production path pays one uniform scalar branch per stamp point.
-__device__ __forceinline__ void stamp(unsigned long long* st, int idx) {
-  if (st != nullptr && threadIdx.x == 0) st[blockIdx.x * 16 + idx] = __builtin_amdgcn_s_memrealtime();
+// Diagnostic phase stamps (s_memrealtime, 100 MHz).  Stamps are kept in registers
+// and written once at kernel end (a mid-kernel store makes hipcc wait vmcnt(0) and
+// distorts what it measures).  `st` is null unless DAMD_STAMPS is set on the host.
+struct Stamps {
+  unsigned long long t[8];
+};
+__device__ __forceinline__ void stamp(Stamps& s, unsigned long long* st, int idx) {
+  if (st != nullptr) s.t[idx] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void stamp_flush(const Stamps& s, unsigned long long* st, int n) {
+  if (st != nullptr && threadIdx.x == 0)
+    for (int i = 0; i < n; ++i) st[blockIdx.x * 16 + i] = s.t[i];
 }
 
 }  // namespace damd

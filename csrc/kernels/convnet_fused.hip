@@ -134,17 +134,98 @@ __device__ __forceinline__ void x_store(const XStage& st, float* xs, int nrows) 
   }
 }
 
+// ---- conv 3x3 + bias + ReLU + 2x2 max-pool of a slice on MFMA (shared by F1 and F3) ----
+// One 16x16x32 bf16 MFMA per tile with a split-precision K packing:
+//   k in [0,9): x_hi*w_hi   [9,18): x_lo*w_hi   [18,27): x_hi*w_lo   [27,32): 0
+// (x = hi + lo, w = hi + lo in bf16) -> ~16-bit-mantissa conv outputs, so the pool
+// argmax / ReLU mask match an fp32 conv; the 23 spare K slots of a 9-tap conv pay it.
+// Row tile rt = 4 pool windows x 4 sub-pixels (window wi = pl*64 + image), so the 4
+// pixels of one window are the 4 accumulator rows of one lane: bias + ReLU + max +
+// first-max argmax happen in registers.  Per-lane tap offsets / bit masks make the
+// hi/lo selection branch-free (a ?: on the value turns into divergent control flow that
+// serialises the LDS reads).
+struct ConvFrag {
+  bf16x8 w[2];
+  float bias[2];
+  int toff[8];
+  uint32_t lomask[8], zmask[8];
+};
+__device__ __forceinline__ void conv_setup(ConvFrag& f, const float* cw, int lane) {
+  const int kg = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
+    f.toff[j] = (tap / 3) * IMG + (tap % 3);
+    f.lomask[j] = part == 1 ? 0xffffu : 0u;
+    f.zmask[j] = k >= 27 ? 0u : 0xffffu;
+  }
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    s16x8 t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
+      const float w32 = cw[min(tap, 8) * NF + 16 * nt + (lane & 15)];
+      const uint32_t hi = f2bf(w32), lo = bf16_lo(w32, (uint16_t)hi);
+      const uint32_t wlomask = part == 2 ? 0xffffu : 0u;
+      t[j] = (short)((hi ^ ((hi ^ lo) & wlomask)) & f.zmask[j]);
+    }
+    f.w[nt] = __builtin_bit_cast(bf16x8, t);
+    f.bias[nt] = cw[OFF_BC + 16 * nt + (lane & 15)];
+  }
+}
+// emit(image, pl, channel, pooled_bf16, code) for every pooled output of the slice
+template <class Emit>
+__device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, int p0, int np, int r0, int wave,
+                                          int lane, Emit&& emit) {
+  const int nrt = 16 * np;
+  for (int rt = wave; rt < nrt; rt += 8) {
+    s16x8 at;
+    {
+      const int r = lane & 15, wi = 4 * rt + (r >> 2), sub = r & 3;
+      const int pl = wi >> 6, b = wi & 63, pos = p0 + pl, py = pos / PO, px = pos - py * PO;
+      const float* base = xs + (b * XR + 2 * py - r0 + (sub >> 1)) * IMG + 2 * px + (sub & 1);
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = base[f.toff[j]];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t hi = f2bf(v[j]), lo = bf16_lo(v[j], (uint16_t)hi);
+        at[j] = (short)((hi ^ ((hi ^ lo) & f.lomask[j])) & f.zmask[j]);
+      }
+    }
+    const bf16x8 a = __builtin_bit_cast(bf16x8, at);
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 c0 = mfma16(a, f.w[0], zero);
+    const f32x4 c1 = mfma16(a, f.w[1], zero);
+    const int wo = 4 * rt + (lane >> 4), plo = wo >> 6, bo = wo & 63;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const f32x4 cc = nt ? c1 : c0;
+      float best = fmaxf(cc[0] + f.bias[nt], 0.f);
+      int arg = 0;
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        const float v = fmaxf(cc[j] + f.bias[nt], 0.f);
+        arg = v > best ? j : arg;
+        best = fmaxf(best, v);
+      }
+      emit(bo, plo, 16 * nt + (lane & 15), f2bf(best), (uint8_t)(arg | (best > 0.f ? 4 : 0)));
+    }
+  }
+}
+
 // =================================================================================
 // F1
 // =================================================================================
 __global__ __launch_bounds__(512) void f1_forward(
     const float* __restrict__ X, float* __restrict__ P, const float* __restrict__ G,
     float* __restrict__ V, Ctrl* __restrict__ ctrl, const float* __restrict__ cpart,
-    uint16_t* __restrict__ pooled, uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP,
-    unsigned long long* st) {
+    float* __restrict__ slabs, int B, int PP, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  stamp(st, 0);
+  Stamps sts;
+  stamp(sts, st, 0);
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
   const int nsp4 = nsp(gridDim.x) / 4;
@@ -158,7 +239,7 @@ __global__ __launch_bounds__(512) void f1_forward(
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const bool mom = c.momentum != 0.f;
-  stamp(st, 1);
+  stamp(sts, st, 1);
 
   // ---- issue every independent load of the prologue ----
   XStage xst;
@@ -167,7 +248,8 @@ __global__ __launch_bounds__(512) void f1_forward(
   float4 wv[4], gv[4], vv[4];
   const float4* P4 = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID);
   const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
-  const float4* V4 = reinterpret_cast<const float4*>(V + OFF_W1 + p0 * 32 * HID);
+  // without momentum the velocity is never read: point its loads at P (cache hits)
+  const float4* V4 = reinterpret_cast<const float4*>((mom ? V : P) + OFF_W1 + p0 * 32 * HID);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int ic = min(tid + u * 512, n4 - 1);
@@ -205,44 +287,13 @@ __global__ __launch_bounds__(512) void f1_forward(
     sgd_update(cp, cg, cv, c.lr, c.momentum, c.nesterov, wn, vn);
     cw[tid] = wn;
   }
-  stamp(st, 2);
+  stamp(sts, st, 2);
   x_store(xst, xs, nrows);
   lds_barrier();
-  stamp(st, 3);
+  stamp(sts, st, 3);
 
-  // Conv as one 16x16x32 bf16 MFMA per tile with a split-precision K packing:
-  //   k in [0,9): x_hi*w_hi   [9,18): x_lo*w_hi   [18,27): x_hi*w_lo   [27,32): 0
-  // (x = hi + lo, w = hi + lo in bf16) -> ~16-bit-mantissa conv outputs, so the pool
-  // argmax / ReLU mask match an fp32 conv; the 23 spare K slots of a 9-tap conv pay it.
-  // Per-lane tap offsets and bit masks: branch-free selects (a ?: on the value becomes
-  // divergent control flow that serialises the LDS reads).
-  int toff[8];
-  uint32_t lomask[8], zmask[8];
-  const int kg = lane >> 4;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
-    toff[j] = (tap / 3) * IMG + (tap % 3);
-    lomask[j] = part == 1 ? 0xffffu : 0u;
-    zmask[j] = k >= 27 ? 0u : 0xffffu;
-  }
-  bf16x8 wfrag[2];
-  float bias[2];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    s16x8 t;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
-      const float w32 = cw[min(tap, 8) * NF + 16 * nt + (lane & 15)];
-      const uint32_t hi = f2bf(w32), lo = bf16_lo(w32, (uint16_t)hi);
-      const uint32_t wlomask = part == 2 ? 0xffffu : 0u;
-      t[j] = (short)((hi ^ ((hi ^ lo) & wlomask)) & zmask[j]);
-    }
-    wfrag[nt] = __builtin_bit_cast(bf16x8, t);
-    bias[nt] = cw[OFF_BC + 16 * nt + (lane & 15)];
-  }
-
+  ConvFrag cf;
+  conv_setup(cf, cw, lane);
   const int mt = wave & 3, nt0 = (wave >> 2) * 2;
   const int nchunks = (B + CH - 1) / CH;
   for (int chunk = 0; chunk < nchunks; ++chunk) {
@@ -252,52 +303,11 @@ __global__ __launch_bounds__(512) void f1_forward(
       x_store(xst, xs, nrows);
       lds_barrier();
     }
-    // ---- conv + bias + ReLU + 2x2 max-pool on MFMA ----
-    // row tile rt = 4 pool windows x 4 sub-pixels; window wi = pl*64 + image
-    const int nrt = 16 * np;
-    for (int rt = wave; rt < nrt; rt += 8) {
-      s16x8 at;
-      {
-        const int r = lane & 15, wi = 4 * rt + (r >> 2), sub = r & 3;
-        const int pl = wi >> 6, b = wi & 63, pos = p0 + pl, py = pos / PO, px = pos - py * PO;
-        const float* base = xs + (b * XR + 2 * py - r0 + (sub >> 1)) * IMG + 2 * px + (sub & 1);
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = base[toff[j]];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t hi = f2bf(v[j]), lo = bf16_lo(v[j], (uint16_t)hi);
-          at[j] = (short)((hi ^ ((hi ^ lo) & lomask[j])) & zmask[j]);
-        }
-      }
-      const bf16x8 a = __builtin_bit_cast(bf16x8, at);
-      const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-      const f32x4 c0 = mfma16(a, wfrag[0], zero);
-      const f32x4 c1 = mfma16(a, wfrag[1], zero);
-      const int wo = 4 * rt + (lane >> 4), plo = wo >> 6, bo = wo & 63, lb = chunk * CH + bo;
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const f32x4 cc = nt ? c1 : c0;
-        float best = fmaxf(cc[0] + bias[nt], 0.f);
-        int arg = 0;
-#pragma unroll
-        for (int j = 1; j < 4; ++j) {
-          const float v = fmaxf(cc[j] + bias[nt], 0.f);
-          arg = v > best ? j : arg;
-          best = fmaxf(best, v);
-        }
-        const int ch = 16 * nt + (lane & 15);
-        const uint16_t hb = f2bf(best);
-        as[bo * KP + plo * 32 + ch] = hb;
-        if (lb < B) {
-          const long o = (long)lb * FEAT + (p0 + plo) * NF + ch;
-          pooled[o] = hb;
-          code[o] = (uint8_t)(arg | (best > 0.f ? 4 : 0));
-        }
-      }
-    }
+    conv_pool(cf, xs, p0, np, r0, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t) {
+      as[bo * KP + plo * 32 + ch] = hb;
+    });
     lds_barrier();
-    stamp(st, 4);
+    stamp(sts, st, 4);
     // ---- dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n] ----
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     const int ar = 16 * mt + (lane & 15), ko = 8 * (lane >> 4);
@@ -319,7 +329,8 @@ __global__ __launch_bounds__(512) void f1_forward(
       }
     }
   }
-  stamp(st, 5);
+  stamp(sts, st, 5);
+  stamp_flush(sts, st, 6);
 }
 
 // =================================================================================
@@ -329,7 +340,8 @@ __global__ __launch_bounds__(256) void f2_head(
     const int* __restrict__ labels, float* __restrict__ P, const float* __restrict__ G, float* __restrict__ V,
     Ctrl* __restrict__ ctrl, const float* __restrict__ cpart, const float* __restrict__ slabs,
     float* __restrict__ dh, float* __restrict__ rec, int B, int NS, unsigned long long* st) {
-  stamp(st, 0);
+  Stamps sts;
+  stamp(sts, st, 0);
   __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 64 + 16];
   float* sp = lds;                 // updated b1[64], W2[640], b2[10]
   float* hw = sp + NSMALL + 2;     // [4][64] per-wave partial slab sums
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(256) void f2_head(
   }
   hw[w * 64 + l] = hsum;
   lds_barrier();
-  stamp(st, 1);
+  stamp(sts, st, 1);
   const float* b1n = sp;
   const float* w2n = sp + HID;
   const float* b2n = sp + HID + HID * NCLS;
@@ -457,7 +469,8 @@ __global__ __launch_bounds__(256) void f2_head(
     rec[(long)714 * B + b] = valid ? (lse - zy) : 0.f;
     rec[(long)715 * B + b] = (valid && am == y) ? 1.f : 0.f;
   }
-  stamp(st, 2);
+  stamp(sts, st, 2);
+  stamp_flush(sts, st, 3);
 }
 
 // =================================================================================
@@ -488,11 +501,11 @@ __device__ __forceinline__ float rec_sum(const float* __restrict__ rc, int q, in
 
 __global__ __launch_bounds__(512) void f3_backward(
     const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
-    Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
-    const float* __restrict__ dh, const float* __restrict__ rec, float* __restrict__ cpart, int B, int PP,
-    unsigned long long* st) {
+    Ctrl* __restrict__ ctrl, const float* __restrict__ dh, const float* __restrict__ rec,
+    float* __restrict__ cpart, int B, int PP, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  stamp(st, 0);
+  Stamps sts;
+  stamp(sts, st, 0);
   const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x, NSP = nsp(gridDim.x);
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KD = PP * 32 + 4;   // dps pitch (f32)
@@ -503,7 +516,8 @@ __global__ __launch_bounds__(512) void f3_backward(
   uint16_t* dht = pt + PP * 32 * HP;                                       // [2][HID][HP] hi, lo
   uint16_t* dhs = dht + 2 * HID * HP;                                      // [2][CH][HP]  hi, lo
   uint16_t* w1s = dhs + 2 * CH * HP;                                       // [PP*32][HP]
-  uint8_t* cs = reinterpret_cast<uint8_t*>(w1s + PP * 32 * HP);            // [CH][KC]
+  uint8_t* cs = reinterpret_cast<uint8_t*>(w1s + PP * 32 * HP);            // [CH][KC] argmax codes
+  float* cwl = reinterpret_cast<float*>(cs + CH * KC);                     // [320] conv params
   float* red = reinterpret_cast<float*>(pt);  // [16][320] reduction scratch, after the MFMAs
   const Ctrl c = *ctrl;
   if (s == 0 && tid == 0) {
@@ -543,31 +557,14 @@ __global__ __launch_bounds__(512) void f3_backward(
     wv[u] = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID)[min(tid + u * 512, n4 - 1)];
   XStage xst;
   float4 dv[2];
-  uint4 pv[2];
-  uint4 cv;
-  const int kq = K / 8;   // uint4 (8 bf16) per image row of the pooled slice
-  const int kc = K / 16;  // uint4 of code bytes per image
+  // conv parameters as written back by F2 of this step (== F1's register copy)
+  const float cpw = P[min(tid, NCONV - 1)];
   auto load_chunk = [&](int chunk) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {  // dh: 64x64 fp32 = 1024 float4
       const int i = tid + u * 512, bb = i >> 4, lb = chunk * CH + bb;
       const float4 v = reinterpret_cast<const float4*>(dh + (long)min(lb, B - 1) * HID)[i & 15];
       dv[u] = lb < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * 512, bb = i / kq, q = i - bb * kq, lb = chunk * CH + bb;
-      const bool ok = i < CH * kq && lb < B;
-      const uint4 v = *reinterpret_cast<const uint4*>(pooled + (long)min(lb, B - 1) * FEAT + p0 * NF +
-                                                      min(q, kq - 1) * 8);
-      pv[u] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-    }
-    {
-      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
-      const bool ok = i < CH * kc && lb < B;
-      const uint4 v = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF +
-                                                      min(q, kc - 1) * 16);
-      cv = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
     x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
   };
@@ -584,23 +581,6 @@ __global__ __launch_bounds__(512) void f3_backward(
         dht[(n + j) * HP + bb] = hi;
         dht[HID * HP + (n + j) * HP + bb] = lo;
       }
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * 512;
-      if (i < CH * kq) {
-        const int bb = i / kq, q = i - bb * kq;
-        const uint32_t w4[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pt[(q * 8 + 2 * j) * HP + bb] = (uint16_t)(w4[j] & 0xffff);
-          pt[(q * 8 + 2 * j + 1) * HP + bb] = (uint16_t)(w4[j] >> 16);
-        }
-      }
-    }
-    if (tid < CH * kc) {
-      const int bb = tid / kc, q = tid - bb * kc;
-      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
     }
     x_store(xst, xs, nrows);
   };
@@ -625,6 +605,7 @@ __global__ __launch_bounds__(512) void f3_backward(
 #pragma unroll
   for (int t = 0; t < 9; ++t) gw[t] = 0.f;
   const int nchunks = (B + CH - 1) / CH;
+  ConvFrag cf;
 
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     if (chunk) {
@@ -632,8 +613,18 @@ __global__ __launch_bounds__(512) void f3_backward(
       load_chunk(chunk);
     }
     store_chunk();
+    if (chunk == 0 && tid < NCONV) cwl[tid] = cpw;
     lds_barrier();
-    stamp(st, 1);
+    // recompute this slice's conv + ReLU + max-pool (cheaper than storing the pooled
+    // tile and argmax codes in F1 and re-reading them here): pooled -> pt [k][b] (the
+    // A operand of dW1), codes -> cs
+    if (chunk == 0) conv_setup(cf, cwl, lane);
+    conv_pool(cf, xs, p0, np, r0, wave, lane, [&](int bo, int plo, int chn, uint16_t hb, uint8_t cd) {
+      pt[(plo * 32 + chn) * HP + bo] = hb;
+      cs[bo * KC + plo * 32 + chn] = chunk * CH + bo < B ? cd : (uint8_t)0;
+    });
+    lds_barrier();
+    stamp(sts, st, 1);
     // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
 #pragma unroll
     for (int i = 0; i < MAXPP; ++i) {
@@ -669,7 +660,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
     lds_barrier();
-    stamp(st, 2);
+    stamp(sts, st, 2);
     // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
     // (branch-free: the gradient is masked, the reads always hit staged LDS rows)
 #pragma unroll
@@ -691,7 +682,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
   }
-  stamp(st, 3);
+  stamp(sts, st, 3);
   // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
@@ -736,7 +727,8 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
   }
-  stamp(st, 4);
+  stamp(sts, st, 4);
+  stamp_flush(sts, st, 5);
 }
 
 // =================================================================================
@@ -789,18 +781,18 @@ size_t convnet_f3_lds(int PP) {
   using namespace convnet;
   const int KD = PP * 32 + 4;
   return XS_BYTES + (size_t)CH * KD * 4 + (size_t)PP * 32 * HP * 2 * 2 + (size_t)2 * (HID + CH) * HP * 2 +
-         (size_t)CH * PP * 32 + 16;
+         (size_t)CH * PP * 32 + NCONV * 4 + 16;
 }
 
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   hipLaunchKernelGGL(f1_forward, dim3(NS), dim3(512), convnet_f1_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.cpart, b.pooled, b.code, b.slabs, B, PP, b.stamps);
+                     b.cpart, b.slabs, B, PP, b.stamps);
   hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.cpart, b.slabs, b.dh,
                      b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
   hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.pooled, b.code, b.dh, b.hpart, b.cpart, B, PP,
+                     b.dh, b.hpart, b.cpart, B, PP,
                      b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   return hipGetLastError();
 }

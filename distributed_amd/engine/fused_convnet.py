@@ -96,8 +96,6 @@ class FusedConvNetEngine(Engine):
         self.G = self.gbuf[:NGRAD]
         self.V = torch.zeros(NGRAD, **f32)
         self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
-        self.pooled = torch.zeros(B, FEAT, dtype=torch.bfloat16, device=dev)
-        self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
         self.slabs = torch.zeros(NS, B, HID, **f32)
         self.dh = torch.zeros(B, HID, **f32)
         self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
@@ -122,7 +120,7 @@ class FusedConvNetEngine(Engine):
         self._write_hparams()
         torch.cuda.synchronize(dev)
         bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
-                    ctrl=self.ctrl.data_ptr(), pooled=self.pooled.data_ptr(), code=self.code.data_ptr(),
+                    ctrl=self.ctrl.data_ptr(),
                     slabs=self.slabs.data_ptr(), dh=self.dh.data_ptr(), hpart=self.hpart.data_ptr(),
                     cpart=self.cpart.data_ptr())
         self.stamps = None

@@ -139,7 +139,7 @@ def test_momentum_three_steps(monkeypatch):
     eng.end_epoch()
     eng.finish()
     for s in range(3):
-        g, _, _ = _ref_step(w, x[s * 64:(s + 1) * 64], y[s * 64:(s + 1) * 64], 64)
+        g, _, _ = _ref_step(w, x[s * 64:(s + 1) * 64], y[s * 64:(s + 1) * 64], 64, quant=True)
         for i in range(6):
             v[i] = mom * v[i] - lr * g[i]
             w[i] = w[i] + mom * v[i] - lr * g[i]
