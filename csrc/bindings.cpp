@@ -78,7 +78,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("convnet_num_slices", &convnet_num_slices);
   m.def("convnet_cpart_pitch", &convnet_cpart_pitch);
   m.def("convnet_grad_count", &convnet_grad_count);
-  m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP), convnet_f3_lds(PP)); });
+  m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP, 4), convnet_f1_lds(PP, 6), convnet_f3_lds(PP)); });
 
   m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) n = 0; return n; });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });

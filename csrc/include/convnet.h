@@ -18,7 +18,8 @@ constexpr int kConvNetNGrad = 347152;
 constexpr int kConvNetRec = 716;  // F2 record columns (hpart is [kConvNetRec][B])
 int convnet_num_slices(int PP);
 int convnet_cpart_pitch(int PP);  // cpart is [320][pitch]
-size_t convnet_f1_lds(int PP);
+int convnet_f1_lg(int B);
+size_t convnet_f1_lds(int PP, int lg);
 size_t convnet_f3_lds(int PP);
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st);

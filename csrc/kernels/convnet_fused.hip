@@ -107,23 +107,23 @@ __device__ __forceinline__ float cpart_row_sum(const float* __restrict__ row, in
 struct XStage {
   float4 v[6];
 };
+// rows [r0, r0+nrows) of images b < nimg (valid if b < nvalid and row_base+b < nsamples)
 __device__ __forceinline__ void x_load(XStage& st, const float* __restrict__ X, long row_base, int nsamples,
-                                       int B, int chunk, int r0, int nrows) {
-  const int per_img = nrows * 7, total = CH * per_img;
+                                       int nvalid, int nimg, int r0, int nrows) {
+  const int per_img = nrows * 7, total = nimg * per_img;
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
     const int i = min((int)threadIdx.x + u * 512, total - 1);
     const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-    const int lb = chunk * CH + b;
-    const long g = row_base + lb;
-    const bool ok = ((int)threadIdx.x + u * 512 < total) && lb < B && g < nsamples;
+    const long g = row_base + b;
+    const bool ok = ((int)threadIdx.x + u * 512 < total) && b < nvalid && g < nsamples;
     const long gs = max(0L, min(g, (long)nsamples - 1));
     const float4 v = reinterpret_cast<const float4*>(X + gs * NPIX + (r0 + r) * IMG)[q];
     st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
-__device__ __forceinline__ void x_store(const XStage& st, float* xs, int nrows) {
-  const int per_img = nrows * 7, total = CH * per_img;
+__device__ __forceinline__ void x_store(const XStage& st, float* xs, int nimg, int nrows) {
+  const int per_img = nrows * 7, total = nimg * per_img;
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
     const int i = threadIdx.x + u * 512;
@@ -176,14 +176,14 @@ __device__ __forceinline__ void conv_setup(ConvFrag& f, const float* cw, int lan
 }
 // emit(image, pl, channel, pooled_bf16, code) for every pooled output of the slice
 template <class Emit>
-__device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, int p0, int np, int r0, int wave,
-                                          int lane, Emit&& emit) {
-  const int nrt = 16 * np;
+__device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, int p0, int np, int r0, int lg,
+                                          int wave, int lane, Emit&& emit) {
+  const int nrt = (np << lg) >> 2;  // np positions x 2^lg images / 4 windows per tile
   for (int rt = wave; rt < nrt; rt += 8) {
     s16x8 at;
     {
       const int r = lane & 15, wi = 4 * rt + (r >> 2), sub = r & 3;
-      const int pl = wi >> 6, b = wi & 63, pos = p0 + pl, py = pos / PO, px = pos - py * PO;
+      const int pl = wi >> lg, b = wi & ((1 << lg) - 1), pos = p0 + pl, py = pos / PO, px = pos - py * PO;
       const float* base = xs + (b * XR + 2 * py - r0 + (sub >> 1)) * IMG + 2 * px + (sub & 1);
       float v[8];
 #pragma unroll
@@ -198,7 +198,7 @@ __device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, in
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     const f32x4 c0 = mfma16(a, f.w[0], zero);
     const f32x4 c1 = mfma16(a, f.w[1], zero);
-    const int wo = 4 * rt + (lane >> 4), plo = wo >> 6, bo = wo & 63;
+    const int wo = 4 * rt + (lane >> 4), plo = wo >> lg, bo = wo & ((1 << lg) - 1);
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
       const f32x4 cc = nt ? c1 : c0;
@@ -216,26 +216,27 @@ __device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, in
 }
 
 // =================================================================================
-// F1
+// F1: grid (NS slices, ISPLIT image groups of IB = 2^lg images)
 // =================================================================================
 __global__ __launch_bounds__(512) void f1_forward(
-    const float* __restrict__ X, float* __restrict__ P, const float* __restrict__ G,
-    float* __restrict__ V, Ctrl* __restrict__ ctrl, const float* __restrict__ cpart,
-    float* __restrict__ slabs, int B, int PP, unsigned long long* st) {
+    const float* __restrict__ X, const float* __restrict__ P, const float* __restrict__ G,
+    const float* __restrict__ V, Ctrl* __restrict__ ctrl, const float* __restrict__ cpart,
+    float* __restrict__ slabs, int B, int PP, int lg, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   Stamps sts;
   stamp(sts, st, 0);
+  const int IB = 1 << lg, img0 = blockIdx.y * IB;
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
   const int nsp4 = nsp(gridDim.x) / 4;
-  float* xs = reinterpret_cast<float*>(smem);
-  uint16_t* as = reinterpret_cast<uint16_t*>(smem + XS_BYTES);   // [CH][KP] pooled tile
-  uint16_t* w1t = as + CH * KP;                                    // [HID][KP] W1 slice^T
-  float* cw = reinterpret_cast<float*>(w1t + HID * KP);            // [320] conv params
+  float* xs = reinterpret_cast<float*>(smem);                              // [IB][XR][28]
+  uint16_t* as = reinterpret_cast<uint16_t*>(smem + IB * XR * IMG * 4);    // [IB][KP] pooled tile
+  uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
+  float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
   const Ctrl c = *ctrl;
-  if (s == 0 && tid == 0) ctrl->cur2 = c.cursor;
-  const long row_base = (long)c.cursor * c.global_batch + c.row0;
+  if (s == 0 && blockIdx.y == 0 && tid == 0) ctrl->cur2 = c.cursor;
+  const long row_base = (long)c.cursor * c.global_batch + c.row0 + img0;
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const bool mom = c.momentum != 0.f;
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(512) void f1_forward(
 
   // ---- issue every independent load of the prologue ----
   XStage xst;
-  x_load(xst, X, row_base, c.nsamples, B, 0, r0, nrows);
+  x_load(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
   const int n4 = K * HID / 4;  // <= 2048
   float4 wv[4], gv[4], vv[4];
   const float4* P4 = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID);
@@ -261,9 +262,8 @@ __global__ __launch_bounds__(512) void f1_forward(
   const float cp = P[tcl], cv = V[tcl];
   const float cg = cpart_row_sum(cpart + (long)tcl * nsp4 * 4, nsp4);
 
-  // ---- pending SGD update: W1 rows of this slice (owner block) + conv (registers) ----
-  float4* P4w = reinterpret_cast<float4*>(P + OFF_W1 + p0 * 32 * HID);
-  float4* V4w = reinterpret_cast<float4*>(V + OFF_W1 + p0 * 32 * HID);
+  // ---- pending SGD update of the W1 slice and of the conv weights, in registers only:
+  //      the write-backs happen in F3 (W1 rows, slice owner) and F2 (conv) ----
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = tid + u * 512;
@@ -273,8 +273,6 @@ __global__ __launch_bounds__(512) void f1_forward(
       sgd_update(wv[u].y, gv[u].y, vv[u].y, c.lr, c.momentum, c.nesterov, wn.y, vn.y);
       sgd_update(wv[u].z, gv[u].z, vv[u].z, c.lr, c.momentum, c.nesterov, wn.z, vn.z);
       sgd_update(wv[u].w, gv[u].w, vv[u].w, c.lr, c.momentum, c.nesterov, wn.w, vn.w);
-      P4w[i] = wn;
-      if (mom) V4w[i] = vn;
       const int e = i * 4, kr = e >> 6, n = e & 63;
       w1t[(n + 0) * KP + kr] = f2bf(wn.x);
       w1t[(n + 1) * KP + kr] = f2bf(wn.y);
@@ -288,45 +286,33 @@ __global__ __launch_bounds__(512) void f1_forward(
     cw[tid] = wn;
   }
   stamp(sts, st, 2);
-  x_store(xst, xs, nrows);
+  x_store(xst, xs, IB, nrows);
   lds_barrier();
   stamp(sts, st, 3);
 
   ConvFrag cf;
   conv_setup(cf, cw, lane);
-  const int mt = wave & 3, nt0 = (wave >> 2) * 2;
-  const int nchunks = (B + CH - 1) / CH;
-  for (int chunk = 0; chunk < nchunks; ++chunk) {
-    if (chunk) {
-      lds_barrier();
-      x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
-      x_store(xst, xs, nrows);
-      lds_barrier();
-    }
-    conv_pool(cf, xs, p0, np, r0, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t) {
-      as[bo * KP + plo * 32 + ch] = hb;
-    });
-    lds_barrier();
-    stamp(sts, st, 4);
-    // ---- dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n] ----
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const int ar = 16 * mt + (lane & 15), ko = 8 * (lane >> 4);
-    const int bn0 = 16 * nt0 + (lane & 15), bn1 = bn0 + 16;
+  conv_pool(cf, xs, p0, np, r0, lg, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t) {
+    as[bo * KP + plo * 32 + ch] = hb;
+  });
+  lds_barrier();
+  stamp(sts, st, 4);
+  // ---- dense-1 split-K partial: slab[s][row][n] = sum_k pooled[row][k] * W1[k][n] ----
+  const int ko = 8 * (lane >> 4);
+  const int ntiles = (IB >> 4) * 4;  // (row tile, col tile) pairs
+  for (int t = wave; t < ntiles; t += 8) {
+    const int mt = t >> 2, nt = t & 3;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ar = 16 * mt + (lane & 15), bn = 16 * nt + (lane & 15);
     for (int ks = 0; ks < np; ++ks) {
       const bf16x8 a = ld_frag(as + ar * KP + ks * 32 + ko);
-      const bf16x8 b0 = ld_frag(w1t + bn0 * KP + ks * 32 + ko);
-      const bf16x8 b1 = ld_frag(w1t + bn1 * KP + ks * 32 + ko);
-      acc0 = mfma16(a, b0, acc0);
-      acc1 = mfma16(a, b1, acc1);
+      const bf16x8 bb = ld_frag(w1t + bn * KP + ks * 32 + ko);
+      acc = mfma16(a, bb, acc);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int row = 16 * mt + 4 * (lane >> 4) + j, lb = chunk * CH + row;
-      if (lb < B) {
-        float* dst = slabs + ((long)s * B + lb) * HID;
-        dst[bn0] = acc0[j];
-        dst[bn1] = acc1[j];
-      }
+      const int row = 16 * mt + 4 * (lane >> 4) + j, lb = img0 + row;
+      if (lb < B) slabs[((long)s * B + lb) * HID + bn] = acc[j];
     }
   }
   stamp(sts, st, 5);
@@ -550,11 +536,23 @@ __global__ __launch_bounds__(512) void f3_backward(
   }
 
   // ---- prologue loads: W1 slice, dh, pooled slice, code slice, input rows ----
+  // W1 slice: this block owns these rows -> apply their pending update (the same
+  // arithmetic F1 did in registers), write it back, and use it for dP
   const int n4 = K * HID / 4;
-  float4 wv[4];
+  const bool mom = c.momentum != 0.f;
+  float4 wv[4], gv1[4], vv1[4];
+  {
+    const float4* P4 = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID);
+    const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
+    const float4* V4 = reinterpret_cast<const float4*>((mom ? V : P) + OFF_W1 + p0 * 32 * HID);
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    wv[u] = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID)[min(tid + u * 512, n4 - 1)];
+    for (int u = 0; u < 4; ++u) {
+      const int ic = min(tid + u * 512, n4 - 1);
+      wv[u] = P4[ic];
+      gv1[u] = G4[ic];
+      vv1[u] = V4[ic];
+    }
+  }
   XStage xst;
   float4 dv[2];
   // conv parameters as written back by F2 of this step (== F1's register copy)
@@ -566,7 +564,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       const float4 v = reinterpret_cast<const float4*>(dh + (long)min(lb, B - 1) * HID)[i & 15];
       dv[u] = lb < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    x_load(xst, X, row_base, c.nsamples, B, chunk, r0, nrows);
+    x_load(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
   };
   auto store_chunk = [&]() {
 #pragma unroll
@@ -582,17 +580,28 @@ __global__ __launch_bounds__(512) void f3_backward(
         dht[HID * HP + (n + j) * HP + bb] = lo;
       }
     }
-    x_store(xst, xs, nrows);
+    x_store(xst, xs, CH, nrows);
   };
   load_chunk(0);
+  {
+    float4* P4w = reinterpret_cast<float4*>(P + OFF_W1 + p0 * 32 * HID);
+    float4* V4w = reinterpret_cast<float4*>(V + OFF_W1 + p0 * 32 * HID);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int i = tid + u * 512;
-    if (i < n4) {
-      const int e = i * 4, kr = e >> 6, n = e & 63;
-      uint2 pk = make_uint2((uint32_t)f2bf(wv[u].x) | ((uint32_t)f2bf(wv[u].y) << 16),
-                            (uint32_t)f2bf(wv[u].z) | ((uint32_t)f2bf(wv[u].w) << 16));
-      *reinterpret_cast<uint2*>(w1s + kr * HP + n) = pk;
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + u * 512;
+      if (i < n4) {
+        float4 wn, vn;
+        sgd_update(wv[u].x, gv1[u].x, vv1[u].x, c.lr, c.momentum, c.nesterov, wn.x, vn.x);
+        sgd_update(wv[u].y, gv1[u].y, vv1[u].y, c.lr, c.momentum, c.nesterov, wn.y, vn.y);
+        sgd_update(wv[u].z, gv1[u].z, vv1[u].z, c.lr, c.momentum, c.nesterov, wn.z, vn.z);
+        sgd_update(wv[u].w, gv1[u].w, vv1[u].w, c.lr, c.momentum, c.nesterov, wn.w, vn.w);
+        P4w[i] = wn;
+        if (mom) V4w[i] = vn;
+        const int e = i * 4, kr = e >> 6, n = e & 63;
+        uint2 pk = make_uint2((uint32_t)f2bf(wn.x) | ((uint32_t)f2bf(wn.y) << 16),
+                              (uint32_t)f2bf(wn.z) | ((uint32_t)f2bf(wn.w) << 16));
+        *reinterpret_cast<uint2*>(w1s + kr * HP + n) = pk;
+      }
     }
   }
 
@@ -615,16 +624,17 @@ __global__ __launch_bounds__(512) void f3_backward(
     store_chunk();
     if (chunk == 0 && tid < NCONV) cwl[tid] = cpw;
     lds_barrier();
+    stamp(sts, st, 1);
     // recompute this slice's conv + ReLU + max-pool (cheaper than storing the pooled
     // tile and argmax codes in F1 and re-reading them here): pooled -> pt [k][b] (the
     // A operand of dW1), codes -> cs
     if (chunk == 0) conv_setup(cf, cwl, lane);
-    conv_pool(cf, xs, p0, np, r0, wave, lane, [&](int bo, int plo, int chn, uint16_t hb, uint8_t cd) {
+    conv_pool(cf, xs, p0, np, r0, 6, wave, lane, [&](int bo, int plo, int chn, uint16_t hb, uint8_t cd) {
       pt[(plo * 32 + chn) * HP + bo] = hb;
       cs[bo * KC + plo * 32 + chn] = chunk * CH + bo < B ? cd : (uint8_t)0;
     });
     lds_barrier();
-    stamp(sts, st, 1);
+    stamp(sts, st, 2);
     // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
 #pragma unroll
     for (int i = 0; i < MAXPP; ++i) {
@@ -660,7 +670,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
     lds_barrier();
-    stamp(sts, st, 2);
+    stamp(sts, st, 3);
     // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
     // (branch-free: the gradient is masked, the reads always hit staged LDS rows)
 #pragma unroll
@@ -682,7 +692,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
   }
-  stamp(sts, st, 3);
+  stamp(sts, st, 4);
   // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
@@ -727,8 +737,8 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
   }
-  stamp(sts, st, 4);
-  stamp_flush(sts, st, 5);
+  stamp(sts, st, 5);
+  stamp_flush(sts, st, 6);
 }
 
 // =================================================================================
@@ -773,9 +783,13 @@ size_t convnet_grad_count(int PP) {
   return (size_t)convnet::NGRAD + (size_t)convnet::NCONV * convnet_cpart_pitch(PP);
 }
 
-size_t convnet_f1_lds(int PP) {
-  const int KP = convnet::kpitch(PP);
-  return convnet::XS_BYTES + (size_t)(convnet::CH + convnet::HID) * KP * 2 + convnet::NCONV * 4;
+// F1 images per block = 2^lg: 16 up to B = 256 (more blocks, shorter per-block chains),
+// 64 beyond (bounded replication of the W1-slice / conv-partial loads)
+int convnet_f1_lg(int B) { return B <= 256 ? 4 : 6; }
+size_t convnet_f1_lds(int PP, int lg) {
+  using namespace convnet;
+  const int KP = kpitch(PP), IB = 1 << lg;
+  return (size_t)IB * XR * IMG * 4 + (size_t)(IB + HID) * KP * 2 + NCONV * 4;
 }
 size_t convnet_f3_lds(int PP) {
   using namespace convnet;
@@ -787,8 +801,9 @@ size_t convnet_f3_lds(int PP) {
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
-  hipLaunchKernelGGL(f1_forward, dim3(NS), dim3(512), convnet_f1_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.cpart, b.slabs, B, PP, b.stamps);
+  const int lg = convnet_f1_lg(B);
+  hipLaunchKernelGGL(f1_forward, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st, b.X,
+                     b.P, b.G, b.V, b.ctrl, b.cpart, b.slabs, B, PP, lg, b.stamps);
   hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.cpart, b.slabs, b.dh,
                      b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
   hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
