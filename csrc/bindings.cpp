@@ -42,10 +42,9 @@ class ConvNetTrainer : public StepExecutor {
     b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
     b_.ctrl = P_<Ctrl>(g("ctrl"));
     b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
-    b_.hpart = P_<float>(g("hpart")); b_.cpart = P_<float>(g("cpart"));
+    b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
+    b_.hpart = P_<float>(g("hpart"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
-    if (b_.cpart != b_.G + kConvNetNGrad)
-      throw std::invalid_argument("cpart must directly follow the gradient buffer (one all-reduce)");
     HIP_CHECK(convnet_set_lds_limits());
   }
   // X [n][784] fp32 and labels [n] int32: epoch-permuted copies (stable pointers).
@@ -76,7 +75,6 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
   m.attr("CONVNET_REC") = kConvNetRec;
   m.def("convnet_num_slices", &convnet_num_slices);
-  m.def("convnet_cpart_pitch", &convnet_cpart_pitch);
   m.def("convnet_grad_count", &convnet_grad_count);
   m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP, 4), convnet_f1_lds(PP, 6), convnet_f3_lds(PP)); });
 

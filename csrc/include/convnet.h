@@ -5,25 +5,23 @@
 
 namespace damd {
 struct Ctrl;
-// cpart must directly follow G in memory (one all-reduce covers both).
 // X / labels are the epoch-permuted copies of the dataset (row g = global sample g).
 struct ConvNetBuffers {
   const float* X; const int* labels;
   float* P; float* G; float* V; Ctrl* ctrl;
-  float* slabs; float* dh; float* hpart; float* cpart;
+  uint16_t* pooled; uint8_t* code; float* slabs; float* dh; float* hpart;
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
 };
 constexpr int kConvNetNParam = 347146;
 constexpr int kConvNetNGrad = 347152;
 constexpr int kConvNetRec = 716;  // F2 record columns (hpart is [kConvNetRec][B])
 int convnet_num_slices(int PP);
-int convnet_cpart_pitch(int PP);  // cpart is [320][pitch]
 int convnet_f1_lg(int B);
 size_t convnet_f1_lds(int PP, int lg);
 size_t convnet_f3_lds(int PP);
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st);
-// elements of the all-reduced gradient buffer: G[kConvNetNGrad] followed by cpart[320][pitch]
+// elements of the all-reduced gradient buffer
 size_t convnet_grad_count(int PP);
 hipError_t convnet_set_lds_limits();
 }  // namespace damd

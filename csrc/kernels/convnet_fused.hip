@@ -18,7 +18,7 @@
 //
 //   F1 (grid NS slices of PP pooled positions, 512 thr): pending SGD update of this
 //       slice's W1 rows (owned by exactly one block) and of the conv weights (in
-//       registers; their gradient = sum of F3's per-slice partials), conv on MFMA
+//       registers), conv on MFMA
 //       (16x16x32 bf16 with a split-precision K packing): the 4 pixels of one 2x2 pool
 //       window are the 4 accumulator rows of one lane, so bias+ReLU+max+argmax happen
 //       in registers; the pooled tile stays in LDS and is multiplied by the W1 K-slice
@@ -29,8 +29,8 @@
 //       write-back of the conv parameters' pending update (spread over blocks).
 //   F3 (grid NS, 512 thr): dW1 = P^T dh (MFMA, straight into the gradient buffer),
 //       dP = dh W1^T (MFMA into LDS), MaxPool/ReLU backward through the stored argmax
-//       code, this slice's conv weight/bias gradient partial (a column of `cpart`,
-//       which is all-reduced with the gradient buffer); every block also applies the
+//       code, this slice's conv weight/bias gradient partial (atomically added into
+//       the gradient buffer); every block also applies the
 //       pending update of a slice of b1/W2/b2 and reduces that slice's new gradient
 //       from F2's records (fixed order: deterministic, no atomics).
 //   dh enters both backward MFMAs as a hi+lo pair of bf16 (~16-bit mantissa) because
@@ -43,8 +43,7 @@
 // Flat parameter / gradient layout = Keras weight order (views of the master buffer are
 // the Keras variables): conv2d/kernel (3,3,1,32), conv2d/bias, dense/kernel (5408,64),
 // dense/bias, dense_1/kernel (64,10), dense_1/bias; the gradient buffer tail carries
-// [loss_sum, correct, count] and is followed by cpart[320][NSP], so ONE all-reduce per
-// step moves grads + metrics.  Inputs are epoch-permuted copies of
+// [loss_sum, correct, count], so ONE all-reduce per step moves grads + metrics.  Inputs are epoch-permuted copies of
 // the dataset (row g of the epoch = global sample g), read without an index gather.
 #include "convnet.h"
 #include "damd_common.h"
@@ -84,23 +83,6 @@ __device__ __forceinline__ uint16_t bf16_lo(float v, uint16_t hi) { return f2bf(
 // next step index (wraps for benchmark epochs)
 __device__ __forceinline__ int next_cursor(const Ctrl& c, int cur) {
   return (c.wrap > 0 && cur + 1 >= c.wrap) ? 0 : cur + 1;
-}
-
-// Sum of one cpart row (NSP floats, 16-B aligned) with every load in flight at once.
-__device__ __forceinline__ float cpart_row_sum(const float* __restrict__ row, int nsp4) {
-  const float4* r4 = reinterpret_cast<const float4*>(row);
-  float4 t[12];
-  float a = 0.f;
-  for (int q0 = 0; q0 < nsp4; q0 += 12) {
-#pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      const float4 v = r4[min(q0 + q, nsp4 - 1)];
-      t[q] = (q0 + q < nsp4) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int q = 0; q < 12; ++q) a += (t[q].x + t[q].y) + (t[q].z + t[q].w);
-  }
-  return a;
 }
 
 // ---- staged input rows: registers first (loads in flight early), LDS later ------------
@@ -220,8 +202,8 @@ __device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, in
 // =================================================================================
 __global__ __launch_bounds__(512) void f1_forward(
     const float* __restrict__ X, const float* __restrict__ P, const float* __restrict__ G,
-    const float* __restrict__ V, Ctrl* __restrict__ ctrl, const float* __restrict__ cpart,
-    float* __restrict__ slabs, int B, int PP, int lg, unsigned long long* st) {
+    const float* __restrict__ V, Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
+    uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP, int lg, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   Stamps sts;
@@ -229,7 +211,6 @@ __global__ __launch_bounds__(512) void f1_forward(
   const int IB = 1 << lg, img0 = blockIdx.y * IB;
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
-  const int nsp4 = nsp(gridDim.x) / 4;
   float* xs = reinterpret_cast<float*>(smem);                              // [IB][XR][28]
   uint16_t* as = reinterpret_cast<uint16_t*>(smem + IB * XR * IMG * 4);    // [IB][KP] pooled tile
   uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
@@ -259,8 +240,7 @@ __global__ __launch_bounds__(512) void f1_forward(
     vv[u] = V4[ic];
   }
   const int tcl = min(tid, NCONV - 1);
-  const float cp = P[tcl], cv = V[tcl];
-  const float cg = cpart_row_sum(cpart + (long)tcl * nsp4 * 4, nsp4);
+  const float cp = P[tcl], cv = V[tcl], cg = G[tcl];
 
   // ---- pending SGD update of the W1 slice and of the conv weights, in registers only:
   //      the write-backs happen in F3 (W1 rows, slice owner) and F2 (conv) ----
@@ -292,8 +272,13 @@ __global__ __launch_bounds__(512) void f1_forward(
 
   ConvFrag cf;
   conv_setup(cf, cw, lane);
-  conv_pool(cf, xs, p0, np, r0, lg, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t) {
+  conv_pool(cf, xs, p0, np, r0, lg, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t cd) {
     as[bo * KP + plo * 32 + ch] = hb;
+    if (img0 + bo < B) {  // pooled tile + argmax codes for F3 (async stores, off the critical path)
+      const long o = (long)(img0 + bo) * FEAT + (p0 + plo) * NF + ch;
+      pooled[o] = hb;
+      code[o] = cd;
+    }
   });
   lds_barrier();
   stamp(sts, st, 4);
@@ -323,8 +308,8 @@ __global__ __launch_bounds__(512) void f1_forward(
 // F2: one sample row per block
 // =================================================================================
 __global__ __launch_bounds__(256) void f2_head(
-    const int* __restrict__ labels, float* __restrict__ P, const float* __restrict__ G, float* __restrict__ V,
-    Ctrl* __restrict__ ctrl, const float* __restrict__ cpart, const float* __restrict__ slabs,
+    const int* __restrict__ labels, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
+    Ctrl* __restrict__ ctrl, const float* __restrict__ slabs,
     float* __restrict__ dh, float* __restrict__ rec, int B, int NS, unsigned long long* st) {
   Stamps sts;
   stamp(sts, st, 0);
@@ -341,7 +326,6 @@ __global__ __launch_bounds__(256) void f2_head(
   const bool valid = g < c.nsamples;
   const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
   const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
-  const int nsp4 = nsp(NS) / 4;
 
   // ---- issue: label, small params (3 per thread), slab slices, conv write-back inputs ----
   const int yl = labels[max(0L, min(g, (long)c.nsamples - 1))];
@@ -358,8 +342,7 @@ __global__ __launch_bounds__(256) void f2_head(
   const int cpb = (NCONV + gridDim.x - 1) / gridDim.x;
   const int ci = min(b * cpb + tid, NCONV - 1);
   const bool c_on = tid < cpb && b * cpb + tid < NCONV;
-  const float cpp = P[ci], cvv = V[ci];
-  const float cgg = cpart_row_sum(cpart + (long)ci * nsp4 * 4, nsp4);
+  const float cpp = P[ci], cvv = V[ci], cgg = G[ci];
   float hsum = 0.f;
   {
     const float* src = slabs + (long)b * HID + l;
@@ -390,6 +373,7 @@ __global__ __launch_bounds__(256) void f2_head(
     sgd_update(cpp, cgg, cvv, c.lr, c.momentum, c.nesterov, wn, vn);
     P[ci] = wn;
     if (c.momentum != 0.f) V[ci] = vn;
+    G[ci] = 0.f;  // consumed (F1 read it before this launch); F3 accumulates the new one
   }
   hw[w * 64 + l] = hsum;
   lds_barrier();
@@ -487,12 +471,12 @@ __device__ __forceinline__ float rec_sum(const float* __restrict__ rc, int q, in
 
 __global__ __launch_bounds__(512) void f3_backward(
     const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
-    Ctrl* __restrict__ ctrl, const float* __restrict__ dh, const float* __restrict__ rec,
-    float* __restrict__ cpart, int B, int PP, unsigned long long* st) {
+    Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
+    const float* __restrict__ dh, const float* __restrict__ rec, int B, int PP, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Stamps sts;
   stamp(sts, st, 0);
-  const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x, NSP = nsp(gridDim.x);
+  const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x;
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KD = PP * 32 + 4;   // dps pitch (f32)
   const int KC = PP * 32;       // code pitch (bytes)
@@ -503,7 +487,6 @@ __global__ __launch_bounds__(512) void f3_backward(
   uint16_t* dhs = dht + 2 * HID * HP;                                      // [2][CH][HP]  hi, lo
   uint16_t* w1s = dhs + 2 * CH * HP;                                       // [PP*32][HP]
   uint8_t* cs = reinterpret_cast<uint8_t*>(w1s + PP * 32 * HP);            // [CH][KC] argmax codes
-  float* cwl = reinterpret_cast<float*>(cs + CH * KC);                     // [320] conv params
   float* red = reinterpret_cast<float*>(pt);  // [16][320] reduction scratch, after the MFMAs
   const Ctrl c = *ctrl;
   if (s == 0 && tid == 0) {
@@ -555,14 +538,31 @@ __global__ __launch_bounds__(512) void f3_backward(
   }
   XStage xst;
   float4 dv[2];
-  // conv parameters as written back by F2 of this step (== F1's register copy)
-  const float cpw = P[min(tid, NCONV - 1)];
+  uint4 pv[2];
+  uint4 cv;
+  const int kq = K / 8;   // uint4 (8 bf16) per image row of the pooled slice
+  const int kc = K / 16;  // uint4 of code bytes per image
   auto load_chunk = [&](int chunk) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {  // dh: 64x64 fp32 = 1024 float4
       const int i = tid + u * 512, bb = i >> 4, lb = chunk * CH + bb;
       const float4 v = reinterpret_cast<const float4*>(dh + (long)min(lb, B - 1) * HID)[i & 15];
       dv[u] = lb < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 512, bb = i / kq, q = i - bb * kq, lb = chunk * CH + bb;
+      const bool ok = i < CH * kq && lb < B;
+      const uint4 v = *reinterpret_cast<const uint4*>(pooled + (long)min(lb, B - 1) * FEAT + p0 * NF +
+                                                      min(q, kq - 1) * 8);
+      pv[u] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+    }
+    {
+      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
+      const bool ok = i < CH * kc && lb < B;
+      const uint4 v = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF +
+                                                      min(q, kc - 1) * 16);
+      cv = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
     x_load(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
   };
@@ -579,6 +579,23 @@ __global__ __launch_bounds__(512) void f3_backward(
         dht[(n + j) * HP + bb] = hi;
         dht[HID * HP + (n + j) * HP + bb] = lo;
       }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 512;
+      if (i < CH * kq) {
+        const int bb = i / kq, q = i - bb * kq;
+        const uint32_t w4[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pt[(q * 8 + 2 * j) * HP + bb] = (uint16_t)(w4[j] & 0xffff);
+          pt[(q * 8 + 2 * j + 1) * HP + bb] = (uint16_t)(w4[j] >> 16);
+        }
+      }
+    }
+    if (tid < CH * kc) {
+      const int bb = tid / kc, q = tid - bb * kc;
+      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
     }
     x_store(xst, xs, CH, nrows);
   };
@@ -614,7 +631,6 @@ __global__ __launch_bounds__(512) void f3_backward(
 #pragma unroll
   for (int t = 0; t < 9; ++t) gw[t] = 0.f;
   const int nchunks = (B + CH - 1) / CH;
-  ConvFrag cf;
 
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     if (chunk) {
@@ -622,19 +638,8 @@ __global__ __launch_bounds__(512) void f3_backward(
       load_chunk(chunk);
     }
     store_chunk();
-    if (chunk == 0 && tid < NCONV) cwl[tid] = cpw;
     lds_barrier();
     stamp(sts, st, 1);
-    // recompute this slice's conv + ReLU + max-pool (cheaper than storing the pooled
-    // tile and argmax codes in F1 and re-reading them here): pooled -> pt [k][b] (the
-    // A operand of dW1), codes -> cs
-    if (chunk == 0) conv_setup(cf, cwl, lane);
-    conv_pool(cf, xs, p0, np, r0, 6, wave, lane, [&](int bo, int plo, int chn, uint16_t hb, uint8_t cd) {
-      pt[(plo * 32 + chn) * HP + bo] = hb;
-      cs[bo * KC + plo * 32 + chn] = chunk * CH + bo < B ? cd : (uint8_t)0;
-    });
-    lds_barrier();
-    stamp(sts, st, 2);
     // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
 #pragma unroll
     for (int i = 0; i < MAXPP; ++i) {
@@ -670,7 +675,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
     lds_barrier();
-    stamp(sts, st, 3);
+    stamp(sts, st, 2);
     // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
     // (branch-free: the gradient is masked, the reads always hit staged LDS rows)
 #pragma unroll
@@ -692,7 +697,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       }
     }
   }
-  stamp(sts, st, 4);
+  stamp(sts, st, 3);
   // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
@@ -711,12 +716,14 @@ __global__ __launch_bounds__(512) void f3_backward(
   float* ared = dps;
   ared[tid] = arsum;
   lds_barrier();
-  // this slice's conv-gradient partial: column s of cpart (all-reduced with G)
+  // this slice's conv-gradient partial -> G[conv] (device-scope fp32 atomics: 320 per
+  // block; the summation order over the 43 slices is not fixed, so the conv gradient is
+  // reproducible to rounding, not bitwise -- ranks still agree after the all-reduce)
   for (int i = tid; i < NCONV; i += 512) {
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
-    cpart[(long)i * NSP + s] = a;
+    atomicAdd(&G[i], a);
   }
   // ---- aux: pending update of b1/W2/b2, their new gradients, metrics ----
   if (aux_on && aq == 0) {
@@ -737,8 +744,8 @@ __global__ __launch_bounds__(512) void f3_backward(
       G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
   }
-  stamp(sts, st, 5);
-  stamp_flush(sts, st, 6);
+  stamp(sts, st, 4);
+  stamp_flush(sts, st, 5);
 }
 
 // =================================================================================
@@ -746,20 +753,12 @@ __global__ __launch_bounds__(512) void f3_backward(
 // buffers and fold the pending metrics into the epoch accumulators.
 // =================================================================================
 __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, float* __restrict__ G,
-                                                     float* __restrict__ V, Ctrl* __restrict__ ctrl,
-                                                     float* __restrict__ cpart, int NSP) {
+                                                     float* __restrict__ V, Ctrl* __restrict__ ctrl) {
   const Ctrl c = *ctrl;
   const bool mom = c.momentum != 0.f;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NPARAM; i += gridDim.x * blockDim.x) {
-    float g;
-    if (i < NCONV) {
-      g = cpart_row_sum(cpart + (long)i * NSP, NSP / 4);
-      for (int q = 0; q < NSP; ++q) cpart[(long)i * NSP + q] = 0.f;
-    } else {
-      g = G[i];
-    }
     float wn, vn;
-    sgd_update(P[i], g, V[i], c.lr, c.momentum, c.nesterov, wn, vn);
+    sgd_update(P[i], G[i], V[i], c.lr, c.momentum, c.nesterov, wn, vn);
     P[i] = wn;
     if (mom) V[i] = vn;
     G[i] = 0.f;
@@ -778,10 +777,7 @@ __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, floa
 // Host-side launchers (no allocation / sync: capturable into a hipGraph).
 // ---------------------------------------------------------------------------------
 int convnet_num_slices(int PP) { return (convnet::NPOS + PP - 1) / PP; }
-int convnet_cpart_pitch(int PP) { return convnet::nsp(convnet_num_slices(PP)); }
-size_t convnet_grad_count(int PP) {
-  return (size_t)convnet::NGRAD + (size_t)convnet::NCONV * convnet_cpart_pitch(PP);
-}
+size_t convnet_grad_count(int) { return (size_t)convnet::NGRAD; }
 
 // F1 images per block = 2^lg: 16 up to B = 256 (more blocks, shorter per-block chains),
 // 64 beyond (bounded replication of the W1-slice / conv-partial loads)
@@ -795,7 +791,7 @@ size_t convnet_f3_lds(int PP) {
   using namespace convnet;
   const int KD = PP * 32 + 4;
   return XS_BYTES + (size_t)CH * KD * 4 + (size_t)PP * 32 * HP * 2 * 2 + (size_t)2 * (HID + CH) * HP * 2 +
-         (size_t)CH * PP * 32 + NCONV * 4 + 16;
+         (size_t)CH * PP * 32 + 16;
 }
 
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
@@ -803,18 +799,17 @@ hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
   hipLaunchKernelGGL(f1_forward, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st, b.X,
-                     b.P, b.G, b.V, b.ctrl, b.cpart, b.slabs, B, PP, lg, b.stamps);
-  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.cpart, b.slabs, b.dh,
+                     b.P, b.G, b.V, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg, b.stamps);
+  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dh,
                      b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
   hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
-                     b.dh, b.hpart, b.cpart, B, PP,
+                     b.pooled, b.code, b.dh, b.hpart, B, PP,
                      b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   return hipGetLastError();
 }
 
 hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st) {
-  hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.ctrl, b.cpart,
-                     convnet_cpart_pitch(PP));
+  hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.ctrl);
   return hipGetLastError();
 }
 

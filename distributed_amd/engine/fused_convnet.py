@@ -87,19 +87,16 @@ class FusedConvNetEngine(Engine):
         if not 1 <= self.PP <= 4:
             raise ValueError("DAMD_PP must be in [1, 4]")
         NS = C.convnet_num_slices(self.PP)
-        NSP = C.convnet_cpart_pitch(self.PP)
         f32 = dict(dtype=torch.float32, device=dev)
         self.P = torch.zeros(NGRAD, **f32)
-        # one all-reduced buffer: flat gradient (+ metric tail) followed by the per-slice
-        # conv-gradient partials cpart[320][NSP]
-        self.gbuf = torch.zeros(C.convnet_grad_count(self.PP), **f32)
-        self.G = self.gbuf[:NGRAD]
+        self.G = torch.zeros(C.convnet_grad_count(self.PP), **f32)  # grads + metric tail
         self.V = torch.zeros(NGRAD, **f32)
         self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
         self.slabs = torch.zeros(NS, B, HID, **f32)
         self.dh = torch.zeros(B, HID, **f32)
         self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
-        self.cpart = self.gbuf[NGRAD:].view(NCONV, NSP)
+        self.pooled = torch.zeros(B, FEAT, dtype=torch.bfloat16, device=dev)
+        self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
         off = 0
@@ -122,7 +119,7 @@ class FusedConvNetEngine(Engine):
         bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
                     ctrl=self.ctrl.data_ptr(),
                     slabs=self.slabs.data_ptr(), dh=self.dh.data_ptr(), hpart=self.hpart.data_ptr(),
-                    cpart=self.cpart.data_ptr())
+                    pooled=self.pooled.data_ptr(), code=self.code.data_ptr())
         self.stamps = None
         if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
             self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)

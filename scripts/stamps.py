@@ -35,7 +35,7 @@ def main():
     grids = {"F1": NS * ((B + 15) // 16), "F2": B, "F3": NS}
     names = {"F1": ["start", "ctrl", "sgd+loads", "xs staged", "conv done", "end"],
              "F2": ["start", "slabs+params", "end"],
-             "F3": ["start", "loads staged", "conv recomputed", "mfma", "convgrad", "end"]}
+             "F3": ["start", "loads staged", "mfma", "convgrad", "end"]}
     t0 = None
     for k, (kn, n) in enumerate(grids.items()):
         a = st[k, :n].astype(np.int64)
