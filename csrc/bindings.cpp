@@ -44,6 +44,7 @@ class ConvNetTrainer : public StepExecutor {
     b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
     b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
     b_.hpart = P_<float>(g("hpart"));
+    b_.W1alt = P_<float>(g("w1alt")); b_.V1alt = P_<float>(g("v1alt")); b_.w1bf = P_<uint16_t>(g("w1bf"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
     HIP_CHECK(convnet_set_lds_limits());
   }

@@ -54,7 +54,8 @@ struct Ctrl {
   int   wrap;               // 13 if > 0: cursor wraps modulo `wrap` (benchmark epochs)
   int   cur2;               // 14 step index as seen by the 2nd kernel of a step (set by the 1st)
   int   cur3;               // 15 step index as seen by the 3rd kernel (set by the 2nd)
-  int   pad[16];
+  int   wpar;               // 16 which W1 buffer is current (0: inside P, 1: the alternate)
+  int   pad[15];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

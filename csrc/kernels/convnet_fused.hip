@@ -202,7 +202,8 @@ __device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, in
 // =================================================================================
 __global__ __launch_bounds__(512) void f1_forward(
     const float* __restrict__ X, const float* __restrict__ P, const float* __restrict__ G,
-    const float* __restrict__ V, Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
+    const float* __restrict__ V, float* __restrict__ W1alt, float* __restrict__ V1alt,
+    uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
     uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP, int lg, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -228,10 +229,21 @@ __global__ __launch_bounds__(512) void f1_forward(
   x_load(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
   const int n4 = K * HID / 4;  // <= 2048
   float4 wv[4], gv[4], vv[4];
-  const float4* P4 = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID);
+  // W1 (and its velocity) are double-buffered by step parity: this step reads the
+  // current buffer and the slice's first image-group block writes the updated rows into
+  // the other one, so the four blocks sharing a slice never race on the master copy
+  const float* Wcur = c.wpar ? W1alt : P + OFF_W1;
+  const float* Vcur = c.wpar ? V1alt : V + OFF_W1;
+  float* Wnext = c.wpar ? const_cast<float*>(P) + OFF_W1 : W1alt;
+  float* Vnext = c.wpar ? const_cast<float*>(V) + OFF_W1 : V1alt;
+  const float4* P4 = reinterpret_cast<const float4*>(Wcur + p0 * 32 * HID);
   const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
-  // without momentum the velocity is never read: point its loads at P (cache hits)
-  const float4* V4 = reinterpret_cast<const float4*>((mom ? V : P) + OFF_W1 + p0 * 32 * HID);
+  // without momentum the velocity is never read: point its loads at W (cache hits)
+  const float4* V4 = reinterpret_cast<const float4*>((mom ? Vcur : Wcur) + p0 * 32 * HID);
+  const bool owner = blockIdx.y == 0;
+  float4* Wn4 = reinterpret_cast<float4*>(Wnext + p0 * 32 * HID);
+  float4* Vn4 = reinterpret_cast<float4*>(Vnext + p0 * 32 * HID);
+  uint2* Wb = reinterpret_cast<uint2*>(w1bf + p0 * 32 * HID);
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int ic = min(tid + u * 512, n4 - 1);
@@ -242,8 +254,8 @@ __global__ __launch_bounds__(512) void f1_forward(
   const int tcl = min(tid, NCONV - 1);
   const float cp = P[tcl], cv = V[tcl], cg = G[tcl];
 
-  // ---- pending SGD update of the W1 slice and of the conv weights, in registers only:
-  //      the write-backs happen in F3 (W1 rows, slice owner) and F2 (conv) ----
+  // ---- pending SGD update of the W1 slice (the owner block writes the next buffer and
+  //      a bf16 copy for F3) and of the conv weights (registers; F2 writes them back) ----
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = tid + u * 512;
@@ -254,10 +266,16 @@ __global__ __launch_bounds__(512) void f1_forward(
       sgd_update(wv[u].z, gv[u].z, vv[u].z, c.lr, c.momentum, c.nesterov, wn.z, vn.z);
       sgd_update(wv[u].w, gv[u].w, vv[u].w, c.lr, c.momentum, c.nesterov, wn.w, vn.w);
       const int e = i * 4, kr = e >> 6, n = e & 63;
-      w1t[(n + 0) * KP + kr] = f2bf(wn.x);
-      w1t[(n + 1) * KP + kr] = f2bf(wn.y);
-      w1t[(n + 2) * KP + kr] = f2bf(wn.z);
-      w1t[(n + 3) * KP + kr] = f2bf(wn.w);
+      const uint16_t h0 = f2bf(wn.x), h1 = f2bf(wn.y), h2 = f2bf(wn.z), h3 = f2bf(wn.w);
+      w1t[(n + 0) * KP + kr] = h0;
+      w1t[(n + 1) * KP + kr] = h1;
+      w1t[(n + 2) * KP + kr] = h2;
+      w1t[(n + 3) * KP + kr] = h3;
+      if (owner) {
+        Wn4[i] = wn;
+        if (mom) Vn4[i] = vn;
+        Wb[i] = make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), (uint32_t)h2 | ((uint32_t)h3 << 16));
+      }
     }
   }
   if (tid < NCONV) {
@@ -471,8 +489,9 @@ __device__ __forceinline__ float rec_sum(const float* __restrict__ rc, int q, in
 
 __global__ __launch_bounds__(512) void f3_backward(
     const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
-    Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
-    const float* __restrict__ dh, const float* __restrict__ rec, int B, int PP, unsigned long long* st) {
+    const uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled,
+    const uint8_t* __restrict__ code, const float* __restrict__ dh, const float* __restrict__ rec, int B, int PP,
+    unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Stamps sts;
   stamp(sts, st, 0);
@@ -492,6 +511,7 @@ __global__ __launch_bounds__(512) void f3_backward(
   if (s == 0 && tid == 0) {
     ctrl->cursor = next_cursor(c, c.cur3);
     ctrl->iterations = c.iterations + 1;
+    ctrl->wpar = c.wpar ^ 1;  // F1 of this step wrote the next W1 buffer
   }
   const long gstart = (long)c.cur3 * c.global_batch;
   const long row_base = gstart + c.row0;
@@ -519,23 +539,12 @@ __global__ __launch_bounds__(512) void f3_backward(
   }
 
   // ---- prologue loads: W1 slice, dh, pooled slice, code slice, input rows ----
-  // W1 slice: this block owns these rows -> apply their pending update (the same
-  // arithmetic F1 did in registers), write it back, and use it for dP
-  const int n4 = K * HID / 4;
-  const bool mom = c.momentum != 0.f;
-  float4 wv[4], gv1[4], vv1[4];
-  {
-    const float4* P4 = reinterpret_cast<const float4*>(P + OFF_W1 + p0 * 32 * HID);
-    const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
-    const float4* V4 = reinterpret_cast<const float4*>((mom ? V : P) + OFF_W1 + p0 * 32 * HID);
+  // W1 slice of this step (bf16 copy written by F1's owner block) for dP
+  const int n8 = K * HID / 8;  // uint4 of 8 bf16
+  uint4 wv[2];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int ic = min(tid + u * 512, n4 - 1);
-      wv[u] = P4[ic];
-      gv1[u] = G4[ic];
-      vv1[u] = V4[ic];
-    }
-  }
+  for (int u = 0; u < 2; ++u)
+    wv[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n8 - 1)];
   XStage xst;
   float4 dv[2];
   uint4 pv[2];
@@ -600,26 +609,10 @@ __global__ __launch_bounds__(512) void f3_backward(
     x_store(xst, xs, CH, nrows);
   };
   load_chunk(0);
-  {
-    float4* P4w = reinterpret_cast<float4*>(P + OFF_W1 + p0 * 32 * HID);
-    float4* V4w = reinterpret_cast<float4*>(V + OFF_W1 + p0 * 32 * HID);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = tid + u * 512;
-      if (i < n4) {
-        float4 wn, vn;
-        sgd_update(wv[u].x, gv1[u].x, vv1[u].x, c.lr, c.momentum, c.nesterov, wn.x, vn.x);
-        sgd_update(wv[u].y, gv1[u].y, vv1[u].y, c.lr, c.momentum, c.nesterov, wn.y, vn.y);
-        sgd_update(wv[u].z, gv1[u].z, vv1[u].z, c.lr, c.momentum, c.nesterov, wn.z, vn.z);
-        sgd_update(wv[u].w, gv1[u].w, vv1[u].w, c.lr, c.momentum, c.nesterov, wn.w, vn.w);
-        P4w[i] = wn;
-        if (mom) V4w[i] = vn;
-        const int e = i * 4, kr = e >> 6, n = e & 63;
-        uint2 pk = make_uint2((uint32_t)f2bf(wn.x) | ((uint32_t)f2bf(wn.y) << 16),
-                              (uint32_t)f2bf(wn.z) | ((uint32_t)f2bf(wn.w) << 16));
-        *reinterpret_cast<uint2*>(w1s + kr * HP + n) = pk;
-      }
-    }
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * 512;
+    if (i < n8) *reinterpret_cast<uint4*>(w1s + (i >> 3) * HP + (i & 7) * 8) = wv[u];
   }
 
   const int dn = wave & 3, dm0 = wave >> 2;
@@ -753,12 +746,15 @@ __global__ __launch_bounds__(512) void f3_backward(
 // buffers and fold the pending metrics into the epoch accumulators.
 // =================================================================================
 __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, float* __restrict__ G,
-                                                     float* __restrict__ V, Ctrl* __restrict__ ctrl) {
+                                                     float* __restrict__ V, const float* __restrict__ W1alt,
+                                                     const float* __restrict__ V1alt, Ctrl* __restrict__ ctrl) {
   const Ctrl c = *ctrl;
   const bool mom = c.momentum != 0.f;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NPARAM; i += gridDim.x * blockDim.x) {
+    const bool alt = c.wpar && i >= OFF_W1 && i < OFF_B1;  // current W1 lives in the alternate
+    const float w = alt ? W1alt[i - OFF_W1] : P[i], v = alt ? V1alt[i - OFF_W1] : V[i];
     float wn, vn;
-    sgd_update(P[i], G[i], V[i], c.lr, c.momentum, c.nesterov, wn, vn);
+    sgd_update(w, G[i], v, c.lr, c.momentum, c.nesterov, wn, vn);
     P[i] = wn;
     if (mom) V[i] = vn;
     G[i] = 0.f;
@@ -770,6 +766,8 @@ __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, floa
     for (int i = NPARAM; i < NGRAD; ++i) G[i] = 0.f;
   }
 }
+// after flush_pending (separate launch: its blocks read wpar): W1 is back inside P
+__global__ void flush_fixup(Ctrl* __restrict__ ctrl) { ctrl->wpar = 0; }
 
 }  // namespace convnet
 
@@ -799,17 +797,20 @@ hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
   hipLaunchKernelGGL(f1_forward, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st, b.X,
-                     b.P, b.G, b.V, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg, b.stamps);
+                     b.P, b.G, b.V, b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg,
+                     b.stamps);
   hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dh,
                      b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
-  hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.ctrl,
+  hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.w1bf,
+                     b.ctrl,
                      b.pooled, b.code, b.dh, b.hpart, B, PP,
                      b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   return hipGetLastError();
 }
 
 hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st) {
-  hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.ctrl);
+  hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.ctrl);
+  hipLaunchKernelGGL(convnet::flush_fixup, dim3(1), dim3(1), 0, st, b.ctrl);
   return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 REC = 716
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
-C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3 = range(16)
+C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR = range(17)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -95,6 +95,9 @@ class FusedConvNetEngine(Engine):
         self.slabs = torch.zeros(NS, B, HID, **f32)
         self.dh = torch.zeros(B, HID, **f32)
         self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
+        self.w1alt = torch.zeros(FEAT * HID, **f32)   # W1 double buffer (by step parity)
+        self.v1alt = torch.zeros(FEAT * HID, **f32)
+        self.w1bf = torch.zeros(FEAT * HID, dtype=torch.bfloat16, device=dev)
         self.pooled = torch.zeros(B, FEAT, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
         # model variables -> views of the fp32 master buffer (Keras weight order)
@@ -119,7 +122,8 @@ class FusedConvNetEngine(Engine):
         bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
                     ctrl=self.ctrl.data_ptr(),
                     slabs=self.slabs.data_ptr(), dh=self.dh.data_ptr(), hpart=self.hpart.data_ptr(),
-                    pooled=self.pooled.data_ptr(), code=self.code.data_ptr())
+                    pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
+                    v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr())
         self.stamps = None
         if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
             self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)
