@@ -41,7 +41,7 @@ class ConvNetTrainer : public StepExecutor {
     b_.X = nullptr; b_.labels = nullptr;
     b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
     b_.ctrl = P_<Ctrl>(g("ctrl"));
-    b_.slabs = P_<float>(g("slabs")); b_.dh = P_<float>(g("dh"));
+    b_.slabs = P_<float>(g("slabs")); b_.dhq = P_<uint16_t>(g("dhq"));
     b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
     b_.hpart = P_<float>(g("hpart"));
     b_.W1alt = P_<float>(g("w1alt")); b_.V1alt = P_<float>(g("v1alt")); b_.w1bf = P_<uint16_t>(g("w1bf"));

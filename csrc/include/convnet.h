@@ -10,7 +10,7 @@ struct ConvNetBuffers {
   const float* X; const int* labels;
   float* P; float* G; float* V; Ctrl* ctrl;
   float* W1alt; float* V1alt; uint16_t* w1bf;  // W1 double buffer (fp32, velocity) + bf16 copy
-  uint16_t* pooled; uint8_t* code; float* slabs; float* dh; float* hpart;
+  uint16_t* pooled /* [5408][BP] */; uint8_t* code /* [B][5408] */; float* slabs; uint16_t* dhq; float* hpart;
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
 };
 constexpr int kConvNetNParam = 347146;

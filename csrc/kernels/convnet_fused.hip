@@ -210,6 +210,7 @@ __global__ __launch_bounds__(512) void f1_forward(
   Stamps sts;
   stamp(sts, st, 0);
   const int IB = 1 << lg, img0 = blockIdx.y * IB;
+  const int BP = (B + CH - 1) / CH * CH;  // padded batch pitch of the feature-major buffers
   const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
   const int KP = kpitch(PP);
   float* xs = reinterpret_cast<float*>(smem);                              // [IB][XR][28]
@@ -293,9 +294,9 @@ __global__ __launch_bounds__(512) void f1_forward(
   conv_pool(cf, xs, p0, np, r0, lg, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t cd) {
     as[bo * KP + plo * 32 + ch] = hb;
     if (img0 + bo < B) {  // pooled tile + argmax codes for F3 (async stores, off the critical path)
-      const long o = (long)(img0 + bo) * FEAT + (p0 + plo) * NF + ch;
-      pooled[o] = hb;
-      code[o] = cd;
+      const int k = (p0 + plo) * NF + ch;
+      pooled[(long)k * BP + img0 + bo] = hb;  // feature-major: F3's dW1 A operand, no transpose
+      code[(long)(img0 + bo) * FEAT + k] = cd;
     }
   });
   lds_barrier();
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(512) void f1_forward(
 __global__ __launch_bounds__(256) void f2_head(
     const int* __restrict__ labels, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
     Ctrl* __restrict__ ctrl, const float* __restrict__ slabs,
-    float* __restrict__ dh, float* __restrict__ rec, int B, int NS, unsigned long long* st) {
+    uint16_t* __restrict__ dhq, float* __restrict__ rec, int B, int NS, unsigned long long* st) {
   Stamps sts;
   stamp(sts, st, 0);
   __shared__ __attribute__((aligned(16))) float lds[NSMALL + 2 + 4 * 64 + 64 + 16];
@@ -436,7 +437,15 @@ __global__ __launch_bounds__(256) void f2_head(
 #pragma unroll
     for (int k = 0; k < NCLS; ++k) dhl = fmaf(dz[k], w2n[l * NCLS + k], dhl);
     dhl = h > 0.f ? dhl : 0.f;
-    dh[(long)b * HID + l] = dhl;
+    // dh as a bf16 hi+lo pair, row-major [b][n] (dP's A operand) and feature-major [n][b]
+    // (dW1's B operand), so F3 stages both with plain 16-byte copies
+    const int BP = (B + CH - 1) / CH * CH;
+    const long Q = (long)BP * HID;
+    const uint16_t hi = f2bf(dhl), lo = bf16_lo(dhl, hi);
+    dhq[(long)b * HID + l] = hi;
+    dhq[Q + (long)b * HID + l] = lo;
+    dhq[2 * Q + (long)l * BP + b] = hi;
+    dhq[3 * Q + (long)l * BP + b] = lo;
     rec[(long)(650 + l) * B + b] = dhl;  // db1 contribution
   }
   // dW2[k][c] = h_k dz_c   (column-major records: rec[col][row])
@@ -490,7 +499,7 @@ __device__ __forceinline__ float rec_sum(const float* __restrict__ rc, int q, in
 __global__ __launch_bounds__(512) void f3_backward(
     const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
     const uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled,
-    const uint8_t* __restrict__ code, const float* __restrict__ dh, const float* __restrict__ rec, int B, int PP,
+    const uint8_t* __restrict__ code, const uint16_t* __restrict__ dhq, const float* __restrict__ rec, int B, int PP,
     unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Stamps sts;
@@ -546,25 +555,26 @@ __global__ __launch_bounds__(512) void f3_backward(
   for (int u = 0; u < 2; ++u)
     wv[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n8 - 1)];
   XStage xst;
-  float4 dv[2];
-  uint4 pv[2];
+  // named registers, not arrays: arrays captured by the lambdas below end up in scratch
+  uint4 dq0, dq1, dq2, dq3;  // dh hi/lo [b][n] rows, dh hi/lo [n][b] rows
+  uint4 pv0, pv1;            // pooled [k][b] rows of the slice
   uint4 cv;
-  const int kq = K / 8;   // uint4 (8 bf16) per image row of the pooled slice
+  const int BP = (B + CH - 1) / CH * CH;
+  const long Q = (long)BP * HID;
   const int kc = K / 16;  // uint4 of code bytes per image
-  auto load_chunk = [&](int chunk) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {  // dh: 64x64 fp32 = 1024 float4
-      const int i = tid + u * 512, bb = i >> 4, lb = chunk * CH + bb;
-      const float4 v = reinterpret_cast<const float4*>(dh + (long)min(lb, B - 1) * HID)[i & 15];
-      dv[u] = lb < B ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
+    {
+      const int r = tid >> 3, q = tid & 7;  // 64 rows x 8 uint4
+      const long rowo = (long)(chunk * CH + r) * HID + q * 8, colo = (long)r * BP + chunk * CH + q * 8;
+      dq0 = *reinterpret_cast<const uint4*>(dhq + rowo);
+      dq1 = *reinterpret_cast<const uint4*>(dhq + Q + rowo);
+      dq2 = *reinterpret_cast<const uint4*>(dhq + 2 * Q + colo);
+      dq3 = *reinterpret_cast<const uint4*>(dhq + 3 * Q + colo);
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * 512, bb = i / kq, q = i - bb * kq, lb = chunk * CH + bb;
-      const bool ok = i < CH * kq && lb < B;
-      const uint4 v = *reinterpret_cast<const uint4*>(pooled + (long)min(lb, B - 1) * FEAT + p0 * NF +
-                                                      min(q, kq - 1) * 8);
-      pv[u] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+    {
+      const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
+      pv0 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i0 >> 3)) * BP + chunk * CH + (i0 & 7) * 8);
+      pv1 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i1 >> 3)) * BP + chunk * CH + (i1 & 7) * 8);
     }
     {
       const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
@@ -575,33 +585,16 @@ __global__ __launch_bounds__(512) void f3_backward(
     }
     x_load(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
   };
-  auto store_chunk = [&]() {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * 512, bb = i >> 4, n = (i & 15) * 4;
-      const float e[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint16_t hi = f2bf(e[j]), lo = bf16_lo(e[j], hi);
-        dhs[bb * HP + n + j] = hi;
-        dhs[CH * HP + bb * HP + n + j] = lo;
-        dht[(n + j) * HP + bb] = hi;
-        dht[HID * HP + (n + j) * HP + bb] = lo;
-      }
+  auto store_chunk = [&]() __attribute__((always_inline)) {
+    {
+      const int r = tid >> 3, q = tid & 7;
+      *reinterpret_cast<uint4*>(dhs + r * HP + q * 8) = dq0;
+      *reinterpret_cast<uint4*>(dhs + CH * HP + r * HP + q * 8) = dq1;
+      *reinterpret_cast<uint4*>(dht + r * HP + q * 8) = dq2;
+      *reinterpret_cast<uint4*>(dht + HID * HP + r * HP + q * 8) = dq3;
     }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = tid + u * 512;
-      if (i < CH * kq) {
-        const int bb = i / kq, q = i - bb * kq;
-        const uint32_t w4[4] = {pv[u].x, pv[u].y, pv[u].z, pv[u].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          pt[(q * 8 + 2 * j) * HP + bb] = (uint16_t)(w4[j] & 0xffff);
-          pt[(q * 8 + 2 * j + 1) * HP + bb] = (uint16_t)(w4[j] >> 16);
-        }
-      }
-    }
+    if (tid < K * 8) *reinterpret_cast<uint4*>(pt + (tid >> 3) * HP + (tid & 7) * 8) = pv0;
+    if (tid + 512 < K * 8) *reinterpret_cast<uint4*>(pt + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = pv1;
     if (tid < CH * kc) {
       const int bb = tid / kc, q = tid - bb * kc;
       *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
@@ -799,11 +792,11 @@ hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream
   hipLaunchKernelGGL(f1_forward, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st, b.X,
                      b.P, b.G, b.V, b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg,
                      b.stamps);
-  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dh,
+  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dhq,
                      b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
   hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.w1bf,
                      b.ctrl,
-                     b.pooled, b.code, b.dh, b.hpart, B, PP,
+                     b.pooled, b.code, b.dhq, b.hpart, B, PP,
                      b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   return hipGetLastError();
 }

@@ -93,12 +93,13 @@ class FusedConvNetEngine(Engine):
         self.V = torch.zeros(NGRAD, **f32)
         self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
         self.slabs = torch.zeros(NS, B, HID, **f32)
-        self.dh = torch.zeros(B, HID, **f32)
+        self.dhq = torch.zeros(4, BP * HID, dtype=torch.bfloat16, device=dev)  # dh hi/lo, two layouts
         self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
         self.w1alt = torch.zeros(FEAT * HID, **f32)   # W1 double buffer (by step parity)
         self.v1alt = torch.zeros(FEAT * HID, **f32)
         self.w1bf = torch.zeros(FEAT * HID, dtype=torch.bfloat16, device=dev)
-        self.pooled = torch.zeros(B, FEAT, dtype=torch.bfloat16, device=dev)
+        BP = (B + 63) // 64 * 64  # padded batch pitch of the feature-major buffers
+        self.pooled = torch.zeros(FEAT, BP, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
@@ -121,7 +122,7 @@ class FusedConvNetEngine(Engine):
         torch.cuda.synchronize(dev)
         bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
                     ctrl=self.ctrl.data_ptr(),
-                    slabs=self.slabs.data_ptr(), dh=self.dh.data_ptr(), hpart=self.hpart.data_ptr(),
+                    slabs=self.slabs.data_ptr(), dhq=self.dhq.data_ptr(), hpart=self.hpart.data_ptr(),
                     pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
                     v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr())
         self.stamps = None
