@@ -88,6 +88,7 @@ class FusedConvNetEngine(Engine):
             raise ValueError("DAMD_PP must be in [1, 4]")
         NS = C.convnet_num_slices(self.PP)
         f32 = dict(dtype=torch.float32, device=dev)
+        BP = (B + 63) // 64 * 64  # padded batch pitch of the feature-major buffers
         self.P = torch.zeros(NGRAD, **f32)
         self.G = torch.zeros(C.convnet_grad_count(self.PP), **f32)  # grads + metric tail
         self.V = torch.zeros(NGRAD, **f32)
@@ -98,7 +99,6 @@ class FusedConvNetEngine(Engine):
         self.w1alt = torch.zeros(FEAT * HID, **f32)   # W1 double buffer (by step parity)
         self.v1alt = torch.zeros(FEAT * HID, **f32)
         self.w1bf = torch.zeros(FEAT * HID, dtype=torch.bfloat16, device=dev)
-        BP = (B + 63) // 64 * 64  # padded batch pitch of the feature-major buffers
         self.pooled = torch.zeros(FEAT, BP, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
         # model variables -> views of the fp32 master buffer (Keras weight order)
