@@ -38,7 +38,7 @@ class ConvNetTrainer : public StepExecutor {
     if (B <= 0) throw std::invalid_argument("batch must be > 0");
     if (PP < 1 || PP > 4) throw std::invalid_argument("positions per slice must be in [1,4]");
     auto g = [&](const char* k) -> uintptr_t { return bufs[k].cast<uintptr_t>(); };
-    b_.X = nullptr; b_.labels = nullptr;
+    b_.X = nullptr; b_.labels = nullptr; b_.x_u8 = 0;
     b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
     b_.ctrl = P_<Ctrl>(g("ctrl"));
     b_.slabs = P_<float>(g("slabs")); b_.dhq = P_<uint16_t>(g("dhq"));
@@ -48,9 +48,10 @@ class ConvNetTrainer : public StepExecutor {
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
     HIP_CHECK(convnet_set_lds_limits());
   }
-  // X [n][784] fp32 and labels [n] int32: epoch-permuted copies (stable pointers).
-  void set_data(uintptr_t X, uintptr_t labels) {
-    b_.X = P_<const float>(X); b_.labels = P_<const int>(labels);
+  // X [n][784] (fp32, or uint8 holding k for inputs k/255) and labels [n] int32:
+  // epoch-permuted copies (stable pointers).
+  void set_data(uintptr_t X, uintptr_t labels, int x_u8) {
+    b_.X = P_<const void>(X); b_.labels = P_<const int>(labels); b_.x_u8 = x_u8;
     invalidate_graphs();
   }
   void flush() { HIP_CHECK(convnet_launch_flush(b_, PP_, stream_)); }
@@ -118,7 +119,7 @@ PYBIND11_MODULE(_C, m) {
   py::class_<ConvNetTrainer>(m, "ConvNetTrainer")
       .def(py::init<int, py::dict, int, int, int>(), py::arg("device"), py::arg("buffers"),
            py::arg("batch"), py::arg("positions_per_slice") = 4, py::arg("grad_allreduce") = 1)
-      .def("set_data", &ConvNetTrainer::set_data)
+      .def("set_data", &ConvNetTrainer::set_data, py::arg("x"), py::arg("labels"), py::arg("x_u8") = 0)
       .def("set_comm", [](ConvNetTrainer& t, RcclComm* c) { t.set_comm(c); },
            py::keep_alive<1, 2>())
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())

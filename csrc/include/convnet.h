@@ -7,7 +7,8 @@ namespace damd {
 struct Ctrl;
 // X / labels are the epoch-permuted copies of the dataset (row g = global sample g).
 struct ConvNetBuffers {
-  const float* X; const int* labels;
+  const void* X; const int* labels;  // X: fp32 [n][784], or uint8 [n][784] when x_u8
+  int x_u8;
   float* P; float* G; float* V; Ctrl* ctrl;
   float* W1alt; float* V1alt; uint16_t* w1bf;  // W1 double buffer (fp32, velocity) + bf16 copy
   uint16_t* pooled /* [5408][BP] */; uint8_t* code /* [B][5408] */; float* slabs; uint16_t* dhq; float* hpart;

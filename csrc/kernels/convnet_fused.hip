@@ -89,8 +89,12 @@ __device__ __forceinline__ int next_cursor(const Ctrl& c, int cur) {
 struct XStage {
   float4 v[6];
 };
-// rows [r0, r0+nrows) of images b < nimg (valid if b < nvalid and row_base+b < nsamples)
-__device__ __forceinline__ void x_load(XStage& st, const float* __restrict__ X, long row_base, int nsamples,
+// Input rows [r0, r0+nrows) of images b < nimg (valid if b < nvalid and row_base+b <
+// nsamples).  U8: the dataset is kept as uint8 (inputs that are exactly k/255, e.g.
+// MNIST) -- 4x fewer bytes -- and k/255.f (correctly rounded, == float32(k/255.0)) is
+// formed when staging; otherwise fp32 rows.  One unit = 16 B (fp32) or 4 B (u8).
+template <bool U8>
+__device__ __forceinline__ void x_load(XStage& st, const void* __restrict__ X, long row_base, int nsamples,
                                        int nvalid, int nimg, int r0, int nrows) {
   const int per_img = nrows * 7, total = nimg * per_img;
 #pragma unroll
@@ -100,10 +104,17 @@ __device__ __forceinline__ void x_load(XStage& st, const float* __restrict__ X, 
     const long g = row_base + b;
     const bool ok = ((int)threadIdx.x + u * 512 < total) && b < nvalid && g < nsamples;
     const long gs = max(0L, min(g, (long)nsamples - 1));
-    const float4 v = reinterpret_cast<const float4*>(X + gs * NPIX + (r0 + r) * IMG)[q];
-    st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (U8) {
+      const uint32_t w = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + gs * NPIX +
+                                                           (r0 + r) * IMG)[q];
+      st.v[u].x = __uint_as_float(ok ? w : 0u);
+    } else {
+      const float4 v = reinterpret_cast<const float4*>(static_cast<const float*>(X) + gs * NPIX + (r0 + r) * IMG)[q];
+      st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
 }
+template <bool U8>
 __device__ __forceinline__ void x_store(const XStage& st, float* xs, int nimg, int nrows) {
   const int per_img = nrows * 7, total = nimg * per_img;
 #pragma unroll
@@ -111,7 +122,13 @@ __device__ __forceinline__ void x_store(const XStage& st, float* xs, int nimg, i
     const int i = threadIdx.x + u * 512;
     if (i < total) {
       const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-      reinterpret_cast<float4*>(xs + (b * XR + r) * IMG)[q] = st.v[u];
+      float4 v = st.v[u];
+      if constexpr (U8) {
+        const uint32_t w = __float_as_uint(st.v[u].x);
+        v = make_float4((float)(w & 0xff) / 255.f, (float)((w >> 8) & 0xff) / 255.f,
+                        (float)((w >> 16) & 0xff) / 255.f, (float)(w >> 24) / 255.f);
+      }
+      reinterpret_cast<float4*>(xs + (b * XR + r) * IMG)[q] = v;
     }
   }
 }
@@ -200,8 +217,9 @@ __device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, in
 // =================================================================================
 // F1: grid (NS slices, ISPLIT image groups of IB = 2^lg images)
 // =================================================================================
+template <bool U8>
 __global__ __launch_bounds__(512) void f1_forward(
-    const float* __restrict__ X, const float* __restrict__ P, const float* __restrict__ G,
+    const void* __restrict__ X, const float* __restrict__ P, const float* __restrict__ G,
     const float* __restrict__ V, float* __restrict__ W1alt, float* __restrict__ V1alt,
     uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
     uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP, int lg, unsigned long long* st) {
@@ -227,7 +245,7 @@ __global__ __launch_bounds__(512) void f1_forward(
 
   // ---- issue every independent load of the prologue ----
   XStage xst;
-  x_load(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
+  x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
   const int n4 = K * HID / 4;  // <= 2048
   float4 wv[4], gv[4], vv[4];
   // W1 (and its velocity) are double-buffered by step parity: this step reads the
@@ -285,7 +303,7 @@ __global__ __launch_bounds__(512) void f1_forward(
     cw[tid] = wn;
   }
   stamp(sts, st, 2);
-  x_store(xst, xs, IB, nrows);
+  x_store<U8>(xst, xs, IB, nrows);
   lds_barrier();
   stamp(sts, st, 3);
 
@@ -496,8 +514,9 @@ __device__ __forceinline__ float rec_sum(const float* __restrict__ rc, int q, in
   return a;
 }
 
+template <bool U8>
 __global__ __launch_bounds__(512) void f3_backward(
-    const float* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
+    const void* __restrict__ X, float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
     const uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl, const uint16_t* __restrict__ pooled,
     const uint8_t* __restrict__ code, const uint16_t* __restrict__ dhq, const float* __restrict__ rec, int B, int PP,
     unsigned long long* st) {
@@ -583,7 +602,7 @@ __global__ __launch_bounds__(512) void f3_backward(
                                                       min(q, kc - 1) * 16);
       cv = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
-    x_load(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
+    x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
   };
   auto store_chunk = [&]() __attribute__((always_inline)) {
     {
@@ -599,7 +618,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       const int bb = tid / kc, q = tid - bb * kc;
       *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
     }
-    x_store(xst, xs, CH, nrows);
+    x_store<U8>(xst, xs, CH, nrows);
   };
   load_chunk(0);
 #pragma unroll
@@ -785,19 +804,23 @@ size_t convnet_f3_lds(int PP) {
          (size_t)CH * PP * 32 + 16;
 }
 
-hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+template <bool U8>
+static void launch_step_impl(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
-  hipLaunchKernelGGL(f1_forward, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st, b.X,
-                     b.P, b.G, b.V, b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg,
+  hipLaunchKernelGGL(f1_forward<U8>, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st,
+                     b.X, b.P, b.G, b.V, b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg,
                      b.stamps);
   hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dhq,
                      b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
-  hipLaunchKernelGGL(f3_backward, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.w1bf,
-                     b.ctrl,
-                     b.pooled, b.code, b.dhq, b.hpart, B, PP,
-                     b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+  hipLaunchKernelGGL(f3_backward<U8>, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.w1bf,
+                     b.ctrl, b.pooled, b.code, b.dhq, b.hpart, B, PP, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+}
+
+hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+  if (b.x_u8) launch_step_impl<true>(b, B, PP, st);
+  else launch_step_impl<false>(b, B, PP, st);
   return hipGetLastError();
 }
 
@@ -808,11 +831,13 @@ hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st)
 }
 
 hipError_t convnet_set_lds_limits() {
-  hipError_t e = hipFuncSetAttribute((const void*)convnet::f3_backward,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)convnet::f1_forward, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             160 * 1024);
+  const void* fns[4] = {(const void*)convnet::f3_backward<false>, (const void*)convnet::f3_backward<true>,
+                        (const void*)convnet::f1_forward<false>, (const void*)convnet::f1_forward<true>};
+  for (const void* f : fns) {
+    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace damd

@@ -187,13 +187,13 @@ class FusedConvNetEngine(Engine):
         key = (id(x), id(y), len(x))
         if self.feed is None or getattr(self, "_feed_key", None) != key:
             self.trainer.sync(0.0)
-            self.feed = DataFeed(x, y, self.device, flatten=True)
+            self.feed = DataFeed(x, y, self.device, flatten=True, allow_u8=env.get_bool("DAMD_X_U8", True))
             self._feed_key = key
             torch.cuda.synchronize(self.device)
             self.x_ep = torch.empty_like(self.feed.x)
             self.y_ep = torch.empty_like(self.feed.y)
             torch.cuda.synchronize(self.device)
-            self.trainer.set_data(self.x_ep.data_ptr(), self.y_ep.data_ptr())
+            self.trainer.set_data(self.x_ep.data_ptr(), self.y_ep.data_ptr(), int(self.feed.x_u8))
             self._ctrl_write({C_NS: self.feed.n})
         return self.feed
 

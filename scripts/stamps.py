@@ -9,7 +9,8 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ["DAMD_STAMPS"] = "1"
-os.environ.setdefault("DAMD_GRAPH", "0")
+os.environ.setdefault("DAMD_GRAPH", "1")
+os.environ.setdefault("DAMD_GRAPH_STEPS", "10")
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
@@ -28,7 +29,7 @@ def main():
     eng.run(50)
     eng.sync()
     eng.stamps.zero_()
-    eng.run(1)
+    eng.run(10)  # one captured 10-step graph; the stamps keep the last step's values
     eng.sync()
     st = eng.stamps.cpu().numpy()
     NS = eng.trainer.num_slices

@@ -188,3 +188,25 @@ def test_native_module_loaded():
     C = n.require_C()
     assert C.__file__.endswith(".so")
     assert any(k.startswith("distributed_amd._C") for k in sys.modules)
+
+
+def test_uint8_dataset_path_matches_fp32(monkeypatch):
+    """Inputs that are exactly k/255 are kept as uint8 on device; results must equal the fp32 path."""
+    _need_gpu()
+    monkeypatch.setenv("DAMD_GRAPH", "0")
+    rng = np.random.default_rng(7)
+    x = rng.integers(0, 256, (512, 28, 28, 1)).astype(np.uint8) / 255.0
+    y = rng.integers(0, 10, 512)
+    out = []
+    for u8 in ("1", "0"):
+        monkeypatch.setenv("DAMD_X_U8", u8)
+        m = _model(lr=0.1, seed=21)
+        eng = _engine(m, 64)
+        eng.bind(x, y)
+        assert eng.feed.x_u8 == (u8 == "1")
+        eng.start_epoch(0, shuffle=False)
+        eng.run(3)
+        eng.end_epoch()
+        eng.finish()
+        out.append(np.concatenate([w.ravel() for w in m.get_weights()]))
+    np.testing.assert_allclose(out[0], out[1], rtol=1e-5, atol=1e-7)
