@@ -38,6 +38,9 @@ class Engine:
     def lr_changed(self):
         pass
 
+    def reload_optimizer_state(self):
+        """Optimizer slots / iterations were replaced on the host (checkpoint restore)."""
+
     def sync(self):
         pass
 

@@ -174,6 +174,17 @@ class FusedConvNetEngine(Engine):
     def _iterations(self):
         return self._ctrl_host()[C_IT]
 
+    def reload_optimizer_state(self):
+        self._flush()
+        self.trainer.sync(0.0)
+        opt = self.model.optimizer
+        if opt.momentum and "momentum" in opt.slots and opt.slots["momentum"].numel() == NPARAM:
+            self.V[:NPARAM].copy_(opt.slots["momentum"].to(self.device))
+        opt._iter_source = None
+        it = int(opt.iterations)
+        opt._iter_source = self._iterations
+        self._ctrl_write({C_IT: it})
+
     def lr_changed(self):
         self._flush()
         c = {C_LR: _f2i(self.model.optimizer.learning_rate)}
