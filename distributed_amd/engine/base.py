@@ -15,6 +15,14 @@ class Engine:
         self.per_replica, self.global_batch = per_replica_batch, global_batch
         self.world, self.rank = strategy.num_replicas_in_sync, strategy.rank
         self.device = strategy.device
+        # every replica must draw the same epoch permutation (disjoint shards of one global
+        # batch): the shuffle seed is rank 0's, broadcast once
+        from ..utils import random as _r
+
+        seed = _r._GLOBAL_SEED if _r._GLOBAL_SEED is not None else 0x5EED
+        if self.world > 1:
+            seed = strategy.communicator.broadcast_object(seed, 0)
+        self.shuffle_seed = int(seed)
 
     def bind(self, x, y):  # -> DataFeed
         raise NotImplementedError

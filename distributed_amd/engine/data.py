@@ -12,7 +12,6 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from ..utils.random import _GLOBAL_SEED  # noqa: F401
 
 _BASE_SEED = 0x5EED
 
@@ -58,14 +57,11 @@ class DataFeed:
         self.device = device
 
     def set_epoch(self, epoch: int, shuffle: bool = True, seed: int = None) -> None:
-        from ..utils import random as _r
-
         if not shuffle:
             p = torch.arange(self.n, dtype=torch.int32)
         else:
             g = torch.Generator()
-            base = _r._GLOBAL_SEED if _r._GLOBAL_SEED is not None else _BASE_SEED
-            g.manual_seed(int(seed if seed is not None else base) * 7919 + int(epoch))
+            g.manual_seed(int(seed if seed is not None else _BASE_SEED) * 7919 + int(epoch))
             p = torch.randperm(self.n, generator=g).to(torch.int32)
         self.perm.copy_(p.to(self.device))
 

@@ -213,7 +213,7 @@ class FusedConvNetEngine(Engine):
         epoch without host round trips); fit() manages epochs on the host (wrap 0)."""
         self._flush()
         self.trainer.sync(0.0)
-        self.feed.set_epoch(epoch, shuffle)
+        self.feed.set_epoch(epoch, shuffle, self.shuffle_seed)
         # materialise the epoch order once (one gather per epoch instead of an index
         # indirection on every step's critical path)
         perm = self.feed.perm.long()

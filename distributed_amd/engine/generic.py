@@ -61,7 +61,7 @@ class GenericEngine(Engine):
         return self.feed
 
     def start_epoch(self, epoch, shuffle):
-        self.feed.set_epoch(epoch, shuffle)
+        self.feed.set_epoch(epoch, shuffle, self.shuffle_seed)
         self.step_in_epoch = 0
         self.acc.zero_()
 

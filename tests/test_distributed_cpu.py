@@ -1,0 +1,169 @@
+"""Multi-process data parallelism on CPU (gloo), launched like the reference's workers:
+one process per worker, TF_CONFIG per rank (README.md:84-113, 319-357)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from distributed_amd import launch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "helpers", "dist_worker.py")
+pytestmark = pytest.mark.dist
+
+
+def _env(out, **kw):
+    e = {"DAMD_DEVICE": "cpu", "DAMD_TEST_OUT": str(out), "PYTHONPATH": ROOT, "OMP_NUM_THREADS": "2",
+         "DAMD_LOG_LEVEL": "WARNING"}
+    e.update({k: str(v) for k, v in kw.items()})
+    return e
+
+
+def _load(out, r):
+    w = [a for a in np.load(os.path.join(out, f"rank{r}.npz")).values()]
+    with open(os.path.join(out, f"rank{r}.json")) as f:
+        return w, json.load(f)
+
+
+@pytest.mark.timeout(300)
+def test_two_workers_mirror_and_match_single_worker(tmp_path):
+    d2 = tmp_path / "w2"
+    d2.mkdir()
+    res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=16), timeout=240)
+    assert res.ok, res.returncodes
+    (w0, j0), (w1, j1) = _load(d2, 0), _load(d2, 1)
+    assert j0["world"] == j1["world"] == 2
+    # mirrored variables: bitwise identical on every worker (init broadcast + same all-reduced grads)
+    assert all(np.array_equal(a, b) for a, b in zip(w0, w1))
+    # global metrics: identical History on every worker (README.md:229-231)
+    assert j0["history"] == j1["history"]
+    assert j0["iterations"] == 6
+    # N-worker DP at global batch B == 1 worker at batch B from the same initial weights
+    d1 = tmp_path / "w1"
+    d1.mkdir()
+    res = launch.launch_script([WORKER], nproc=1, env=_env(d1, DAMD_TEST_PER_REPLICA=32,
+                                                           DAMD_TEST_INIT_FROM=d2 / "init0.npz"), timeout=240)
+    assert res.ok, res.returncodes
+    ws, js = _load(d1, 0)
+    for a, b in zip(w0, ws):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-5)
+
+
+def _ranked(df, barrier):
+    import os as _os
+
+    return f"{barrier['partition']}/{len(barrier['address'])}/{_os.environ['DAMD_LOCAL_RANK']}"
+
+
+def _fails_on_1(df, barrier):
+    if barrier["partition"] == 1:
+        raise ValueError("boom")
+    return "ok"
+
+
+def _crash_first_attempt(df, barrier):
+    import os as _os
+
+    if barrier["partition"] == 0 and _os.environ.get("DAMD_RESTART_COUNT") == "0":
+        _os._exit(3)  # hard crash of one task: the whole gang must be retried
+    return int(_os.environ["DAMD_RESTART_COUNT"])
+
+
+def test_barrier_apply_order_and_error_strings():
+    out = launch.barrier_apply(_ranked, 3)
+    assert out == ["0/3/0", "1/3/1", "2/3/2"]
+    out = launch.barrier_apply(_fails_on_1, 3)  # tryCatch contract (README.md:176, 221)
+    assert out[0] == "ok" and out[2] == "ok" and out[1] == "ValueError: boom"
+    with pytest.raises(RuntimeError):
+        launch.barrier_apply(_fails_on_1, 2, on_error="raise")
+
+
+def test_barrier_apply_gang_restart():
+    assert launch.barrier_apply(_crash_first_attempt, 2, max_restarts=1) == [1, 1]
+    with pytest.raises(RuntimeError):
+        launch.barrier_apply(_crash_first_attempt, 2, max_restarts=0)
+
+
+def test_launcher_cli_gang_restart(tmp_path):
+    script = tmp_path / "flaky.py"
+    script.write_text(
+        "import os, sys\n"
+        "if os.environ['DAMD_LOCAL_RANK'] == '1' and os.environ['DAMD_RESTART_COUNT'] == '0': sys.exit(7)\n"
+        "import json; c = json.loads(os.environ['TF_CONFIG'])\n"
+        "open(os.path.join(%r, 'r%%s' %% c['task']['index']), 'w').write(os.environ['DAMD_RESTART_COUNT'])\n"
+        % str(tmp_path))
+    r = subprocess.run([sys.executable, "-m", "distributed_amd.launch", "--nproc", "2", "--max-restarts", "1",
+                        str(script)], cwd=ROOT, capture_output=True, text=True, timeout=120,
+                       env={**os.environ, "PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "r0").read_text() == "1" and (tmp_path / "r1").read_text() == "1"
+    r = subprocess.run([sys.executable, "-m", "distributed_amd.launch", "--nproc", "2", str(script)], cwd=ROOT,
+                       capture_output=True, text=True, timeout=120, env={**os.environ, "PYTHONPATH": ROOT})
+    assert r.returncode == 1 and "failed" in r.stderr
+
+
+def _spark_closure(df, barrier):
+    """The README's Spark closure (README.md:175-221), transliterated."""
+    import os as _os
+
+    _os.environ["DAMD_DEVICE"] = "cpu"
+    _os.environ["OMP_NUM_THREADS"] = "2"
+    try:
+        from distributed_amd import r_api as k
+        import distributed_amd as tf
+
+        k.sys_setenv(TF_CONFIG=k.barrier_tf_config(barrier, base_port=int(_os.environ["SPARK_PORT_BASE"])))
+        if k.tf_version() is None:
+            k.install_tensorflow()
+        strategy = tf.distribute.experimental.MultiWorkerMirroredStrategy()
+        num_workers = 3
+        batch_size = 64 * num_workers
+        mnist = k.dataset_mnist()
+        x_train = k.array_reshape(mnist["train"]["x"][:2048], k.c(2048, 28, 28, 1)) / 255
+        y_train = mnist["train"]["y"][:2048]
+        with strategy.scope():
+            model = k.keras_model_sequential()
+            k.layer_conv_2d(model, filters=32, kernel_size=3, activation="relu", input_shape=k.c(28, 28, 1))
+            k.layer_max_pooling_2d(model)
+            k.layer_flatten(model)
+            k.layer_dense(model, units=64, activation="relu")
+            k.layer_dense(model, units=10)
+            k.compile(model, loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tf.keras.optimizers.SGD(learning_rate=0.001), metrics="accuracy")
+        result = k.fit(model, x_train, y_train, batch_size=batch_size, epochs=3, steps_per_epoch=5, verbose=0)
+        return str(max(result.metrics["accuracy"]))
+    except Exception as e:  # error = function(e) e$message
+        return str(e)
+
+
+@pytest.mark.timeout(300)
+def test_spark_apply_barrier_readme_closure(monkeypatch):
+    monkeypatch.setenv("SPARK_PORT_BASE", str(launch.free_port_base(4)))
+    sdf = launch.sdf_len(3, repartition=3)
+    rows = launch.collect(launch.spark_apply(sdf, _spark_closure, barrier=True, columns={"address": "character"},
+                                             timeout=240))
+    assert len(rows) == 3
+    vals = [r["address"] for r in rows]
+    # every worker reports the identical (global) accuracy, like README.md:229-231
+    assert len(set(vals)) == 1, vals
+    assert 0.0 <= float(vals[0]) <= 1.0
+
+
+def test_bench_two_ranks_cpu(tmp_path):
+    """bench.py's multi-rank contract on CPU/gloo (torch.distributed.run, 127.0.0.1)."""
+    port = launch.free_port_base(1)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--engine", "generic"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300,
+                       env={**os.environ, "DAMD_DEVICE": "cpu", "OMP_NUM_THREADS": "2", "PYTHONPATH": ROOT})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 128 and out["config"]["parallelism"] == "dp2"
+    assert out["value"] > 0 and out["steps"] == 3 and out["scaling"] == "weak"
