@@ -131,11 +131,12 @@ class FusedConvNetEngine(Engine):
             bufs["stamps"] = self.stamps.data_ptr()
         self.trainer = C.ConvNetTrainer(dev.index or 0, bufs, B, self.PP, 1)
         native = strategy.communicator.native if self.world > 1 else None
+        # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
+        # time, the gradient/metric buffer all-reduced through the host between steps
+        self.host_collective = self.world > 1 and native is None
         if native is not None:
             self.trainer.set_comm(native)
-        elif self.world > 1:
-            raise RuntimeError("fused engine needs the native RCCL communicator for world > 1 (DAMD_COMM=rccl)")
-        self.use_graph = env.get_bool("DAMD_GRAPH", True)
+        self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph_steps = max(1, env.get_int("DAMD_GRAPH_STEPS", 20))
         self.watchdog_s = env.get_float("DAMD_WATCHDOG_S", 0.0)
         opt._iter_source = self._iterations
@@ -224,6 +225,15 @@ class FusedConvNetEngine(Engine):
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
 
     def run(self, n_steps):
+        if self.host_collective:
+            for _ in range(n_steps):
+                self.trainer.step(1)
+                self.trainer.sync(0.0)
+                self.strategy.communicator.allreduce_(self.G, "sum")
+                torch.cuda.synchronize(self.device)
+            self._pending = True
+            self.steps_done += n_steps
+            return
         if self.use_graph and n_steps >= self.graph_steps:
             self.trainer.capture(self.graph_steps)
         if self.use_graph:

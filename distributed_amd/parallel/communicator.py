@@ -89,11 +89,17 @@ class TorchCommunicator(Communicator):
 
     name = "torch"
 
-    def __init__(self, world_size: int, rank: int, data_group=None):
+    def __init__(self, world_size: int, rank: int, data_group=None, host_staging: bool = False):
         self.world_size, self.rank = world_size, rank
         self._data_group = data_group  # None -> default (gloo) group
+        self.host_staging = host_staging
 
     def allreduce_(self, t, op="sum"):
+        if self._staged(t):
+            h = t.detach().cpu()
+            self.allreduce_(h, op)
+            t.copy_(h)
+            return t
         if op == "avg":
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self._group_for(t))
             t.div_(self.world_size)
@@ -102,8 +108,18 @@ class TorchCommunicator(Communicator):
         return t
 
     def broadcast_(self, t, root=0):
+        if self._staged(t):
+            h = t.detach().cpu()
+            dist.broadcast(h, src=root)
+            t.copy_(h)
+            return t
         dist.broadcast(t, src=root, group=self._group_for(t))
         return t
+
+    def _staged(self, t):
+        # DAMD_COMM=gloo on a GPU: device tensors go through host memory (test/debug mode,
+        # e.g. several ranks sharing one GPU, which RCCL does not allow)
+        return t.is_cuda and self._data_group is None and self.host_staging
 
     def allgather(self, t):
         out = [torch.empty_like(t) for _ in range(self.world_size)]
@@ -214,6 +230,8 @@ def make_communicator(world_size: int, rank: int, device: torch.device, kind: Op
                 dlog.warning("size-1 RCCL communicator unavailable (%s); using loopback", e)
         return LoopbackCommunicator()
     if device.type == "cuda":
+        if kind == "gloo":
+            return TorchCommunicator(world_size, rank, host_staging=True)
         if kind == "torch":
             grp = dist.new_group(backend="nccl")
             return TorchCommunicator(world_size, rank, data_group=grp)

@@ -45,7 +45,9 @@ def main():
     h = model.fit(x_train, y_train, batch_size=batch_size, epochs=epochs, steps_per_epoch=steps, verbose=0)
     np.savez(os.path.join(out, f"rank{rank}.npz"), *model.get_weights())
     with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        eng = getattr(model, "_engine", None)
         json.dump({"history": h.history, "world": num_workers, "rank": rank,
+                   "engine": getattr(eng, "name", None),
                    "iterations": int(model.optimizer.iterations)}, f)
     if rank == 0:
         np.savez(os.path.join(out, "init0.npz"), *init)
