@@ -1,0 +1,32 @@
+// Generic bf16 MFMA GEMM / implicit-GEMM convolution (csrc/kernels/gemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace damd {
+
+enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4 };
+enum GemmBMode { B_NC = 0, B_KC = 1 };
+enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32 };
+
+struct GemmArgs {
+  const void* A;       // bf16
+  const void* B;       // bf16
+  void* C;             // fp32 or bf16 (E_BF16)
+  const float* bias;   // [N] (E_BIAS)
+  float* stats;        // [M-tiles][splits][2][N] partial column sum / sumsq (E_STATS)
+  const void* R;       // bf16 [M][ldc] added to the result (E_ADD; may alias C)
+  int M, N, K;
+  int lda, ldb, ldc;
+  // convolution geometry (A_IM2COL / A_DGRAD / A_WGRAD):
+  //   x [Nimg][H][W][Cin], y [Nimg][Ho][Wo][Cout], kernel KHxKW, stride, pad (top/left)
+  //   A_DGRAD: Cin = Cout (the gathered tensor's channel count)
+  int H, W, Cin, Ho, Wo, KH, KW, stride, pad;
+  int kc;              // B_KC: inner k length per tap
+  int k_per_split;     // multiple of 32
+};
+
+// tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)
+hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int splits, int tile, hipStream_t s);
+int gemm_stats_tile_rows(int tile);
+
+}  // namespace damd

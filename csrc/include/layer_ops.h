@@ -1,0 +1,87 @@
+// Non-GEMM per-layer kernels of the generic path (csrc/kernels/layer_ops.hip).
+// Activations are NHWC bf16 (uint16 storage) with the channel count C a multiple of 8,
+// parameters / statistics fp32.  All launches are stream-ordered on `s`.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace damd {
+
+// BatchNorm (training) ---------------------------------------------------------------
+// partials [T][2][C] (column sum, sum of squares; from the conv GEMM epilogue) ->
+// st[4][C] = mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; moving
+// statistics updated Keras-style (m = m*momentum + batch*(1-momentum), biased variance).
+hipError_t bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta,
+                       float eps, float momentum, float* rmean, float* rvar, float* st, hipStream_t s);
+// y = act(x*scale + shift [+ r | + r*scale2 + shift2])   (res_mode 0 / 1 / 2)
+hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const float* st2, int res_mode,
+                    int relu, uint16_t* y, long M, int C, hipStream_t s);
+// inference: y = act(x*scale + shift) with scale/shift from the moving statistics
+// backward, pass 1: dz = dy * [y > 0] (relu_mask) ; per-block partial sums of dz and
+// dz * xhat -> part [T][2][C]; optionally writes dz (bf16).  Returns T via *T_out.
+hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
+                         const float* st, uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s);
+int bn_bwd_blocks(long M, int C);
+// pass 2: dgamma/dbeta (accumulated into the gradient sinks, may be null) and the
+// coefficients co[3][C] so that dx = a*dz + b + c*xhat
+hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const float* st, const float* gamma,
+                           float* dgamma, float* dbeta, float* co, hipStream_t s);
+// pass 3: dx = a*dz + b + c*xhat, dz recomputed from dy and the relu mask (bf16 out)
+hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
+                        const float* co, uint16_t* dx, long M, int C, hipStream_t s);
+
+// Pooling ----------------------------------------------------------------------------------
+hipError_t maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
+                       int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s);
+hipError_t maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw, int sh,
+                       int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s);
+// global average pool over H*W: x [N][HW][C] bf16 -> y [N][C] (bf16 or fp32)
+hipError_t gap_fwd(const uint16_t* x, int N, int HW, int C, void* y, int y_f32, hipStream_t s);
+hipError_t gap_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* dx, hipStream_t s);
+
+// Elementwise -----------------------------------------------------------------------------
+// dz = dy * [y > 0]  (bf16)
+hipError_t relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, long n, hipStream_t s);
+// out = a + b (bf16)
+hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n, hipStream_t s);
+// fp32 -> bf16
+hipError_t cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t s);
+// uint8 (k) -> bf16(k * scale)
+hipError_t cast_u8_bf16(const uint8_t* x, float scale, uint16_t* y, long n, hipStream_t s);
+// out[n] += sum_m x[m][n]  (x bf16 or fp32, [M][ld])
+hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hipStream_t s);
+
+// Loss --------------------------------------------------------------------------------------
+// Sparse softmax cross-entropy from fp32 logits [B][ld]: dlogits (bf16, [B][K]) =
+// (softmax - onehot) * scale; tail[0] += sum loss, tail[1] += sum correct (argmax ==
+// label, first max wins), tail[2] += B.  labels int32.
+// dlogits shares the row pitch ld of the logits; its padding columns are left untouched.
+hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale,
+                        uint16_t* dlogits, float* tail, hipStream_t s);
+
+// Optimizer ---------------------------------------------------------------------------------
+// flat multi-tensor Keras SGD over the master buffer: P, V fp32 updated from G; Pb = bf16(P)
+hipError_t sgd_flat(float* P, const float* G, float* V, uint16_t* Pb, long n, float lr, float momentum,
+                    int nesterov, hipStream_t s);
+
+// one training step's optimizer tail for the graph-captured generic path: hyper-parameters
+// from ctrl (lr / momentum / nesterov, so a new lr needs no re-capture); block 0 also
+// folds the step's metric tail [loss, correct, count] into the epoch accumulators and
+// advances ctrl->cursor / ctrl->iterations.
+struct Ctrl;
+hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ctrl* ctrl, const float* tail,
+                    hipStream_t s);
+
+// Data / layout glue -------------------------------------------------------------------------
+// the step's rows of the (epoch-permuted) dataset: row = (cursor*global_batch + row0 + i)
+// mod nsamples (cursor from ctrl); x fp32 or uint8 (k / scale, i.e. exactly float32(k/255)
+// for scale 255) [n][HW][Cin] -> bf16
+// [per][HW][Cp] zero-padded channels; labels int32.
+hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, const Ctrl* ctrl, int per,
+                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s);
+// fp32 [R][C1][C2] -> bf16 [R][C1p][C2p] (zero padding)
+hipError_t pad_cast(const float* src, int R, int C1, int C2, int C1p, int C2p, uint16_t* dst, hipStream_t s);
+// dst fp32 [R][C1][C2] += src fp32 [R][C1p][C2p] (the un-padded part)
+hipError_t unpad_add(const float* src, int R, int C1, int C2, int C1p, int C2p, float* dst, hipStream_t s);
+
+}  // namespace damd

@@ -1,0 +1,632 @@
+// Generic bf16 MFMA GEMM / implicit-GEMM convolution for the per-layer (generic) path:
+// Dense fwd/bwd, Conv2D fwd / backprop-input / backprop-filter for any Keras model
+// (ResNet-18 in particular), NHWC activations, Keras weight
+// layouts ([KH][KW][Cin][Cout], [in][out]).
+//
+//   C[M,N] (op)= sum_k A(m,k) * B(k,n)      bf16 operands, fp32 accumulation
+//
+// One kernel template, specialised by how the two operands are addressed:
+//   A_KC     A stored [M][lda], k contiguous              (Dense fwd x, Dense dgrad dy)
+//   A_IM2COL implicit im2col of an NHWC image, k=(kh,kw,ci) (Conv fwd)
+//   A_DGRAD  implicit gather of dy for backprop-input, k=(kh,kw,co), stride 1|2
+//   A_MC     A stored [K][lda], m contiguous (A^T)        (Dense wgrad: x^T)
+//   A_WGRAD  implicit im2col^T, m=(kh,kw,ci), k=output pixel (Conv backprop-filter)
+//   B_NC     B stored [K][ldb], n contiguous              (weights [K][N], dy for wgrad)
+//   B_KC     B(k,n) = Bt[((k/kc)*N + n)*kc + k%kc]         (W^T per tap for dgrads)
+//
+// CDNA4 mapping: 256-thread workgroups (4 waves), every wave owns a 64x64 block of C as
+// 4x4 v_mfma_f32_16x16x32_bf16 tiles, BK = 32.  Operands are staged global->registers->
+// LDS with a register prefetch of tile k+1 during the MFMAs of tile k (double-buffered
+// LDS, one LDS-only barrier per k-step).  k-contiguous sources land in a [rows][32] LDS
+// image read with ds_read_b128; mn-contiguous sources land untransposed in a [32][cols]
+// image and are read with the gfx950 transpose read ds_read_b64_tr_b16 (no transposing
+// stores).  Both images are XOR-swizzled so every fragment read is bank-conflict free
+// (swizzles checked exhaustively against the MI355X LDS lane groups).  The MFMA is issued
+// with swapped operands (C^T = B^T A^T) so each lane ends up with 4 consecutive columns
+// of one row: 8/16-byte vector stores in the epilogue.
+//
+// Epilogue (flags): +bias[n], ReLU, bf16 or fp32 output, fp32 atomic accumulation
+// (split-K), and per-column partial sum / sum of squares of the (pre-ReLU) output per
+// M-block (BatchNorm batch statistics without re-reading the activation).
+#include "damd_common.h"
+#include "gemm.h"
+
+namespace damd {
+namespace {
+
+constexpr int BK = 32;
+constexpr int NT = 256;
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ s16x4 ds_tr16(const void* lds_byte_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)((__attribute__((address_space(3))) char*)(
+          (uintptr_t)lds_byte_ptr)));
+}
+
+// ---- LDS images --------------------------------------------------------------------
+// KC image: [rows][32] bf16, 64-B rows; 16-B chunk c of row r stored at chunk c^((r>>1)&3).
+__device__ __forceinline__ int kc_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
+// MC image: [32][COLS] bf16; chunk (8 cols) ch of row r stored at ch ^ f(r).
+template <int COLS>
+__device__ __forceinline__ int mc_off(int r, int ch) {
+  if constexpr (COLS == 64) return r * 128 + 16 * (ch ^ (((r & 3)) ^ ((r >> 1) & 7)));
+  else return r * (COLS * 2) + 16 * (ch ^ ((((r & 3) << 2) ^ ((r >> 2) & 3)) & (COLS / 8 - 1)));
+}
+
+// ---- per-thread operand loaders ----------------------------------------------------
+// Each loader owns CH chunks (16 B each) of the tile; `load(kt)` fills registers for
+// k-tile starting at k0, `store(lds)` writes them into the LDS image.
+
+// KC-image chunk assignment: chunk c = t&3 of rows (t>>2) + 64*i.
+// MC-image chunk assignment: chunk ch = t % CPR of rows t / CPR + (256/CPR)*i.
+
+struct Geo {
+  int H, W, C, Ho, Wo, KH, KW, stride, pad;
+};
+
+__device__ __forceinline__ uint4 ld16(const uint16_t* p, bool ok, const uint16_t* safe) {
+  uint4 v = *reinterpret_cast<const uint4*>(ok ? p : safe);
+  uint32_t m = ok ? 0xffffffffu : 0u;
+  v.x &= m; v.y &= m; v.z &= m; v.w &= m;
+  return v;
+}
+
+template <int MODE, int ROWS>
+struct ALoader;
+
+// A stored [M][lda], k contiguous
+template <int ROWS>
+struct ALoader<A_KC, ROWS> {
+  static constexpr int CH = ROWS / 64;
+  const uint16_t* base;
+  const uint16_t* p[CH];
+  bool rv[CH];
+  int k;  // this thread's k within the matrix
+  int K;
+  __device__ void init(const GemmArgs& a, int m0, int kbeg) {
+    base = (const uint16_t*)a.A;
+    K = a.K;
+    int t = threadIdx.x;
+    k = kbeg + 8 * (t & 3);
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int m = m0 + (t >> 2) + 64 * i;
+      rv[i] = m < a.M;
+      p[i] = base + (size_t)(rv[i] ? m : 0) * a.lda;
+    }
+  }
+  __device__ void load(uint4* r, int kend) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) r[i] = ld16(p[i] + k, rv[i] && k < kend, base);
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + kc_off((t >> 2) + 64 * i, t & 3)) = r[i];
+  }
+};
+
+// implicit im2col of NHWC x: m = (n, oh, ow), k = (kh, kw, ci), C % 8 == 0
+template <int ROWS>
+struct ALoader<A_IM2COL, ROWS> {
+  static constexpr int CH = ROWS / 64;
+  const uint16_t* base;
+  const uint16_t* img[CH];
+  int ih0[CH], iw0[CH];
+  bool rv[CH];
+  int k, kh, kw, ci;
+  Geo g;
+  __device__ void init(const GemmArgs& a, int m0, int kbeg) {
+    base = (const uint16_t*)a.A;
+    g = Geo{a.H, a.W, a.Cin, a.Ho, a.Wo, a.KH, a.KW, a.stride, a.pad};
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int m = m0 + (t >> 2) + 64 * i;
+      rv[i] = m < a.M;
+      int mm = rv[i] ? m : 0;
+      int ow = mm % g.Wo, tmp = mm / g.Wo, oh = tmp % g.Ho, n = tmp / g.Ho;
+      img[i] = base + (size_t)n * g.H * g.W * g.C;
+      ih0[i] = oh * g.stride - g.pad;
+      iw0[i] = ow * g.stride - g.pad;
+    }
+    k = kbeg + 8 * (t & 3);
+    int tap = k / g.C;
+    ci = k - tap * g.C;
+    kh = tap / g.KW;
+    kw = tap - kh * g.KW;
+  }
+  __device__ void load(uint4* r, int kend) {
+    bool kv = k < kend;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int ih = ih0[i] + kh, iw = iw0[i] + kw;
+      bool ok = kv && rv[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      r[i] = ld16(img[i] + ((size_t)ih * g.W + iw) * g.C + ci, ok, base);
+    }
+  }
+  __device__ void advance() {
+    k += BK;
+    ci += BK;
+    while (ci >= g.C) {
+      ci -= g.C;
+      if (++kw == g.KW) { kw = 0; ++kh; }
+    }
+  }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + kc_off((t >> 2) + 64 * i, t & 3)) = r[i];
+  }
+};
+
+// backprop-input gather of dy [N][Ho][Wo][Cout]: m = (n, ih, iw) of dx, k = (kh, kw, co)
+// dy index oh = (ih + pad - kh) / stride when divisible and in range (stride 1 or 2).
+template <int ROWS>
+struct ALoader<A_DGRAD, ROWS> {
+  static constexpr int CH = ROWS / 64;
+  const uint16_t* base;
+  const uint16_t* img[CH];
+  int ihp[CH], iwp[CH];
+  bool rv[CH];
+  int k, kh, kw, co;
+  Geo g;  // C here = Cout (the k-inner length)
+  __device__ void init(const GemmArgs& a, int m0, int kbeg) {
+    base = (const uint16_t*)a.A;
+    g = Geo{a.H, a.W, a.Cin, a.Ho, a.Wo, a.KH, a.KW, a.stride, a.pad};
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int m = m0 + (t >> 2) + 64 * i;
+      rv[i] = m < a.M;
+      int mm = rv[i] ? m : 0;
+      int iw = mm % g.W, tmp = mm / g.W, ih = tmp % g.H, n = tmp / g.H;
+      img[i] = base + (size_t)n * g.Ho * g.Wo * g.C;
+      ihp[i] = ih + g.pad;
+      iwp[i] = iw + g.pad;
+    }
+    k = kbeg + 8 * (t & 3);
+    int tap = k / g.C;
+    co = k - tap * g.C;
+    kh = tap / g.KW;
+    kw = tap - kh * g.KW;
+  }
+  __device__ void load(uint4* r, int kend) {
+    bool kv = k < kend;
+    int sm = g.stride - 1, sh = g.stride >> 1;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int ohn = ihp[i] - kh, own = iwp[i] - kw;
+      int oh = ohn >> sh, ow = own >> sh;
+      bool ok = kv && rv[i] && ohn >= 0 && own >= 0 && !(ohn & sm) && !(own & sm) && oh < g.Ho && ow < g.Wo;
+      r[i] = ld16(img[i] + ((size_t)oh * g.Wo + ow) * g.C + co, ok, base);
+    }
+  }
+  __device__ void advance() {
+    k += BK;
+    co += BK;
+    while (co >= g.C) {
+      co -= g.C;
+      if (++kw == g.KW) { kw = 0; ++kh; }
+    }
+  }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + kc_off((t >> 2) + 64 * i, t & 3)) = r[i];
+  }
+};
+
+// A stored [K][lda] (m contiguous): MC image [32][ROWS]
+template <int ROWS>
+struct ALoader<A_MC, ROWS> {
+  static constexpr int CPR = ROWS / 8;          // chunks per k-row
+  static constexpr int RPP = NT / CPR;          // k-rows per pass
+  static constexpr int CH = BK / RPP;
+  const uint16_t* base;
+  const uint16_t* p;
+  bool mv;
+  int k, lda;
+  __device__ void init(const GemmArgs& a, int m0, int kbeg) {
+    base = (const uint16_t*)a.A;
+    lda = a.lda;
+    int t = threadIdx.x;
+    int m = m0 + 8 * (t % CPR);
+    mv = m < a.M;
+    p = base + (mv ? m : 0);
+    k = kbeg + t / CPR;
+  }
+  __device__ void load(uint4* r, int kend) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int kk = k + RPP * i;
+      r[i] = ld16(p + (size_t)kk * lda, mv && kk < kend, base);
+    }
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + mc_off<ROWS>(t / CPR + RPP * i, t % CPR)) = r[i];
+  }
+};
+
+// backprop-filter: A(m = (kh,kw,ci), k = output pixel p = (n,oh,ow)) = x[n][oh*s-pad+kh][ow*s-pad+kw][ci]
+template <int ROWS>
+struct ALoader<A_WGRAD, ROWS> {
+  static constexpr int CPR = ROWS / 8;
+  static constexpr int RPP = NT / CPR;
+  static constexpr int CH = BK / RPP;
+  const uint16_t* base;
+  bool mv;
+  int kh, kw, ci;
+  int pn[CH], poh[CH], pow_[CH], pk[CH];
+  Geo g;
+  __device__ void init(const GemmArgs& a, int m0, int kbeg) {
+    base = (const uint16_t*)a.A;
+    g = Geo{a.H, a.W, a.Cin, a.Ho, a.Wo, a.KH, a.KW, a.stride, a.pad};
+    int t = threadIdx.x;
+    int m = m0 + 8 * (t % CPR);
+    mv = m < a.M;
+    int mm = mv ? m : 0;
+    int tap = mm / g.C;
+    ci = mm - tap * g.C;
+    kh = tap / g.KW;
+    kw = tap - kh * g.KW;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int p = kbeg + t / CPR + RPP * i;
+      pk[i] = p;
+      pow_[i] = p % g.Wo;
+      int tmp = p / g.Wo;
+      poh[i] = tmp % g.Ho;
+      pn[i] = tmp / g.Ho;
+    }
+  }
+  __device__ void load(uint4* r, int kend) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int ih = poh[i] * g.stride - g.pad + kh, iw = pow_[i] * g.stride - g.pad + kw;
+      bool ok = mv && pk[i] < kend && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      r[i] = ld16(base + (((size_t)pn[i] * g.H + ih) * g.W + iw) * g.C + ci, ok, base);
+    }
+  }
+  __device__ void advance() {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      pk[i] += BK;
+      pow_[i] += BK;
+      while (pow_[i] >= g.Wo) {
+        pow_[i] -= g.Wo;
+        if (++poh[i] == g.Ho) { poh[i] = 0; ++pn[i]; }
+      }
+    }
+  }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + mc_off<ROWS>(t / CPR + RPP * i, t % CPR)) = r[i];
+  }
+};
+
+template <int MODE, int COLS>
+struct BLoader;
+
+// B stored [K][ldb], n contiguous: MC image [32][COLS]
+template <int COLS>
+struct BLoader<B_NC, COLS> {
+  static constexpr int CPR = COLS / 8;
+  static constexpr int RPP = NT / CPR;
+  static constexpr int CH = BK / RPP;
+  const uint16_t* base;
+  const uint16_t* p;
+  bool nv;
+  int k, ldb;
+  __device__ void init(const GemmArgs& a, int n0, int kbeg) {
+    base = (const uint16_t*)a.B;
+    ldb = a.ldb;
+    int t = threadIdx.x;
+    int n = n0 + 8 * (t % CPR);
+    nv = n < a.N;
+    p = base + (nv ? n : 0);
+    k = kbeg + t / CPR;
+  }
+  __device__ void load(uint4* r, int kend) {
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int kk = k + RPP * i;
+      r[i] = ld16(p + (size_t)kk * ldb, nv && kk < kend, base);
+    }
+  }
+  __device__ void advance() { k += BK; }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + mc_off<COLS>(t / CPR + RPP * i, t % CPR)) = r[i];
+  }
+};
+
+// B(k, n) = Bt[((k / kc) * N + n) * kc + k % kc]: KC image [COLS][32]
+template <int COLS>
+struct BLoader<B_KC, COLS> {
+  static constexpr int CH = COLS / 64;
+  const uint16_t* base;
+  bool nv[CH];
+  int nn[CH];
+  int k, tap, kk, kc, N;
+  __device__ void init(const GemmArgs& a, int n0, int kbeg) {
+    base = (const uint16_t*)a.B;
+    kc = a.kc;
+    N = a.N;
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      int n = n0 + (t >> 2) + 64 * i;
+      nv[i] = n < a.N;
+      nn[i] = nv[i] ? n : 0;
+    }
+    k = kbeg + 8 * (t & 3);
+    tap = k / kc;
+    kk = k - tap * kc;
+  }
+  __device__ void load(uint4* r, int kend) {
+    bool kv = k < kend;
+#pragma unroll
+    for (int i = 0; i < CH; ++i)
+      r[i] = ld16(base + ((size_t)tap * N + nn[i]) * kc + kk, kv && nv[i], base);
+  }
+  __device__ void advance() {
+    k += BK;
+    kk += BK;
+    while (kk >= kc) { kk -= kc; ++tap; }
+  }
+  __device__ void store(char* lds, const uint4* r) {
+    int t = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < CH; ++i) *reinterpret_cast<uint4*>(lds + kc_off((t >> 2) + 64 * i, t & 3)) = r[i];
+  }
+};
+
+template <int MODE> struct IsKC { static constexpr bool v = (MODE == A_KC || MODE == A_IM2COL || MODE == A_DGRAD); };
+
+// fragment for 16 rows/cols starting at r0 of a KC image: lane gets row r0+(l&15), k 8(l>>4)..+7
+__device__ __forceinline__ bf16x8 frag_kc(const char* img, int r0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + kc_off(r0 + (lane & 15), lane >> 4));
+}
+// same fragment from an MC image ([32][COLS], column c0 .. c0+15) via two transpose reads
+template <int COLS>
+__device__ __forceinline__ bf16x8 frag_mc(const char* img, int c0, int lane) {
+  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  int ch = (c0 >> 3) + (p >> 1);
+  s16x4 lo = ds_tr16(img + mc_off<COLS>(8 * g + q, ch) + 8 * (p & 1));
+  s16x4 hi = ds_tr16(img + mc_off<COLS>(8 * g + 4 + q, ch) + 8 * (p & 1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int BM, int BN, int AMODE, int BMODE, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs a) {
+  constexpr int WN = BN / 64, WM = 4 / WN;  // wave grid (each wave 64x64)
+  static_assert(WM * 64 == BM, "tile shape");
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (A_BYTES + B_BYTES)];
+  __shared__ float red[2][4][64];
+
+  // XCD-aware tile order: consecutive workgroups are dispatched round-robin over the 8
+  // XCDs; remap so that the N-tiles of one M-panel (which share the A rows) run on the
+  // same XCD (same L2).
+  const int tiles_n = gridDim.x, tiles = gridDim.x * gridDim.y;
+  int lin = blockIdx.y * tiles_n + blockIdx.x;
+  if ((tiles & 7) == 0) lin = (lin & 7) * (tiles >> 3) + (lin >> 3);
+  const int tn = lin % tiles_n, tm = lin / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // split-K range
+  const int kbeg = blockIdx.z * a.k_per_split;
+  const int kend = min(a.K, kbeg + a.k_per_split);
+  if (kbeg >= kend) return;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+
+  ALoader<AMODE, BM> al;
+  BLoader<BMODE, BN> bl;
+  al.init(a, m0, kbeg);
+  bl.init(a, n0, kbeg);
+  uint4 ra[ALoader<AMODE, BM>::CH], rb[BLoader<BMODE, BN>::CH];
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  al.load(ra, kend);
+  bl.load(rb, kend);
+  al.store(smem, ra);
+  bl.store(smem + A_BYTES, rb);
+  lds_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = smem + (kt & 1) * (A_BYTES + B_BYTES);
+    char* nxt = smem + ((kt + 1) & 1) * (A_BYTES + B_BYTES);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      al.advance();
+      bl.advance();
+      al.load(ra, kend);
+      bl.load(rb, kend);
+    }
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if constexpr (IsKC<AMODE>::v) af[i] = frag_kc(cur, wm * 64 + i * 16, lane);
+      else af[i] = frag_mc<BM>(cur, wm * 64 + i * 16, lane);
+      if constexpr (BMODE == B_KC) bfr[i] = frag_kc(cur + A_BYTES, wn * 64 + i * 16, lane);
+      else bfr[i] = frag_mc<BN>(cur + A_BYTES, wn * 64 + i * 16, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+    if (more) {
+      al.store(nxt, ra);
+      bl.store(nxt + A_BYTES, rb);
+    }
+    lds_barrier();
+  }
+
+  // ---- epilogue: lane holds C[m = rowbase + (l&15)][n = colbase + 4(l>>4) + j] ----
+  float csum[4][4], csq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[j][e] = csq[j][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    const bool mok = m < a.M;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      const bool ok = mok && n < a.N;
+      f32x4 v = acc[i][j];
+      if constexpr (EPI & E_BIAS) {
+        if (n < a.N) {
+          float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+      }
+      if constexpr (EPI & E_ADD) {
+        if (ok) {
+          const uint2 r = *reinterpret_cast<const uint2*>((const uint16_t*)a.R + (size_t)m * a.ldc + n);
+          v[0] += __uint_as_float(r.x << 16);
+          v[1] += __uint_as_float(r.x & 0xffff0000u);
+          v[2] += __uint_as_float(r.y << 16);
+          v[3] += __uint_as_float(r.y & 0xffff0000u);
+        }
+      }
+      if constexpr (EPI & E_STATS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = ok ? v[e] : 0.f;
+          if constexpr (EPI & E_BF16) x = bf2f(f2bf(x));  // statistics of the stored values
+          csum[j][e] += x;
+          csq[j][e] += x * x;
+        }
+      }
+      if constexpr (EPI & E_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (!ok) continue;
+      if constexpr (EPI & E_ATOMIC) {
+        float* c = (float*)a.C + (size_t)m * a.ldc + n;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(c + e, v[e]);
+      } else if constexpr (EPI & E_BF16) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>((uint16_t*)a.C + (size_t)m * a.ldc + n) = pk;
+      } else {
+        *reinterpret_cast<float4*>((float*)a.C + (size_t)m * a.ldc + n) = float4{v[0], v[1], v[2], v[3]};
+      }
+    }
+  }
+  if constexpr (EPI & E_STATS) {
+    // reduce over the 16 rows held by lanes l&15 (xor 1,2,4,8), then over the wave grid's
+    // M direction through LDS; one partial per column per M-tile: stats[tm][2][N]
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int s = 1; s < 16; s <<= 1) {
+          csum[j][e] += __shfl_xor(csum[j][e], s);
+          csq[j][e] += __shfl_xor(csq[j][e], s);
+        }
+      }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int c = j * 16 + 4 * (lane >> 4) + e;  // column within the wave's 64
+          red[0][wave][c] = csum[j][e];
+          red[1][wave][c] = csq[j][e];
+        }
+    }
+    __syncthreads();
+    if (t < BN) {
+      const int wnn = t / 64, c = t % 64;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s += red[0][w * WN + wnn][c];
+        q += red[1][w * WN + wnn][c];
+      }
+      const int n = n0 + t;
+      if (n < a.N) {
+        float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
+        st[n] = s;
+        st[a.N + n] = q;
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int AM, int BMo, int EPI>
+hipError_t launch_t(const GemmArgs& a, int splits, hipStream_t s) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, splits);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, AM, BMo, EPI>), grid, dim3(NT), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int AM, int BMo>
+hipError_t launch_epi(const GemmArgs& a, int epi, int splits, hipStream_t s) {
+  switch (epi) {
+    case 0: return launch_t<BM, BN, AM, BMo, 0>(a, splits, s);
+    case E_BF16: return launch_t<BM, BN, AM, BMo, E_BF16>(a, splits, s);
+    case E_BIAS: return launch_t<BM, BN, AM, BMo, E_BIAS>(a, splits, s);
+    case E_BIAS | E_RELU: return launch_t<BM, BN, AM, BMo, E_BIAS | E_RELU>(a, splits, s);
+    case E_BIAS | E_BF16: return launch_t<BM, BN, AM, BMo, E_BIAS | E_BF16>(a, splits, s);
+    case E_BIAS | E_RELU | E_BF16: return launch_t<BM, BN, AM, BMo, E_BIAS | E_RELU | E_BF16>(a, splits, s);
+    case E_ATOMIC: return launch_t<BM, BN, AM, BMo, E_ATOMIC>(a, splits, s);
+    case E_BF16 | E_STATS: return launch_t<BM, BN, AM, BMo, E_BF16 | E_STATS>(a, splits, s);
+    case E_BF16 | E_ADD: return launch_t<BM, BN, AM, BMo, E_BF16 | E_ADD>(a, splits, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+template <int AM, int BMo>
+hipError_t launch_tile(const GemmArgs& a, int epi, int splits, int tile, hipStream_t s) {
+  if (tile == 1) return launch_epi<256, 64, AM, BMo>(a, epi, splits, s);
+  return launch_epi<128, 128, AM, BMo>(a, epi, splits, s);
+}
+
+}  // namespace
+
+int gemm_stats_tile_rows(int tile) { return tile == 1 ? 256 : 128; }
+
+hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int splits, int tile, hipStream_t s) {
+  if (splits < 1) return hipErrorInvalidValue;
+  if ((epi & E_ATOMIC) && (epi & ~E_ATOMIC)) return hipErrorInvalidValue;
+  const int key = amode * 2 + bmode;
+  switch (key) {
+    case A_KC * 2 + B_NC: return launch_tile<A_KC, B_NC>(a, epi, splits, tile, s);
+    case A_KC * 2 + B_KC: return launch_tile<A_KC, B_KC>(a, epi, splits, tile, s);
+    case A_IM2COL * 2 + B_NC: return launch_tile<A_IM2COL, B_NC>(a, epi, splits, tile, s);
+    case A_DGRAD * 2 + B_KC: return launch_tile<A_DGRAD, B_KC>(a, epi, splits, tile, s);
+    case A_MC * 2 + B_NC: return launch_tile<A_MC, B_NC>(a, epi, splits, tile, s);
+    case A_WGRAD * 2 + B_NC: return launch_tile<A_WGRAD, B_NC>(a, epi, splits, tile, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace damd

@@ -1,0 +1,657 @@
+// Non-GEMM layer kernels of the generic path: BatchNorm (train fwd/bwd, fused residual
+// add + ReLU), max / global-average pooling, ReLU backward, sparse softmax
+// cross-entropy (+accuracy), column sums (bias grads) and the flat multi-tensor SGD
+// that also refreshes the bf16 weight shadow read by the MFMA GEMMs.
+//
+// Layout: NHWC bf16 activations, channel count C % 8 == 0, so every thread moves one
+// 16-byte vector of 8 channels (global_load_dwordx4) and keeps the 8 per-channel
+// parameters in registers.  Statistics are reduced in fp32 per block (LDS), then across
+// blocks in double by a finalize kernel (deterministic, no atomics on the hot reductions).
+#include "damd_common.h"
+#include "layer_ops.h"
+
+namespace damd {
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return uint4{w[0], w[1], w[2], w[3]};
+}
+__device__ __forceinline__ void ld8f(const float* p, float* f) {
+  float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+
+inline int grid_for(long work, int per_block = NT, int cap = 8192) {
+  long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+// ---- BatchNorm -------------------------------------------------------------------------
+// reduce partials [T][2][C] over T in double: grid ceil(C/64), 256 threads (4 T-phases)
+__device__ __forceinline__ void reduce_partials(const float* part, int T, int C, double& s0, double& s1) {
+  __shared__ double red[2][4][64];
+  const int t = threadIdx.x, cl = t & 63, ph = t >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C)
+    for (int i = ph; i < T; i += 4) {
+      a += part[(size_t)i * 2 * C + c];
+      b += part[(size_t)i * 2 * C + C + c];
+    }
+  red[0][ph][cl] = a;
+  red[1][ph][cl] = b;
+  __syncthreads();
+  s0 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
+  s1 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+}
+
+__global__ __launch_bounds__(NT) void bn_finalize_k(const float* part, int T, int C, float count,
+                                                    const float* gamma, const float* beta, float eps, float mom,
+                                                    float* rmean, float* rvar, float* st) {
+  double s0, s1;
+  reduce_partials(part, T, C, s0, s1);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const double mean = s0 / count;
+  double var = s1 / count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float m = (float)mean, v = (float)var;
+  const float inv = rsqrtf(v + eps);
+  const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+  const float sc = g * inv;
+  st[c] = m;
+  st[C + c] = inv;
+  st[2 * C + c] = sc;
+  st[3 * C + c] = b - m * sc;
+  if (rmean) {
+    rmean[c] = rmean[c] * mom + m * (1.f - mom);
+    rvar[c] = rvar[c] * mom + v * (1.f - mom);
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x, const float* __restrict__ st,
+                                                 const uint16_t* __restrict__ r, const float* __restrict__ st2,
+                                                 int res_mode, int relu, uint16_t* __restrict__ y, long n8, int C) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const int c = (int)((i * 8) % C);
+    float xv[8], sc[8], sh[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+    ld8f(st + 2 * C + c, sc);
+    ld8f(st + 3 * C + c, sh);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) xv[e] = xv[e] * sc[e] + sh[e];
+    if (res_mode) {
+      float rv[8];
+      unpack8(reinterpret_cast<const uint4*>(r)[i], rv);
+      if (res_mode == 2) {
+        float sc2[8], sh2[8];
+        ld8f(st2 + 2 * C + c, sc2);
+        ld8f(st2 + 3 * C + c, sh2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rv[e] = rv[e] * sc2[e] + sh2[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] += rv[e];
+    }
+    if (relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = fmaxf(xv[e], 0.f);
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(xv);
+  }
+}
+
+// dz = dy * [y>0]; partial sums of dz and dz*xhat per channel for a contiguous row range
+__global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                      int relu_mask, const uint16_t* __restrict__ x,
+                                                      const float* __restrict__ st, uint16_t* __restrict__ dz_out,
+                                                      float* __restrict__ part, long M, int C, long rows_per_block) {
+  __shared__ float red[2][NT * 8];
+  const int cg = C / 8, t = threadIdx.x;
+  const int rpi = NT / cg;  // rows per iteration
+  const int g = t % cg, rr = t / cg;
+  const int c = g * 8;
+  float s0[8], s1[8], mean[8], inv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
+  ld8f(st + c, mean);
+  ld8f(st + C + c, inv);
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rr < rpi) {
+    for (long row = r0 + rr; row < r1; row += rpi) {
+      const long off = (row * C + c) / 8;
+      float d[8], xv[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[off], d);
+      if (relu_mask) {
+        float yv[8];
+        unpack8(reinterpret_cast<const uint4*>(y)[off], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+        if (dz_out) reinterpret_cast<uint4*>(dz_out)[off] = pack8(d);
+      }
+      unpack8(reinterpret_cast<const uint4*>(x)[off], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s0[e] += d[e];
+        s1[e] += d[e] * (xv[e] - mean[e]) * inv[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][t * 8 + e] = rr < rpi ? s0[e] : 0.f;
+    red[1][t * 8 + e] = rr < rpi ? s1[e] : 0.f;
+  }
+  __syncthreads();
+  // thread t < C sums channel t over the rpi row groups: element (rr*cg + g)*8 + e, c = 8g+e
+  for (int ch = t; ch < C; ch += NT) {
+    const int gg = ch / 8, e = ch % 8;
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < rpi; ++q) {
+      a += red[0][(q * cg + gg) * 8 + e];
+      b += red[1][(q * cg + gg) * 8 + e];
+    }
+    part[(size_t)blockIdx.x * 2 * C + ch] = a;
+    part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_k(const float* part, int T, int C, float count,
+                                                        const float* st, float* dgamma, float* dbeta, float* co) {
+  double s0, s1;
+  reduce_partials(part, T, C, s0, s1);
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const float db = (float)s0, dg = (float)s1;
+  if (dbeta) dbeta[c] += db;
+  if (dgamma) dgamma[c] += dg;
+  const float a = st[2 * C + c];
+  co[c] = a;
+  co[C + c] = -a * db / count;
+  co[2 * C + c] = -a * dg / count;
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_apply_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                     int relu_mask, const uint16_t* __restrict__ x,
+                                                     const float* __restrict__ st, const float* __restrict__ co,
+                                                     uint16_t* __restrict__ dx, long n8, int C) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const int c = (int)((i * 8) % C);
+    float d[8], xv[8], mean[8], inv[8], a[8], b[8], cc[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+    if (relu_mask) {
+      float yv[8];
+      unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+    }
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+    ld8f(st + c, mean);
+    ld8f(st + C + c, inv);
+    ld8f(co + c, a);
+    ld8f(co + C + c, b);
+    ld8f(co + 2 * C + c, cc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = a[e] * d[e] + b[e] + cc[e] * (xv[e] - mean[e]) * inv[e];
+    reinterpret_cast<uint4*>(dx)[i] = pack8(d);
+  }
+}
+
+// ---- pooling -----------------------------------------------------------------------------
+struct PoolGeo {
+  int N, H, W, C, ph, pw, sh, sw, pt, pl, Ho, Wo;
+};
+
+__global__ __launch_bounds__(NT) void maxpool_fwd_k(const uint16_t* __restrict__ x, PoolGeo g,
+                                                    uint16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int cg = g.C / 8;
+  const long total = (long)g.N * g.Ho * g.Wo * cg;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    long pix = i / cg;
+    const int ow = (int)(pix % g.Wo);
+    pix /= g.Wo;
+    const int oh = (int)(pix % g.Ho);
+    const int n = (int)(pix / g.Ho);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int kh = 0; kh < g.ph; ++kh) {
+      const int ih = oh * g.sh - g.pt + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.pw; ++kw) {
+        const int iw = ow * g.sw - g.pl + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float v[8];
+        unpack8(reinterpret_cast<const uint4*>(x)[(((long)n * g.H + ih) * g.W + iw) * cg + c8], v);
+        const uint8_t idx = (uint8_t)(kh * g.pw + kw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; bi[e] = idx; }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    reinterpret_cast<uint2*>(arg)[i] = a;
+  }
+}
+
+__global__ __launch_bounds__(NT) void maxpool_bwd_k(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                                    PoolGeo g, uint16_t* __restrict__ dx) {
+  const int cg = g.C / 8;
+  const long total = (long)g.N * g.H * g.W * cg;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    long pix = i / cg;
+    const int iw = (int)(pix % g.W);
+    pix /= g.W;
+    const int ih = (int)(pix % g.H);
+    const int n = (int)(pix / g.H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // output rows whose window covers ih: oh*sh - pt <= ih <= oh*sh - pt + ph - 1
+    const int ohlo = max(0, (ih + g.pt - g.ph + g.sh) / g.sh), ohhi = min(g.Ho - 1, (ih + g.pt) / g.sh);
+    const int owlo = max(0, (iw + g.pl - g.pw + g.sw) / g.sw), owhi = min(g.Wo - 1, (iw + g.pl) / g.sw);
+    for (int oh = ohlo; oh <= ohhi; ++oh) {
+      const int kh = ih - (oh * g.sh - g.pt);
+      if (kh < 0 || kh >= g.ph) continue;
+      for (int ow = owlo; ow <= owhi; ++ow) {
+        const int kw = iw - (ow * g.sw - g.pl);
+        if (kw < 0 || kw >= g.pw) continue;
+        const long o = (((long)n * g.Ho + oh) * g.Wo + ow) * cg + c8;
+        const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+        const uint8_t me = (uint8_t)(kh * g.pw + kw);
+        float d[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+        const uint32_t w[2] = {a.x, a.y};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (((w[e >> 2] >> (8 * (e & 3))) & 0xff) == me) acc[e] += d[e];
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(NT) void gap_fwd_k(const uint16_t* __restrict__ x, int N, int HW, int C, void* y,
+                                                int y_f32) {
+  const int cg = C / 8;
+  const long total = (long)N * cg;
+  const float inv = 1.f / HW;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg), n = (int)(i / cg);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int p = 0; p < HW; ++p) {
+      float v[8];
+      unpack8(reinterpret_cast<const uint4*>(x)[((long)n * HW + p) * cg + c8], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    if (y_f32) {
+      float* o = (float*)y + (long)n * C + c8 * 8;
+      *reinterpret_cast<float4*>(o) = float4{acc[0], acc[1], acc[2], acc[3]};
+      *reinterpret_cast<float4*>(o + 4) = float4{acc[4], acc[5], acc[6], acc[7]};
+    } else {
+      reinterpret_cast<uint4*>(y)[i] = pack8(acc);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void gap_bwd_k(const void* dy, int dy_f32, int N, int HW, int C,
+                                                uint16_t* __restrict__ dx) {
+  const int cg = C / 8;
+  const long total = (long)N * HW * cg;
+  const float inv = 1.f / HW;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    const int n = (int)(i / ((long)cg * HW));
+    float d[8];
+    if (dy_f32) ld8f((const float*)dy + (long)n * C + c8 * 8, d);
+    else unpack8(reinterpret_cast<const uint4*>(dy)[(long)n * cg + c8], d);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] *= inv;
+    reinterpret_cast<uint4*>(dx)[i] = pack8(d);
+  }
+}
+
+// ---- elementwise ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void relu_bwd_k(const uint16_t* dy, const uint16_t* y, uint16_t* dz, long n8) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float d[8], yv[8];
+    unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+    reinterpret_cast<uint4*>(dz)[i] = pack8(d);
+  }
+}
+
+__global__ __launch_bounds__(NT) void add_bf16_k(const uint16_t* a, const uint16_t* b, uint16_t* o, long n8) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    float x[8], y[8];
+    unpack8(reinterpret_cast<const uint4*>(a)[i], x);
+    unpack8(reinterpret_cast<const uint4*>(b)[i], y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] += y[e];
+    reinterpret_cast<uint4*>(o)[i] = pack8(x);
+  }
+}
+
+__global__ __launch_bounds__(NT) void cast_f32_bf16_k(const float* x, uint16_t* y, long n) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) y[i] = f2bf(x[i]);
+}
+
+__global__ __launch_bounds__(NT) void cast_u8_bf16_k(const uint8_t* x, float scale, uint16_t* y, long n) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT)
+    y[i] = f2bf((float)x[i] * scale);
+}
+
+// out[n] += sum over rows; grid (ceil(N/64), splits), 4 row phases per block
+__global__ __launch_bounds__(NT) void colsum_k(const void* x, int x_f32, int M, int N, int ld, float* out) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + cl;
+  float a = 0.f;
+  if (n < N)
+    for (int m = blockIdx.y * 4 + ph; m < M; m += gridDim.y * 4)
+      a += x_f32 ? ((const float*)x)[(size_t)m * ld + n] : bf2f(((const uint16_t*)x)[(size_t)m * ld + n]);
+  red[ph][cl] = a;
+  __syncthreads();
+  if (ph == 0 && n < N) atomicAdd(out + n, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+}
+
+// ---- loss ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ logits, int ld,
+                                                     const int32_t* __restrict__ labels, int K, float scale,
+                                                     uint16_t* __restrict__ dl, float* tail) {
+  __shared__ float sv[NT];
+  __shared__ int si[NT];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const float* z = logits + (size_t)b * ld;
+  float mx = -INFINITY;
+  int mi = 0x7fffffff;
+  for (int k = t; k < K; k += NT) {
+    const float v = z[k];
+    if (v > mx) { mx = v; mi = k; }
+  }
+  sv[t] = mx;
+  si[t] = mi;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (t < s) {
+      const float o = sv[t + s];
+      const int oi = si[t + s];
+      if (o > sv[t] || (o == sv[t] && oi < si[t])) { sv[t] = o; si[t] = oi; }
+    }
+    __syncthreads();
+  }
+  const float zmax = sv[0];
+  const int amax = si[0];
+  __syncthreads();
+  float se = 0.f;
+  for (int k = t; k < K; k += NT) se += __expf(z[k] - zmax);
+  sv[t] = se;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (t < s) sv[t] += sv[t + s];
+    __syncthreads();
+  }
+  const float sum = sv[0];
+  const int y = labels[b];
+  const float inv = 1.f / sum;
+  for (int k = t; k < K; k += NT) {
+    const float p = __expf(z[k] - zmax) * inv;
+    dl[(size_t)b * ld + k] = f2bf((p - (k == y ? 1.f : 0.f)) * scale);
+  }
+  if (t == 0) {
+    const float loss = logf(sum) + zmax - z[y];
+    atomicAdd(tail, loss);
+    atomicAdd(tail + 1, amax == y ? 1.f : 0.f);
+    atomicAdd(tail + 2, 1.f);
+  }
+}
+
+// ---- optimizer ------------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void sgd_flat_k(float* __restrict__ P, const float* __restrict__ G,
+                                                 float* __restrict__ V, uint16_t* __restrict__ Pb, long n, float lr,
+                                                 float mom, int nest) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    float wn, vn;
+    sgd_update(P[i], G[i], V ? V[i] : 0.f, lr, mom, nest, wn, vn);
+    P[i] = wn;
+    if (V) V[i] = vn;
+    if (Pb) Pb[i] = f2bf(wn);
+  }
+}
+
+__global__ __launch_bounds__(NT) void sgd_step_k(float* __restrict__ P, const float* __restrict__ G,
+                                                 float* __restrict__ V, uint16_t* __restrict__ Pb, long n,
+                                                 Ctrl* ctrl, const float* tail) {
+  const float lr = ctrl->lr, mom = ctrl->momentum;
+  const int nest = ctrl->nesterov;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    float wn, vn;
+    sgd_update(P[i], G[i], mom != 0.f ? V[i] : 0.f, lr, mom, nest, wn, vn);
+    P[i] = wn;
+    if (mom != 0.f) V[i] = vn;
+    Pb[i] = f2bf(wn);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctrl->acc_loss += tail[0];
+    ctrl->acc_correct += tail[1];
+    ctrl->acc_count += tail[2];
+    int c = ctrl->cursor + 1;
+    if (ctrl->wrap > 0 && c >= ctrl->wrap) c = 0;
+    ctrl->cursor = c;
+    ctrl->iterations += 1;
+  }
+}
+
+__global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x, int x_u8, float scale,
+                                                     const int32_t* __restrict__ labels, const Ctrl* __restrict__ ctrl,
+                                                     int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
+                                                     int32_t* __restrict__ yb) {
+  const long total = (long)per * HW * Cp;
+  const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
+  const int n = ctrl->nsamples;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c = (int)(i % Cp);
+    const long pr = i / Cp;
+    const int p = (int)(pr % HW), r = (int)(pr / HW);
+    const long row = (base + r) % n;
+    float v = 0.f;
+    if (c < Cin) {
+      const long si = (row * HW + p) * Cin + c;
+      v = x_u8 ? (float)((const uint8_t*)x)[si] / scale : ((const float*)x)[si];
+    }
+    xb[i] = f2bf(v);
+    if (p == 0 && c == 0) yb[r] = labels[row];
+  }
+}
+
+__global__ __launch_bounds__(NT) void pad_cast_k(const float* src, int R, int C1, int C2, int C1p, int C2p,
+                                                 uint16_t* dst) {
+  const long total = (long)R * C1p * C2p;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c2 = (int)(i % C2p);
+    const long t = i / C2p;
+    const int c1 = (int)(t % C1p), r = (int)(t / C1p);
+    dst[i] = (c1 < C1 && c2 < C2) ? f2bf(src[((long)r * C1 + c1) * C2 + c2]) : (uint16_t)0;
+  }
+}
+
+__global__ __launch_bounds__(NT) void unpad_add_k(const float* src, int R, int C1, int C2, int C1p, int C2p,
+                                                  float* dst) {
+  const long total = (long)R * C1 * C2;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c2 = (int)(i % C2);
+    const long t = i / C2;
+    const int c1 = (int)(t % C1), r = (int)(t / C1);
+    dst[i] += src[((long)r * C1p + c1) * C2p + c2];
+  }
+}
+
+}  // namespace
+
+hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ctrl* ctrl, const float* tail,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(sgd_step_k, dim3(grid_for(n, NT, 4096)), dim3(NT), 0, s, P, G, V, Pb, n, ctrl, tail);
+  return hipGetLastError();
+}
+
+hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, const Ctrl* ctrl, int per,
+                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s) {
+  hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp)), dim3(NT), 0, s, x, x_u8, scale, labels,
+                     ctrl, per, HW, Cin, Cp, xb, yb);
+  return hipGetLastError();
+}
+
+hipError_t pad_cast(const float* src, int R, int C1, int C2, int C1p, int C2p, uint16_t* dst, hipStream_t s) {
+  hipLaunchKernelGGL(pad_cast_k, dim3(grid_for((long)R * C1p * C2p)), dim3(NT), 0, s, src, R, C1, C2, C1p, C2p, dst);
+  return hipGetLastError();
+}
+
+hipError_t unpad_add(const float* src, int R, int C1, int C2, int C1p, int C2p, float* dst, hipStream_t s) {
+  hipLaunchKernelGGL(unpad_add_k, dim3(grid_for((long)R * C1 * C2)), dim3(NT), 0, s, src, R, C1, C2, C1p, C2p, dst);
+  return hipGetLastError();
+}
+
+hipError_t bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
+                       float momentum, float* rmean, float* rvar, float* st, hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_k, dim3((C + 63) / 64), dim3(NT), 0, s, part, T, C, count, gamma, beta, eps,
+                     momentum, rmean, rvar, st);
+  return hipGetLastError();
+}
+
+hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const float* st2, int res_mode, int relu,
+                    uint16_t* y, long M, int C, hipStream_t s) {
+  const long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, x, st, r, st2, res_mode, relu, y, n8, C);
+  return hipGetLastError();
+}
+
+int bn_bwd_blocks(long M, int C) {
+  const int rpi = NT / (C / 8);
+  long rows = (M + 1023) / 1024;
+  if (rows < rpi) rows = rpi;
+  return (int)((M + rows - 1) / rows);
+}
+
+hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
+                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s) {
+  if (C % 8 || C / 8 > NT) return hipErrorInvalidValue;
+  const long rows = (M + T - 1) / T;
+  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const float* st, const float* gamma,
+                           float* dgamma, float* dbeta, float* co, hipStream_t s) {
+  (void)gamma;
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(NT), 0, s, part, T, C, count, st, dgamma, dbeta,
+                     co);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
+                        const float* co, uint16_t* dx, long M, int C, hipStream_t s) {
+  const long n8 = M * C / 8;
+  hipLaunchKernelGGL(bn_bwd_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, dy, y, relu_mask, x, st, co, dx, n8, C);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
+                       int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s) {
+  if (C % 8 || ph * pw > 255) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  hipLaunchKernelGGL(maxpool_fwd_k, dim3(grid_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0, s, x, g, y, arg);
+  return hipGetLastError();
+}
+
+hipError_t maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw, int sh,
+                       int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  hipLaunchKernelGGL(maxpool_bwd_k, dim3(grid_for((long)N * H * W * C / 8)), dim3(NT), 0, s, dy, arg, g, dx);
+  return hipGetLastError();
+}
+
+hipError_t gap_fwd(const uint16_t* x, int N, int HW, int C, void* y, int y_f32, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gap_fwd_k, dim3(grid_for((long)N * C / 8)), dim3(NT), 0, s, x, N, HW, C, y, y_f32);
+  return hipGetLastError();
+}
+
+hipError_t gap_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* dx, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gap_bwd_k, dim3(grid_for((long)N * HW * C / 8)), dim3(NT), 0, s, dy, dy_f32, N, HW, C, dx);
+  return hipGetLastError();
+}
+
+hipError_t relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, long n, hipStream_t s) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(relu_bwd_k, dim3(grid_for(n / 8)), dim3(NT), 0, s, dy, y, dz, n / 8);
+  return hipGetLastError();
+}
+
+hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n, hipStream_t s) {
+  if (n % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(add_bf16_k, dim3(grid_for(n / 8)), dim3(NT), 0, s, a, b, out, n / 8);
+  return hipGetLastError();
+}
+
+hipError_t cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_k, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t cast_u8_bf16(const uint8_t* x, float scale, uint16_t* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_u8_bf16_k, dim3(grid_for(n)), dim3(NT), 0, s, x, scale, y, n);
+  return hipGetLastError();
+}
+
+hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hipStream_t s) {
+  int splits = (M + 255) / 256;
+  if (splits > 64) splits = 64;
+  if (splits < 1) splits = 1;
+  hipLaunchKernelGGL(colsum_k, dim3((N + 63) / 64, splits), dim3(NT), 0, s, x, x_f32, M, N, ld, out);
+  return hipGetLastError();
+}
+
+hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale,
+                        uint16_t* dlogits, float* tail, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, dlogits, tail);
+  return hipGetLastError();
+}
+
+hipError_t sgd_flat(float* P, const float* G, float* V, uint16_t* Pb, long n, float lr, float momentum, int nesterov,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(sgd_flat_k, dim3(grid_for(n, NT, 4096)), dim3(NT), 0, s, P, G, momentum != 0.f ? V : nullptr,
+                     Pb, n, lr, momentum, nesterov);
+  return hipGetLastError();
+}
+
+}  // namespace damd

@@ -1,11 +1,148 @@
-// Per-layer HIP kernel ops (generic Keras path).  Pointers in, pointers out; shapes are
-// validated on the Python side (distributed_amd/ops/) before any launch.
+// Per-layer HIP kernel ops (generic Keras path).  Pointers in, pointers out; shapes,
+// dtypes, alignment and contiguity are validated on the Python side
+// (distributed_amd/ops/hip.py) before any launch.  Every op is enqueued on the caller's
+// stream (torch's current stream), so it is captured by torch.cuda graphs.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
+#include <stdexcept>
+#include <string>
+
+#include "gemm.h"
 #include "kernels_api.h"
+#include "damd_common.h"
+#include "layer_ops.h"
 
 namespace py = pybind11;
 
+namespace {
+template <typename T>
+T* P_(uintptr_t p) { return reinterpret_cast<T*>(p); }
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
 void register_kernel_ops(py::module_& m) {
-  (void)m;
+  m.def(
+      "gemm",
+      [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,
+         uintptr_t stats, uintptr_t R, int M, int N, int K, int lda, int ldb, int ldc, std::vector<int> geo, int kc,
+         int k_per_split, uintptr_t stream) {
+        damd::GemmArgs a{};
+        a.A = P_<const void>(A);
+        a.B = P_<const void>(B);
+        a.C = P_<void>(C);
+        a.bias = P_<const float>(bias);
+        a.stats = P_<float>(stats);
+        a.R = P_<const void>(R);
+        a.M = M; a.N = N; a.K = K;
+        a.lda = lda; a.ldb = ldb; a.ldc = ldc;
+        if (geo.size() == 9) {
+          a.H = geo[0]; a.W = geo[1]; a.Cin = geo[2]; a.Ho = geo[3]; a.Wo = geo[4];
+          a.KH = geo[5]; a.KW = geo[6]; a.stride = geo[7]; a.pad = geo[8];
+        } else if (!geo.empty()) {
+          throw std::invalid_argument("geo must be [H, W, C, Ho, Wo, KH, KW, stride, pad]");
+        }
+        a.kc = kc;
+        a.k_per_split = k_per_split;
+        check(damd::gemm_launch(a, amode, bmode, epi, splits, tile, P_<ihipStream_t>(stream)), "gemm");
+      },
+      py::arg("amode"), py::arg("bmode"), py::arg("epi"), py::arg("splits"), py::arg("tile"), py::arg("A"),
+      py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("stats"), py::arg("R"), py::arg("M"), py::arg("N"), py::arg("K"),
+      py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
+      py::arg("stream"));
+  m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
+
+  using U = uintptr_t;
+  using u16 = uint16_t;
+  m.def("bn_finalize", [](U part, int T, int C, float count, U gamma, U beta, float eps, float mom, U rmean, U rvar,
+                          U st, U s) {
+    check(damd::bn_finalize(P_<const float>(part), T, C, count, P_<const float>(gamma), P_<const float>(beta), eps,
+                            mom, P_<float>(rmean), P_<float>(rvar), P_<float>(st), P_<ihipStream_t>(s)),
+          "bn_finalize");
+  });
+  m.def("bn_apply", [](U x, U st, U r, U st2, int res_mode, int relu, U y, long M, int C, U s) {
+    check(damd::bn_apply(P_<const u16>(x), P_<const float>(st), P_<const u16>(r), P_<const float>(st2), res_mode,
+                         relu, P_<u16>(y), M, C, P_<ihipStream_t>(s)),
+          "bn_apply");
+  });
+  m.def("bn_bwd_blocks", &damd::bn_bwd_blocks);
+  m.def("bn_bwd_reduce", [](U dy, U y, int relu_mask, U x, U st, U dz, U part, int T, long M, int C, U s) {
+    check(damd::bn_bwd_reduce(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
+                              P_<u16>(dz), P_<float>(part), T, M, C, P_<ihipStream_t>(s)),
+          "bn_bwd_reduce");
+  });
+  m.def("bn_bwd_finalize", [](U part, int T, int C, float count, U st, U gamma, U dgamma, U dbeta, U co, U s) {
+    check(damd::bn_bwd_finalize(P_<const float>(part), T, C, count, P_<const float>(st), P_<const float>(gamma),
+                                P_<float>(dgamma), P_<float>(dbeta), P_<float>(co), P_<ihipStream_t>(s)),
+          "bn_bwd_finalize");
+  });
+  m.def("bn_bwd_apply", [](U dy, U y, int relu_mask, U x, U st, U co, U dx, long M, int C, U s) {
+    check(damd::bn_bwd_apply(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
+                             P_<const float>(co), P_<u16>(dx), M, C, P_<ihipStream_t>(s)),
+          "bn_bwd_apply");
+  });
+  m.def("maxpool_fwd", [](U x, std::vector<int> g, U y, U arg, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::maxpool_fwd(P_<const u16>(x), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10],
+                            g[11], P_<u16>(y), P_<uint8_t>(arg), P_<ihipStream_t>(s)),
+          "maxpool_fwd");
+  });
+  m.def("maxpool_bwd", [](U dy, U arg, std::vector<int> g, U dx, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::maxpool_bwd(P_<const u16>(dy), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
+                            g[7], g[8], g[9], g[10], g[11], P_<u16>(dx), P_<ihipStream_t>(s)),
+          "maxpool_bwd");
+  });
+  m.def("gap_fwd", [](U x, int N, int HW, int C, U y, int y_f32, U s) {
+    check(damd::gap_fwd(P_<const u16>(x), N, HW, C, P_<void>(y), y_f32, P_<ihipStream_t>(s)), "gap_fwd");
+  });
+  m.def("gap_bwd", [](U dy, int dy_f32, int N, int HW, int C, U dx, U s) {
+    check(damd::gap_bwd(P_<const void>(dy), dy_f32, N, HW, C, P_<u16>(dx), P_<ihipStream_t>(s)), "gap_bwd");
+  });
+  m.def("relu_bwd", [](U dy, U y, U dz, long n, U s) {
+    check(damd::relu_bwd(P_<const u16>(dy), P_<const u16>(y), P_<u16>(dz), n, P_<ihipStream_t>(s)), "relu_bwd");
+  });
+  m.def("add_bf16", [](U a, U b, U o, long n, U s) {
+    check(damd::add_bf16(P_<const u16>(a), P_<const u16>(b), P_<u16>(o), n, P_<ihipStream_t>(s)), "add_bf16");
+  });
+  m.def("cast_f32_bf16", [](U x, U y, long n, U s) {
+    check(damd::cast_f32_bf16(P_<const float>(x), P_<u16>(y), n, P_<ihipStream_t>(s)), "cast_f32_bf16");
+  });
+  m.def("cast_u8_bf16", [](U x, float scale, U y, long n, U s) {
+    check(damd::cast_u8_bf16(P_<const uint8_t>(x), scale, P_<u16>(y), n, P_<ihipStream_t>(s)), "cast_u8_bf16");
+  });
+  m.def("colsum", [](U x, int x_f32, int M, int N, int ld, U out, U s) {
+    check(damd::colsum(P_<const void>(x), x_f32, M, N, ld, P_<float>(out), P_<ihipStream_t>(s)), "colsum");
+  });
+  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U dl, U tail, U s) {
+    check(damd::softmax_xent(P_<const float>(logits), ld, P_<const int32_t>(labels), B, K, scale, P_<u16>(dl),
+                             P_<float>(tail), P_<ihipStream_t>(s)),
+          "softmax_xent");
+  });
+  m.def("sgd_step", [](U P, U G, U V, U Pb, long n, U ctrl, U tail, U s) {
+    check(damd::sgd_step(P_<float>(P), P_<const float>(G), P_<float>(V), P_<u16>(Pb), n, P_<damd::Ctrl>(ctrl),
+                         P_<const float>(tail), P_<ihipStream_t>(s)),
+          "sgd_step");
+  });
+  m.def("gather_batch", [](U x, int x_u8, float scale, U labels, U ctrl, int per, int HW, int Cin, int Cp, U xb, U yb,
+                           U s) {
+    check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<const damd::Ctrl>(ctrl),
+                             per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s)),
+          "gather_batch");
+  });
+  m.def("pad_cast", [](U src, int R, int C1, int C2, int C1p, int C2p, U dst, U s) {
+    check(damd::pad_cast(P_<const float>(src), R, C1, C2, C1p, C2p, P_<u16>(dst), P_<ihipStream_t>(s)), "pad_cast");
+  });
+  m.def("unpad_add", [](U src, int R, int C1, int C2, int C1p, int C2p, U dst, U s) {
+    check(damd::unpad_add(P_<const float>(src), R, C1, C2, C1p, C2p, P_<float>(dst), P_<ihipStream_t>(s)),
+          "unpad_add");
+  });
+  m.def("sgd_flat", [](U P, U G, U V, U Pb, long n, float lr, float mom, int nest, U s) {
+    check(damd::sgd_flat(P_<float>(P), P_<const float>(G), P_<float>(V), P_<u16>(Pb), n, lr, mom, nest,
+                         P_<ihipStream_t>(s)),
+          "sgd_flat");
+  });
 }

@@ -63,4 +63,11 @@ def select_engine(model, strategy, per_replica: int, global_batch: int) -> Engin
         if ok:
             return FusedConvNetEngine(model, strategy, per_replica, global_batch)
         dlog.debug("fused ConvNet engine not used: %s", why)
+    if env.get_bool("DAMD_NATIVE_GRAPH", True):
+        from .native_graph import NativeGraphEngine
+
+        ok, why = NativeGraphEngine.eligible(model, strategy)
+        if ok:
+            return NativeGraphEngine(model, strategy, per_replica, global_batch)
+        dlog.debug("native graph engine not used: %s", why)
     return GenericEngine(model, strategy, per_replica, global_batch)

@@ -1,0 +1,838 @@
+"""Native graph engine: any supported Keras model lowered to a static plan of HIP kernel
+launches (no autograd, no per-op Python on the hot path), captured as a HIP graph.
+
+This is the generic-model counterpart of the fused MNIST trainer (fused_convnet.py),
+used for ResNet-style networks (BASELINE.json config 4) and any
+other model built from the supported layers.  What happens per step (one rank):
+
+    gather_batch (device cursor, uint8/fp32 -> bf16 NHWC, channel padding)
+    forward:  implicit-GEMM MFMA convs / dense (csrc/kernels/gemm.hip) with bias / ReLU /
+              BatchNorm-statistics epilogues, fused BN(+residual)(+ReLU) apply, pooling
+    loss:     softmax cross-entropy + accuracy -> dlogits and the metric tail of G
+    backward: reverse plan: BN backward (3 passes), pooling backward, dgrad GEMMs
+              (residual fan-in accumulated in the GEMM epilogue), wgrad GEMMs accumulated
+              with fp32 atomics straight into the flat gradient buffer G (split-K)
+    all-reduce G (RCCL, in the graph) -> flat SGD (+momentum) that also refreshes the
+              bf16 weight shadow and advances the device cursor / epoch accumulators.
+
+Memory is planned once at bind time (bf16 activations + gradients for every tensor —
+small next to 288 GB of HBM), so the captured graph replays with no allocation.
+
+Fusion rules (decided on the layer graph, not traced):
+  Conv2D(no bias, linear) -> BatchNormalization : batch statistics from the conv epilogue
+  BatchNormalization -> ReLU                    : ReLU in the BN apply
+  BatchNormalization -> Add(other) [-> ReLU]    : residual add (+ the other branch's own
+                                                  BN when it is BN-terminated) in one pass
+"""
+from __future__ import annotations
+
+import math
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import hip as H
+from ..utils import env
+from ..utils import logging as dlog
+from .base import Engine
+from .data import DataFeed
+
+C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT = 0, 1, 2, 3, 4, 5, 6, 7
+C_AL, C_AC, C_AN, C_WRAP = 10, 11, 12, 13
+
+
+def _f2i(f):
+    return struct.unpack("<i", struct.pack("<f", float(f)))[0]
+
+
+def _i2f(i):
+    return struct.unpack("<f", struct.pack("<i", int(i)))[0]
+
+
+def _pad8(c):
+    return -(-c // 8) * 8
+
+
+@dataclass
+class T:
+    """A planned tensor (per-replica batch)."""
+
+    shape: tuple
+    dtype: torch.dtype = torch.bfloat16
+    buf: Optional[torch.Tensor] = None
+    grad: Optional[torch.Tensor] = None
+    needs_grad: bool = True
+    alias_of: Optional["T"] = None
+    consumers: List["Node"] = field(default_factory=list)
+    written: bool = False  # backward bookkeeping
+
+    def root(self):
+        t = self
+        while t.alias_of is not None:
+            t = t.alias_of
+        return t
+
+
+@dataclass
+class Node:
+    kind: str
+    layer: object
+    inputs: List[T]
+    out: T
+    attrs: Dict = field(default_factory=dict)
+
+
+def _layer_graph(model):
+    """[(layer, [input keys], output key)], input key, output key."""
+    from ..keras import layers as L
+
+    if hasattr(model, "_layers") and not getattr(model, "_nodes", None):
+        ls = [l for l in model._layers if not isinstance(l, L.InputLayer)]
+        seq = []
+        for i, l in enumerate(ls):
+            seq.append((l, [i], i + 1))
+        return seq, 0, len(ls), tuple(model.input_shape[1:])
+    keys = {id(model._inputs[0]): 0}
+    seq = []
+    for t in model._nodes:
+        keys[id(t)] = len(keys)
+        seq.append((t.layer, [keys[id(i)] for i in t.inputs], keys[id(t)]))
+    return seq, 0, keys[id(model._outputs[0])], tuple(model._inputs[0].shape[1:])
+
+
+class NativeGraphEngine(Engine):
+    name = "native_graph"
+
+    SUPPORTED = ("Conv2D", "BatchNormalization", "Activation", "ReLU", "Add", "MaxPooling2D",
+                 "GlobalAveragePooling2D", "Flatten", "Dense")
+
+    @staticmethod
+    def eligible(model, strategy):
+        from ..keras import losses, optimizers
+
+        if strategy.device.type != "cuda":
+            return False, "not on a GPU"
+        if type(model.optimizer) is not optimizers.SGD:
+            return False, "optimizer (SGD only)"
+        if not (isinstance(model.loss, losses.SparseCategoricalCrossentropy) and model.loss.from_logits):
+            return False, "loss"
+        for m in model.compiled_metrics:
+            if m.name not in ("accuracy", "acc", "sparse_categorical_accuracy"):
+                return False, f"metric {m.name}"
+        try:
+            seq, _, out_key, in_shape = _layer_graph(model)
+        except Exception as e:  # pragma: no cover
+            return False, f"graph: {e}"
+        if len(in_shape) != 3:
+            return False, "input must be an image (H, W, C)"
+        for l, ins, _ in seq:
+            k = type(l).__name__
+            if k not in NativeGraphEngine.SUPPORTED:
+                return False, f"layer {k}"
+            act = getattr(l, "activation", None)
+            an = getattr(act, "__name__", "linear") if act is not None else "linear"
+            if k in ("Conv2D", "Dense", "Activation") and an not in ("relu", "linear"):
+                return False, f"activation {an}"
+            if k == "ReLU" and (l.max_value is not None or l.negative_slope or l.threshold):
+                return False, "ReLU options"
+            if k == "Conv2D":
+                if l.dilation_rate != (1, 1) or l.kernel_size[0] != l.kernel_size[1] or l.strides[0] != l.strides[1]:
+                    return False, "conv geometry"
+                if l.strides[0] not in (1, 2) or l.filters % 8:
+                    return False, "conv stride/filters"
+            if k == "MaxPooling2D" and l.pool_size[0] * l.pool_size[1] > 255:
+                return False, "pool size"
+            if k == "BatchNormalization" and l.axis not in (-1, 3):
+                return False, "BN axis"
+            if k == "Add" and len(ins) != 2:
+                return False, "Add arity"
+        last = seq[-1][0]
+        if type(last).__name__ != "Dense" or getattr(last.activation, "__name__", "") != "linear":
+            return False, "the model must end in a linear Dense (logits)"
+        return True, ""
+
+    # ------------------------------------------------------------------------------------
+    def __init__(self, model, strategy, per_replica_batch, global_batch):
+        super().__init__(model, strategy, per_replica_batch, global_batch)
+        from ..native import require_C
+
+        self.C = require_C()
+        dev = self.device
+        self.B = B = per_replica_batch
+        # flat fp32 master buffer P (Keras trainable-weight order), bf16 shadow, grads, momentum
+        # every variable starts on an 8-element boundary: 16-byte aligned bf16 / 32-byte
+        # aligned fp32 views for the kernels' vector accesses
+        self.vars = model.trainable_weights
+        self.sizes = [int(np.prod(v.shape)) for v in self.vars]
+        offs, off = [], 0
+        for sz in self.sizes:
+            offs.append(off)
+            off = _pad8(off + sz)
+        self.nparam = n = off
+        self.P = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.Pb = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+        self.G = torch.zeros(n + 8, dtype=torch.float32, device=dev)  # + metric tail
+        self.V = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.views, self.bviews, self.gviews = {}, {}, {}
+        self.offsets = offs
+        for v, sz, off in zip(self.vars, self.sizes, offs):
+            v._rebind(self.P[off:off + sz].view(v.shape))
+            self.views[id(v)] = self.P[off:off + sz].view(v.shape)
+            self.bviews[id(v)] = self.Pb[off:off + sz].view(v.shape)
+            self.gviews[id(v)] = self.G[off:off + sz].view(v.shape)
+        # non-trainable (BN moving statistics) live on the device as fp32
+        for w in model.non_trainable_weights:
+            if w.value.device != dev:
+                w._rebind(torch.zeros(w.shape, dtype=torch.float32, device=dev))
+        opt = model.optimizer
+        self._load_momentum()
+        if self.world > 1:
+            comm = strategy.communicator
+            comm.broadcast_(self.P, 0)
+            for w in model.non_trainable_weights:
+                comm.broadcast_(w.value, 0)
+        H.cast_bf16(self.P, self.Pb)
+        self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
+        c = self.ctrl.cpu()
+        c[C_IT] = int(opt.iterations)
+        self.ctrl.copy_(c.to(dev))
+        self._write_hparams()
+        self.native_comm = strategy.communicator.native if self.world > 1 else None
+        self.host_collective = self.world > 1 and self.native_comm is None
+        self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
+        self.graph = None
+        self.feed = None
+        self._plan()
+        opt._iter_source = self._iterations
+        torch.cuda.synchronize(dev)
+        dlog.info("native graph engine: %d nodes, %d params, %.1f MB planned activations", len(self.nodes), n,
+                  self.act_bytes / 2**20)
+
+    # --- planning --------------------------------------------------------------------------
+    def _plan(self):
+        model, dev, B = self.model, self.device, self.B
+        seq, in_key, out_key, in_shape = _layer_graph(model)
+        tensors: Dict[int, T] = {}
+        h, w, c = in_shape
+        self.in_shape = (h, w, c)
+        self.cin_pad = _pad8(c)
+        x0 = T((B, h, w, self.cin_pad), needs_grad=False)
+        tensors[in_key] = x0
+        self.x0 = x0
+        nodes = []
+        for layer, ins, ok in seq:
+            kind = type(layer).__name__
+            xs = [tensors[i] for i in ins]
+            shp = self._out_shape(kind, layer, xs)
+            out = T(shp)
+            nd = Node(kind, layer, xs, out)
+            for x in xs:
+                x.consumers.append(nd)
+            tensors[ok] = out
+            nodes.append(nd)
+        self.logits_t = tensors[out_key]
+        self.nodes = nodes
+        self._fuse()
+        self._allocate()
+
+    def _out_shape(self, kind, l, xs):
+        x = xs[0].shape
+        B = self.B
+        if kind == "Conv2D":
+            ho, _ = H.conv_out(x[1], l.kernel_size[0], l.strides[0], l.padding)
+            wo, _ = H.conv_out(x[2], l.kernel_size[1], l.strides[1], l.padding)
+            return (B, ho, wo, l.filters)
+        if kind == "MaxPooling2D":
+            g = H.pool_geo(x, l.pool_size, l.strides, l.padding)
+            return (B, g[10], g[11], x[3])
+        if kind == "GlobalAveragePooling2D":
+            return (B, x[3])
+        if kind == "Flatten":
+            return (B, int(np.prod(x[1:])))
+        if kind == "Dense":
+            return (B, l.units)
+        return x
+
+    def _fuse(self):
+        def relu_node(nd):
+            if nd.kind == "ReLU":
+                return True
+            return nd.kind == "Activation" and getattr(nd.layer.activation, "__name__", "") == "relu"
+
+        for nd in self.nodes:
+            nd.attrs.setdefault("dead", False)
+            if nd.kind == "Activation" and not relu_node(nd):
+                nd.attrs["dead"] = True  # linear activation: identity
+                self._alias(nd.out, nd.inputs[0])
+            if nd.kind == "Flatten":
+                nd.attrs["dead"] = True  # NHWC flatten is a view
+                self._alias(nd.out, nd.inputs[0])
+        for nd in self.nodes:
+            if nd.kind != "BatchNormalization":
+                continue
+            x = nd.inputs[0]
+            prod = self._producer(x)
+            if (prod is not None and prod.kind == "Conv2D" and not prod.layer.use_bias
+                    and getattr(prod.layer.activation, "__name__", "linear") == "linear" and len(x.consumers) == 1):
+                prod.attrs["stats"] = True
+                nd.attrs["stats_from_conv"] = True
+        for nd in self.nodes:
+            if nd.kind != "BatchNormalization" or nd.attrs.get("stats_only"):
+                continue
+            y = nd.out
+            if len(y.consumers) == 1 and y.consumers[0].kind == "Add":
+                # BN -> Add(other) [-> ReLU]: one pass at the Add's position (after both branches)
+                add = y.consumers[0]
+                other = add.inputs[1] if add.inputs[0] is y else add.inputs[0]
+                op = self._producer(other)
+                nd.attrs["stats_only"] = True
+                if (op is not None and op.kind == "BatchNormalization" and len(other.consumers) == 1
+                        and not op.attrs.get("stats_only")):
+                    op.attrs["stats_only"] = True
+                    add.attrs["fused"] = (nd, ("bn", op))
+                else:
+                    add.attrs["fused"] = (nd, ("raw", other))
+                out = add.out
+                if len(out.consumers) == 1 and relu_node(out.consumers[0]):
+                    r = out.consumers[0]
+                    add.attrs["relu"] = True
+                    r.attrs["dead"] = True
+                    self._alias(r.out, out)
+                continue
+            if len(y.consumers) == 1 and relu_node(y.consumers[0]):
+                r = y.consumers[0]
+                nd.attrs["relu"] = True
+                r.attrs["dead"] = True
+                self._alias(r.out, y)
+
+    def _producer(self, t):
+        for nd in self.nodes:
+            if nd.out is t:
+                return nd
+        return None
+
+    @staticmethod
+    def _alias(t, target):
+        t.alias_of = target
+
+    def _allocate(self):
+        dev = self.device
+        nbytes = 0
+
+        def alloc(t: T, dtype=torch.bfloat16):
+            nonlocal nbytes
+            if t.alias_of is not None:
+                return
+            t.buf = torch.zeros(t.shape, dtype=dtype, device=dev)
+            t.dtype = dtype
+            nbytes += t.buf.numel() * t.buf.element_size()
+            if t.needs_grad:
+                t.grad = torch.zeros(t.shape, dtype=torch.bfloat16, device=dev)
+                nbytes += t.grad.numel() * 2
+
+        alloc(self.x0)
+        self.labels = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        last = self.nodes[-1]
+        for nd in self.nodes:
+            if nd is last:
+                continue
+            alloc(nd.out)
+        # logits: fp32, row pitch padded to 8
+        K = last.layer.units
+        self.K, self.Kp = K, _pad8(K)
+        self.logits = torch.zeros(self.B, self.Kp, dtype=torch.float32, device=dev)
+        self.dlogits = torch.zeros(self.B, self.Kp, dtype=torch.bfloat16, device=dev)
+        last.attrs["logits"] = True
+        # per-node scratch
+        self.st_ident = torch.cat([torch.zeros(1, 1), torch.ones(1, 1), torch.ones(1, 1), torch.zeros(1, 1)])
+        self._ident_cache = {}
+        maxM_C = 0
+        for nd in self.nodes:
+            if nd.attrs.get("dead"):
+                continue
+            k = nd.kind
+            if k == "Conv2D":
+                l = nd.layer
+                cin = nd.inputs[0].root().shape[3]
+                kh, kw, cin0, cout = l.kernel.shape
+                nd.attrs["cin_pad"] = cin
+                if cin != cin0:
+                    nd.attrs["w_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.bfloat16, device=dev)
+                    nd.attrs["dw_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.float32, device=dev)
+                if nd.attrs.get("stats"):
+                    M = int(np.prod(nd.out.shape[:3]))
+                    rows = H.tile_rows(H.pick_tile(cout))
+                    nd.attrs["stats_buf"] = torch.zeros(-(-M // rows), 2, cout, device=dev)
+                if getattr(l.activation, "__name__", "linear") == "relu":
+                    nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
+            elif k == "BatchNormalization":
+                C = nd.out.shape[-1]
+                M = int(np.prod(nd.out.shape[:-1]))
+                nd.attrs["st"] = torch.zeros(4, C, device=dev)
+                T_ = self.C.bn_bwd_blocks(M, C)
+                nd.attrs["T"] = T_
+                nd.attrs["part"] = torch.zeros(max(T_, 1), 2, C, device=dev)
+                nd.attrs["co"] = torch.zeros(3, C, device=dev)
+                maxM_C = max(maxM_C, M * C)
+            elif k == "MaxPooling2D":
+                nd.attrs["arg"] = torch.zeros(nd.out.shape, dtype=torch.uint8, device=dev)
+            elif k == "Dense":
+                l = nd.layer
+                kin, units = l.kernel.shape
+                if nd.attrs.get("logits") and units % 8:
+                    up = _pad8(units)
+                    nd.attrs["w_pad"] = torch.zeros(kin, up, dtype=torch.bfloat16, device=dev)
+                    nd.attrs["dw_pad"] = torch.zeros(kin, up, dtype=torch.float32, device=dev)
+                    if l.use_bias:
+                        nd.attrs["b_pad"] = torch.zeros(up, dtype=torch.float32, device=dev)
+                if getattr(l.activation, "__name__", "linear") == "relu":
+                    nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
+        # one scratch bf16 buffer for "second writer" gradient accumulation
+        big = max([int(np.prod(t.shape)) for t in self._all_tensors()] + [1])
+        self.scratch = torch.zeros(big, dtype=torch.bfloat16, device=dev)
+        self.scratch2 = torch.zeros(big, dtype=torch.bfloat16, device=dev)
+        nbytes += big * 4
+        self.act_bytes = nbytes
+
+    def _all_tensors(self):
+        out = [self.x0]
+        for nd in self.nodes:
+            out.append(nd.out)
+        return out
+
+    def _ident(self, C):
+        t = self._ident_cache.get(C)
+        if t is None:
+            t = self.st_ident.expand(4, C).contiguous().to(self.device)
+            self._ident_cache[C] = t
+        return t
+
+    # --- gradient write protocol ----------------------------------------------------------
+    def _grad_target(self, t: T):
+        """(buffer to write, finish fn) for a producer of t's gradient."""
+        r = t.root()
+        if not r.needs_grad:
+            return None, None
+        if not r.written:
+            r.written = True
+            return r.grad, None
+        tmp = self.scratch[: r.grad.numel()].view(r.grad.shape)
+
+        def finish():
+            H.add_bf16(r.grad, tmp, r.grad)
+
+        return tmp, finish
+
+    # --- hyper-parameters / ctrl -------------------------------------------------------------
+    def _write_hparams(self):
+        opt = self.model.optimizer
+        c = self.ctrl.cpu()
+        c[C_LR] = _f2i(opt.learning_rate)
+        c[C_MOM] = _f2i(opt.momentum)
+        c[C_NEST] = int(opt.nesterov)
+        c[C_ROW0] = self.rank * self.per_replica
+        c[C_GB] = self.global_batch
+        self.ctrl.copy_(c.to(self.device))
+
+    def _ctrl_write(self, updates):
+        torch.cuda.synchronize(self.device)
+        c = self.ctrl.cpu()
+        for k, v in updates.items():
+            c[k] = v
+        self.ctrl.copy_(c.to(self.device))
+        torch.cuda.synchronize(self.device)
+
+    def _iterations(self):
+        torch.cuda.synchronize(self.device)
+        return int(self.ctrl[C_IT].item())
+
+    def lr_changed(self):
+        self._ctrl_write({C_LR: _f2i(self.model.optimizer.learning_rate)})
+
+    def _load_momentum(self):
+        # optimizer slots are dense over the unpadded weights (Keras order)
+        opt = self.model.optimizer
+        tot = int(sum(self.sizes))
+        if opt.momentum and "momentum" in opt.slots and opt.slots["momentum"].numel() == tot:
+            src = opt.slots["momentum"].to(self.device)
+            o = 0
+            for sz, off in zip(self.sizes, self.offsets):
+                self.V[off:off + sz].copy_(src[o:o + sz])
+                o += sz
+
+    def reload_optimizer_state(self):
+        opt = self.model.optimizer
+        torch.cuda.synchronize(self.device)
+        self._load_momentum()
+        opt._iter_source = None
+        it = int(opt.iterations)
+        opt._iter_source = self._iterations
+        H.cast_bf16(self.P, self.Pb)
+        self._ctrl_write({C_IT: it})
+
+    # --- data -------------------------------------------------------------------------------
+    def bind(self, x, y):
+        x = np.asarray(x)
+        h, w, c = self.in_shape
+        if tuple(x.shape[1:]) not in ((h, w, c),) and not (c == 1 and tuple(x.shape[1:]) == (h, w)):
+            raise ValueError(f"native graph engine expects inputs of shape {(h, w, c)}, got {x.shape[1:]}")
+        key = (id(x), id(y), len(x))
+        if self.feed is None or getattr(self, "_feed_key", None) != key:
+            torch.cuda.synchronize(self.device)
+            self.feed = DataFeed(x, y, self.device, flatten=True, allow_u8=env.get_bool("DAMD_X_U8", True))
+            self._feed_key = key
+            self.x_ep = torch.empty_like(self.feed.x)
+            self.y_ep = torch.empty_like(self.feed.y)
+            self.graph = None  # data pointers changed
+            self._ctrl_write({C_NS: self.feed.n})
+        return self.feed
+
+    def start_epoch(self, epoch, shuffle, wrap_steps: int = 0):
+        torch.cuda.synchronize(self.device)
+        self.feed.set_epoch(epoch, shuffle, self.shuffle_seed)
+        perm = self.feed.perm.long()
+        torch.index_select(self.feed.x, 0, perm, out=self.x_ep)
+        torch.index_select(self.feed.y, 0, perm, out=self.y_ep)
+        opt = self.model.optimizer
+        self._ctrl_write({C_CUR: 0, C_AL: 0, C_AC: 0, C_AN: 0, C_WRAP: int(wrap_steps),
+                          C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
+
+    # --- the step ----------------------------------------------------------------------------
+    def _step_body(self):
+        C, B = self.C, self.B
+        s = H.stream_handle()
+        h, w, c = self.in_shape
+        self.G.zero_()
+        C.gather_batch(self.x_ep.data_ptr(), int(self.feed.x_u8), 255.0, self.y_ep.data_ptr(), self.ctrl.data_ptr(),
+                       B, h * w, c, self.cin_pad, self.x0.buf.data_ptr(), self.labels.data_ptr(), s)
+        live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
+        for nd in live:
+            getattr(self, "_fwd_" + nd.kind)(nd)
+        H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:])
+        for t in self._all_tensors():
+            t.root().written = False
+        for nd in reversed(live):
+            getattr(self, "_bwd_" + nd.kind)(nd)
+        if self.native_comm is not None:
+            self.native_comm.allreduce(self.G.data_ptr(), self.G.data_ptr(), self.G.numel(), 0, 0, s)
+        if not self.host_collective:
+            self._optimizer_step()
+
+    def _optimizer_step(self):
+        self.C.sgd_step(self.P.data_ptr(), self.G.data_ptr(), self.V.data_ptr(), self.Pb.data_ptr(), self.nparam,
+                        self.ctrl.data_ptr(), self.G[self.nparam:].data_ptr(), H.stream_handle())
+
+    # forward ops
+    def _w(self, nd, var):
+        return self.bviews[id(var)]
+
+    def _fwd_Conv2D(self, nd):
+        l = nd.layer
+        x = nd.inputs[0].root().buf
+        wb = self._w(nd, l.kernel)
+        if "w_pad" in nd.attrs:
+            kh, kw, cin, cout = l.kernel.shape
+            H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
+            wb = nd.attrs["w_pad"]
+        bias = self.views[id(l.bias)] if l.use_bias else None
+        relu = getattr(l.activation, "__name__", "linear") == "relu"
+        H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
+                   stats=nd.attrs.get("stats_buf"))
+
+    def _fwd_BatchNormalization(self, nd):
+        l = nd.layer
+        x = nd.inputs[0].root()
+        C = x.shape[-1]
+        M = int(np.prod(x.shape[:-1]))
+        st = nd.attrs["st"]
+        gamma = self.views[id(l.gamma)] if l.gamma is not None else None
+        beta = self.views[id(l.beta)] if l.beta is not None else None
+        if nd.attrs.get("stats_from_conv"):
+            part = self._producer(x).attrs["stats_buf"]
+            Tn = part.shape[0]
+        else:
+            part, Tn = nd.attrs["part"], nd.attrs["T"]
+            ident = self._ident(C)
+            self.C.bn_bwd_reduce(x.buf.data_ptr(), 0, 0, x.buf.data_ptr(), ident.data_ptr(), 0, part.data_ptr(), Tn,
+                                 M, C, H.stream_handle())
+        H.bn_finalize(part, Tn, C, M, gamma, beta, l.epsilon, l.momentum, l.moving_mean.value,
+                      l.moving_variance.value, st)
+        if nd.attrs.get("stats_only"):
+            return  # applied by the fused Add that consumes it
+        H.bn_apply(x.buf, st, nd.out.root().buf, relu=nd.attrs.get("relu", False))
+
+    def _fwd_Activation(self, nd):
+        C = nd.out.shape[-1]
+        x = nd.inputs[0].root()
+        H.bn_apply(x.buf, self._ident(C), nd.out.root().buf, relu=True)
+
+    _fwd_ReLU = _fwd_Activation
+
+    def _fwd_Add(self, nd):
+        fused = nd.attrs.get("fused")
+        if fused is None:
+            a, b = nd.inputs[0].root().buf, nd.inputs[1].root().buf
+            H.add_bf16(a, b, nd.out.root().buf)
+            return
+        main, (mode, other) = fused
+        x = main.inputs[0].root()
+        if mode == "raw":
+            r, st2 = other.root().buf, None
+        else:
+            r, st2 = other.inputs[0].root().buf, other.attrs["st"]
+        H.bn_apply(x.buf, main.attrs["st"], nd.out.root().buf, relu=nd.attrs.get("relu", False), r=r, st2=st2)
+
+    def _fwd_MaxPooling2D(self, nd):
+        l = nd.layer
+        H.maxpool_fwd(nd.inputs[0].root().buf, nd.out.root().buf, nd.attrs["arg"], l.pool_size, l.strides, l.padding)
+
+    def _fwd_GlobalAveragePooling2D(self, nd):
+        H.gap_fwd(nd.inputs[0].root().buf, nd.out.root().buf)
+
+    def _fwd_Dense(self, nd):
+        l = nd.layer
+        x = nd.inputs[0].root().buf
+        x2 = x.view(x.shape[0], -1)
+        wb = self._w(nd, l.kernel)
+        bias = self.views[id(l.bias)] if l.use_bias else None
+        if "w_pad" in nd.attrs:
+            kin, units = l.kernel.shape
+            H.pad_cast(self.views[id(l.kernel)], 1, kin, units, kin, nd.attrs["w_pad"].shape[1], nd.attrs["w_pad"])
+            wb = nd.attrs["w_pad"]
+            if bias is not None:
+                nd.attrs["b_pad"][:units].copy_(bias)
+                bias = nd.attrs["b_pad"]
+        relu = getattr(l.activation, "__name__", "linear") == "relu"
+        out = self.logits if nd.attrs.get("logits") else nd.out.root().buf
+        H.dense_fwd(x2, wb, out, bias=bias, relu=relu)
+
+    # backward ops
+    def _dy(self, nd):
+        if nd.attrs.get("logits"):
+            return self.dlogits
+        return nd.out.root().grad
+
+    def _bwd_Conv2D(self, nd):
+        l = nd.layer
+        xt = nd.inputs[0].root()
+        y = nd.out.root()
+        dy = y.grad
+        if "dz" in nd.attrs:
+            H.relu_bwd(dy, y.buf, nd.attrs["dz"])
+            dy = nd.attrs["dz"]
+        if l.use_bias:
+            H.colsum(dy, self.gviews[id(l.bias)])
+        if "dw_pad" in nd.attrs:
+            dwp = nd.attrs["dw_pad"]
+            dwp.zero_()
+            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding)
+            kh, kw, cin, cout = l.kernel.shape
+            H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
+        else:
+            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding)
+        if xt.needs_grad:
+            wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
+            acc = xt.written
+            xt.written = True
+            H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc)
+
+    def _bn_backward(self, bn, dy, ymask, relu, dz_out=None):
+        """BatchNorm backward of node ``bn`` for upstream gradient dy (masked by
+        [ymask > 0] when relu); dgamma/dbeta into the gradient sinks, dx into the input's
+        gradient; optionally also writes the masked dy to dz_out."""
+        l = bn.layer
+        C_ = self.C
+        s = H.stream_handle()
+        x = bn.inputs[0].root()
+        C = x.shape[-1]
+        M = int(np.prod(x.shape[:-1]))
+        st, part, co, Tn = bn.attrs["st"], bn.attrs["part"], bn.attrs["co"], bn.attrs["T"]
+        ym = ymask.data_ptr() if relu else 0
+        C_.bn_bwd_reduce(dy.data_ptr(), ym, int(relu), x.buf.data_ptr(), st.data_ptr(),
+                         dz_out.data_ptr() if (dz_out is not None and relu) else 0, part.data_ptr(), Tn, M, C, s)
+        C_.bn_bwd_finalize(part.data_ptr(), Tn, C, float(M), st.data_ptr(), 0,
+                           self.gviews[id(l.gamma)].data_ptr() if l.gamma is not None else 0,
+                           self.gviews[id(l.beta)].data_ptr() if l.beta is not None else 0, co.data_ptr(), s)
+        dx, fin = self._grad_target(x)
+        if dx is not None:
+            C_.bn_bwd_apply(dy.data_ptr(), ym, int(relu), x.buf.data_ptr(), st.data_ptr(), co.data_ptr(),
+                            dx.data_ptr(), M, C, s)
+            if fin:
+                fin()
+
+    def _bwd_BatchNormalization(self, nd):
+        if nd.attrs.get("stats_only"):
+            return  # handled by the fused Add
+        y = nd.out.root()
+        self._bn_backward(nd, y.grad, y.buf, bool(nd.attrs.get("relu")))
+
+    def _bwd_Activation(self, nd):
+        x = nd.inputs[0].root()
+        y = nd.out.root()
+        dx, fin = self._grad_target(x)
+        if dx is not None:
+            H.relu_bwd(y.grad, y.buf, dx)
+            if fin:
+                fin()
+
+    _bwd_ReLU = _bwd_Activation
+
+    def _bwd_Add(self, nd):
+        out = nd.out.root()
+        fused = nd.attrs.get("fused")
+        if fused is None:
+            for x in nd.inputs:
+                dx, fin = self._grad_target(x)
+                if dx is not None:
+                    dx.copy_(out.grad)
+                    if fin:
+                        fin()
+            return
+        main, (mode, other) = fused
+        relu = bool(nd.attrs.get("relu"))
+        dy = out.grad
+        M = int(np.prod(out.shape[:-1]))
+        C = out.shape[-1]
+        if mode == "raw":
+            # the residual input's gradient is the (masked) dy itself
+            dz, fin = self._grad_target(other)
+            if relu:
+                self._bn_backward(main, dy, out.buf, True, dz_out=dz)
+            else:
+                if dz is not None:
+                    dz.copy_(dy)
+                self._bn_backward(main, dy, out.buf, False)
+            if fin:
+                fin()
+        else:
+            g = dy
+            if relu:
+                g = self.scratch2[: M * C].view(out.shape)
+                H.relu_bwd(dy, out.buf, g)
+            self._bn_backward(main, g, out.buf, False)
+            self._bn_backward(other, g, out.buf, False)
+
+    def _bwd_MaxPooling2D(self, nd):
+        l = nd.layer
+        x = nd.inputs[0].root()
+        dx, fin = self._grad_target(x)
+        if dx is not None:
+            H.maxpool_bwd(nd.out.root().grad, nd.attrs["arg"], dx, l.pool_size, l.strides, l.padding)
+            if fin:
+                fin()
+
+    def _bwd_GlobalAveragePooling2D(self, nd):
+        x = nd.inputs[0].root()
+        dx, fin = self._grad_target(x)
+        if dx is not None:
+            H.gap_bwd(nd.out.root().grad, dx)
+            if fin:
+                fin()
+
+    def _bwd_Dense(self, nd):
+        l = nd.layer
+        xt = nd.inputs[0].root()
+        x2 = xt.buf.view(xt.buf.shape[0], -1)
+        dy = self._dy(nd)
+        if "dz" in nd.attrs:
+            y = nd.out.root()
+            H.relu_bwd(dy, y.buf, nd.attrs["dz"])
+            dy = nd.attrs["dz"]
+        units = l.units
+        if l.use_bias:
+            if dy.shape[1] != units:
+                self.C.colsum(dy.data_ptr(), 0, dy.shape[0], units, dy.shape[1], self.gviews[id(l.bias)].data_ptr(),
+                              H.stream_handle())
+            else:
+                H.colsum(dy, self.gviews[id(l.bias)])
+        if "dw_pad" in nd.attrs:
+            dwp = nd.attrs["dw_pad"]
+            dwp.zero_()
+            H.dense_wgrad(x2, dy, dwp)
+            kin = l.kernel.shape[0]
+            H.unpad_add(dwp, 1, kin, units, kin, dwp.shape[1], self.gviews[id(l.kernel)])
+        else:
+            H.dense_wgrad(x2, dy, self.gviews[id(l.kernel)])
+        if xt.needs_grad:
+            wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
+            acc = xt.written
+            xt.written = True
+            H.dense_dgrad(dy, wb, xt.grad.view(xt.grad.shape[0], -1), accumulate=acc)
+
+    # --- driver ---------------------------------------------------------------------------------
+    def _capture(self):
+        torch.cuda.synchronize(self.device)
+        # warm-up on a side stream (torch's recommended capture prologue); the warm-up
+        # trains one real step, which the caller accounts for
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_body()
+        self.graph = g
+
+    def run(self, n_steps):
+        if self.host_collective:
+            for _ in range(n_steps):
+                self._step_body()
+                torch.cuda.synchronize(self.device)
+                self.strategy.communicator.allreduce_(self.G, "sum")
+                self._optimizer_step()
+            return
+        if not self.use_graph:
+            for _ in range(n_steps):
+                self._step_body()
+            return
+        done = 0
+        if self.graph is None:
+            # eager first step (also validates the plan), then capture
+            self._step_body()
+            done = 1
+            if n_steps > 1:
+                self._capture_safe()
+                # capture does not execute; replay below
+        for _ in range(n_steps - done):
+            if self.graph is None:
+                self._capture_safe()
+            self.graph.replay()
+
+    def _capture_safe(self):
+        # capturing would run allocator/stream ops; make sure no work is pending
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._step_body()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.graph = g
+
+    def metrics(self):
+        torch.cuda.synchronize(self.device)
+        c = self.ctrl.cpu().tolist()
+        loss, corr, cnt = _i2f(c[C_AL]), _i2f(c[C_AC]), _i2f(c[C_AN])
+        d = max(cnt, 1.0)
+        out = {"loss": loss / d, "_count": cnt}
+        for m in self.model.compiled_metrics:
+            out[m.name] = corr / d
+        return out
+
+    def end_epoch(self):
+        return self.metrics()
+
+    def finish(self):
+        torch.cuda.synchronize(self.device)
+        opt = self.model.optimizer
+        if opt.momentum:
+            tot = int(sum(self.sizes))
+            opt.ensure_slots(tot, self.device)
+            o = 0
+            for sz, off in zip(self.sizes, self.offsets):
+                opt.slots["momentum"][o:o + sz].copy_(self.V[off:off + sz])
+                o += sz
+
+    def sync(self):
+        torch.cuda.synchronize(self.device)

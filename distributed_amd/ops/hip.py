@@ -1,0 +1,283 @@
+"""Python launchers for the generic-path HIP kernels (csrc/kernels/gemm.hip,
+csrc/kernels/layer_ops.hip).
+
+These are thin, validating wrappers: they check dtypes, shapes, contiguity and the
+16-byte alignment the kernels' vector accesses assume, pick the tile shape and split-K
+factor, and enqueue on torch's current stream (so everything is captured by a
+``torch.cuda.CUDAGraph``).  Activations are NHWC bf16, parameters fp32 masters with
+bf16 shadows.  There is no silent fallback: a call that does not meet a kernel's
+contract raises.
+
+Keras conventions (reference README.md:58-73): conv kernels ``[kh, kw, cin, cout]``,
+dense kernels ``[in, out]``, TF 'same' padding (the extra pixel at bottom/right).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from ..native import require_C
+
+A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD = range(5)
+B_NC, B_KC = 0, 1
+E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD = 1, 2, 4, 8, 16, 32
+BK = 32
+
+
+def _C():
+    return require_C()
+
+
+def stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _chk(t: torch.Tensor, dtype, name: str):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a device tensor")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.data_ptr() % 16:
+        raise ValueError(f"{name}: must be 16-byte aligned")
+
+
+def same_pad(in_size: int, k: int, s: int) -> Tuple[int, int, int]:
+    """TF 'same': (out, pad_before, pad_after)."""
+    out = math.ceil(in_size / s)
+    total = max((out - 1) * s + k - in_size, 0)
+    return out, total // 2, total - total // 2
+
+
+def conv_out(in_size: int, k: int, s: int, padding: str) -> Tuple[int, int]:
+    if padding == "same":
+        o, pb, _ = same_pad(in_size, k, s)
+        return o, pb
+    return (in_size - k) // s + 1, 0
+
+
+def pick_tile(N: int) -> int:
+    """1 -> 256x64 tiles (narrow layers, no wasted MFMA columns), 0 -> 128x128."""
+    return 1 if N <= 64 else 0
+
+
+def tile_rows(tile: int) -> int:
+    return 256 if tile == 1 else 128
+
+
+def pick_splits(M: int, N: int, K: int, tile: int, target_wg: int = 1024) -> Tuple[int, int]:
+    """Split-K factor so a long-K product still launches >> 256 workgroups (256 CUs)."""
+    bm, bn = (256, 64) if tile == 1 else (128, 128)
+    tiles = -(-M // bm) * -(-N // bn)
+    splits = max(1, min(-(-target_wg // tiles), max(1, K // 256)))
+    kps = -(-K // splits)
+    kps = -(-kps // BK) * BK
+    splits = -(-K // kps)
+    return splits, kps
+
+
+def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
+         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None):
+    t = pick_tile(N) if tile is None else tile
+    kps = k_per_split if k_per_split is not None else -(-K // BK) * BK
+    _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), _ptr(stats), _ptr(R), M, N, K,
+              lda, ldb, ldc, list(geo), kc, kps, stream_handle())
+
+
+# ---- dense -------------------------------------------------------------------------------
+def dense_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, relu=False, stats=None):
+    """out[M,N] = x[M,K] @ w[K,N] (+bias)(relu); x, w bf16; out bf16 or fp32."""
+    M, K = x.shape
+    K2, N = w.shape
+    assert K == K2 and tuple(out.shape) == (M, N)
+    _chk(x, torch.bfloat16, "x")
+    _chk(w, torch.bfloat16, "w")
+    if K % 8 or N % 8:
+        raise ValueError("dense_fwd: K and N must be multiples of 8 (pad the layer)")
+    epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0)
+    epi |= E_BF16 if out.dtype == torch.bfloat16 else 0
+    if stats is not None:
+        epi |= E_STATS
+    gemm(x, w, out, amode=A_KC, bmode=B_NC, M=M, N=N, K=K, lda=K, ldb=N, ldc=N, epi=epi, bias=bias, stats=stats)
+
+
+def dense_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, accumulate=False):
+    """dx[M,K] (+)= dy[M,N] @ w[K,N]^T (bf16 out)."""
+    M, N = dy.shape
+    K, N2 = w.shape
+    assert N == N2 and tuple(dx.shape) == (M, K)
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(w, torch.bfloat16, "w")
+    _chk(dx, torch.bfloat16, "dx")
+    epi = E_BF16 | (E_ADD if accumulate else 0)
+    gemm(dy, w, dx, amode=A_KC, bmode=B_KC, M=M, N=K, K=N, lda=N, ldc=K, epi=epi, kc=N,
+         R=dx if accumulate else None)
+
+
+def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor):
+    """dw[K,N] += x[M,K]^T @ dy[M,N] (fp32, atomically accumulated; split over M)."""
+    M, K = x.shape
+    M2, N = dy.shape
+    assert M == M2 and tuple(dw.shape) == (K, N)
+    _chk(x, torch.bfloat16, "x")
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(dw, torch.float32, "dw")
+    t = pick_tile(N)
+    splits, kps = pick_splits(K, N, M, t)
+    gemm(x, dy, dw, amode=A_MC, bmode=B_NC, M=K, N=N, K=M, lda=K, ldb=N, ldc=N, epi=E_ATOMIC, splits=splits,
+         k_per_split=kps, tile=t)
+
+
+# ---- conv ---------------------------------------------------------------------------------
+def conv_geo(x_shape, w_shape, strides, padding):
+    n, h, w_, c = x_shape
+    kh, kw, cin, cout = w_shape
+    if strides[0] != strides[1] or kh != kw or h != w_:
+        raise ValueError("HIP conv path: square kernels/images and equal strides only")
+    ho, pad = conv_out(h, kh, strides[0], padding)
+    wo, pad2 = conv_out(w_, kw, strides[1], padding)
+    assert pad == pad2
+    return n, h, w_, cin, ho, wo, kh, kw, strides[0], pad, cout
+
+
+def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, stats=None):
+    """out [N,Ho,Wo,Cout] = conv(x [N,H,W,Cin], w [KH,KW,Cin,Cout]); bf16 in/out."""
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, w.shape, strides, padding)
+    _chk(x, torch.bfloat16, "x")
+    _chk(w, torch.bfloat16, "w")
+    if cin % 8 or cout % 8:
+        raise ValueError("conv_fwd: Cin and Cout must be multiples of 8 (pad the channels)")
+    assert tuple(out.shape) == (n, ho, wo, cout)
+    epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | (E_STATS if stats is not None else 0)
+    gemm(x, w, out, amode=A_IM2COL, bmode=B_NC, M=n * ho * wo, N=cout, K=kh * kw * cin, ldb=cout, ldc=cout, epi=epi,
+         bias=bias, stats=stats, geo=(h, wd, cin, ho, wo, kh, kw, s, pad))
+
+
+def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False):
+    """dx [N,H,W,Cin] (+)= backprop-input of dy [N,Ho,Wo,Cout] through w."""
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx.shape, w.shape, strides, padding)
+    if s not in (1, 2):
+        raise ValueError("conv_dgrad: stride 1 or 2")
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(w, torch.bfloat16, "w")
+    _chk(dx, torch.bfloat16, "dx")
+    if cin % 8 or cout % 8:
+        raise ValueError("conv_dgrad: Cin and Cout must be multiples of 8")
+    epi = E_BF16 | (E_ADD if accumulate else 0)
+    gemm(dy, w, dx, amode=A_DGRAD, bmode=B_KC, M=n * h * wd, N=cin, K=kh * kw * cout, ldc=cin, epi=epi, kc=cout,
+         geo=(h, wd, cout, ho, wo, kh, kw, s, pad), R=dx if accumulate else None)
+
+
+def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid"):
+    """dw [KH,KW,Cin,Cout] += sum over pixels of im2col(x)^T dy (fp32 atomics, split-K)."""
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, dw.shape, strides, padding)
+    _chk(x, torch.bfloat16, "x")
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(dw, torch.float32, "dw")
+    if cin % 8 or cout % 8:
+        raise ValueError("conv_wgrad: Cin and Cout must be multiples of 8")
+    M, N, K = kh * kw * cin, cout, n * ho * wo
+    t = pick_tile(N)
+    splits, kps = pick_splits(M, N, K, t)
+    gemm(x, dy, dw, amode=A_WGRAD, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=cout, epi=E_ATOMIC, splits=splits,
+         k_per_split=kps, tile=t, geo=(h, wd, cin, ho, wo, kh, kw, s, pad))
+
+
+# ---- BN / pooling / loss / optimizer -------------------------------------------------------------
+def bn_finalize(part, T, C, count, gamma, beta, eps, momentum, rmean, rvar, st):
+    _C().bn_finalize(_ptr(part), T, C, float(count), _ptr(gamma), _ptr(beta), float(eps), float(momentum),
+                     _ptr(rmean), _ptr(rvar), _ptr(st), stream_handle())
+
+
+def bn_apply(x, st, y, relu=False, r=None, st2=None):
+    C = x.shape[-1]
+    M = x.numel() // C
+    mode = 0 if r is None else (1 if st2 is None else 2)
+    _C().bn_apply(_ptr(x), _ptr(st), _ptr(r), _ptr(st2), mode, int(relu), _ptr(y), M, C, stream_handle())
+
+
+def bn_bwd(dy, y, relu_mask, x, st, part, co, dx, dgamma=None, dbeta=None, dz_out=None):
+    """Full BN backward (reduce, finalize, apply); part must hold bn_bwd_blocks(M, C) x 2C."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    T = _C().bn_bwd_blocks(M, C)
+    assert part.numel() >= T * 2 * C
+    s = stream_handle()
+    _C().bn_bwd_reduce(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dz_out), _ptr(part), T, M, C, s)
+    _C().bn_bwd_finalize(_ptr(part), T, C, float(M), _ptr(st), 0, _ptr(dgamma), _ptr(dbeta), _ptr(co), s)
+    _C().bn_bwd_apply(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(co), _ptr(dx), M, C, s)
+
+
+def pool_geo(x_shape, pool, strides, padding):
+    n, h, w, c = x_shape
+    if padding == "same":
+        ho, pt, _ = same_pad(h, pool[0], strides[0])
+        wo, pl, _ = same_pad(w, pool[1], strides[1])
+    else:
+        ho, pt = (h - pool[0]) // strides[0] + 1, 0
+        wo, pl = (w - pool[1]) // strides[1] + 1, 0
+    return [n, h, w, c, pool[0], pool[1], strides[0], strides[1], pt, pl, ho, wo]
+
+
+def maxpool_fwd(x, y, arg, pool, strides, padding):
+    g = pool_geo(x.shape, pool, strides, padding)
+    _C().maxpool_fwd(_ptr(x), g, _ptr(y), _ptr(arg), stream_handle())
+
+
+def maxpool_bwd(dy, arg, dx, pool, strides, padding):
+    g = pool_geo(dx.shape, pool, strides, padding)
+    _C().maxpool_bwd(_ptr(dy), _ptr(arg), g, _ptr(dx), stream_handle())
+
+
+def gap_fwd(x, y):
+    n, h, w, c = x.shape
+    _C().gap_fwd(_ptr(x), n, h * w, c, _ptr(y), int(y.dtype == torch.float32), stream_handle())
+
+
+def gap_bwd(dy, dx):
+    n, h, w, c = dx.shape
+    _C().gap_bwd(_ptr(dy), int(dy.dtype == torch.float32), n, h * w, c, _ptr(dx), stream_handle())
+
+
+def relu_bwd(dy, y, dz):
+    _C().relu_bwd(_ptr(dy), _ptr(y), _ptr(dz), dy.numel(), stream_handle())
+
+
+def add_bf16(a, b, out):
+    _C().add_bf16(_ptr(a), _ptr(b), _ptr(out), a.numel(), stream_handle())
+
+
+def colsum(x, out):
+    M, N = x.shape[0], x.shape[-1]
+    M = x.numel() // N
+    _C().colsum(_ptr(x), int(x.dtype == torch.float32), M, N, N, _ptr(out), stream_handle())
+
+
+def softmax_xent(logits, labels, K, scale, dlogits, tail):
+    B, ld = logits.shape
+    _C().softmax_xent(_ptr(logits), ld, _ptr(labels), B, K, float(scale), _ptr(dlogits), _ptr(tail),
+                      stream_handle())
+
+
+def sgd_flat(P, G, V, Pb, lr, momentum=0.0, nesterov=False):
+    _C().sgd_flat(_ptr(P), _ptr(G), _ptr(V), _ptr(Pb), P.numel(), float(lr), float(momentum), int(nesterov),
+                  stream_handle())
+
+
+def cast_bf16(x, y):
+    _C().cast_f32_bf16(_ptr(x), _ptr(y), x.numel(), stream_handle())
+
+
+def pad_cast(src, R, C1, C2, C1p, C2p, dst):
+    _C().pad_cast(_ptr(src), R, C1, C2, C1p, C2p, _ptr(dst), stream_handle())
+
+
+def unpad_add(src, R, C1, C2, C1p, C2p, dst):
+    _C().unpad_add(_ptr(src), R, C1, C2, C1p, C2p, _ptr(dst), stream_handle())

@@ -94,6 +94,9 @@ def shutdown() -> None:
                 except Exception:  # pragma: no cover
                     pass
             _RT = None
+            from . import strategy as _strategy
+
+            _strategy._reset_default()  # the default strategy caches the runtime
 
 
 def local_runtime_for_tests(device: str = "cpu") -> Runtime:

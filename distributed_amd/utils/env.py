@@ -33,6 +33,7 @@ def get_str(name: str, default: str) -> str:
 # Documented knobs (README "Configuration"):
 #   DAMD_DEVICE            cpu | cuda          force the compute device
 #   DAMD_FUSED             0/1                 allow the fused native ConvNet engine (default 1)
+#   DAMD_NATIVE_GRAPH      0/1                 allow the native graph engine (HIP plan + graph, default 1)
 #   DAMD_GRAPH             0/1                 capture steps into hipGraphs (default 1)
 #   DAMD_GRAPH_STEPS       int                 steps per captured graph (default 20)
 #   DAMD_PP                1..4                pooled positions per fused slice (default 4)

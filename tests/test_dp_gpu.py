@@ -31,27 +31,29 @@ def _load(out, r):
         return w, json.load(f)
 
 
-@pytest.mark.parametrize("engine", ["fused", "generic"])
+@pytest.mark.parametrize("engine", ["fused", "native_graph", "generic"])
 @pytest.mark.timeout(600)
 def test_two_ranks_one_gpu_match_single_rank(tmp_path, engine):
     fused = "1" if engine == "fused" else "0"
+    ng = "1" if engine == "native_graph" else "0"
     d2 = tmp_path / "w2"
     d2.mkdir()
-    res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=32, DAMD_FUSED=fused),
+    res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=32, DAMD_FUSED=fused,
+                                                           DAMD_NATIVE_GRAPH=ng),
                                timeout=420)
     assert res.ok, res.returncodes
     (w0, j0), (w1, j1) = _load(d2, 0), _load(d2, 1)
     assert j0["world"] == 2 and j0["engine"] == j1["engine"]
-    assert j0["engine"] == ("fused_convnet" if engine == "fused" else "generic")
+    assert j0["engine"] == {"fused": "fused_convnet", "native_graph": "native_graph", "generic": "generic"}[engine]
     assert all(np.array_equal(a, b) for a, b in zip(w0, w1)), "mirrored variables diverged"
     assert j0["history"] == j1["history"]
     d1 = tmp_path / "w1"
     d1.mkdir()
-    res = launch.launch_script([WORKER], nproc=1, env=_env(d1, DAMD_TEST_PER_REPLICA=64, DAMD_FUSED=fused,
+    res = launch.launch_script([WORKER], nproc=1, env=_env(d1, DAMD_TEST_PER_REPLICA=64, DAMD_FUSED=fused, DAMD_NATIVE_GRAPH=ng,
                                                            DAMD_TEST_INIT_FROM=d2 / "init0.npz"), timeout=420)
     assert res.ok, res.returncodes
     ws, js = _load(d1, 0)
-    tol = dict(rtol=2e-3, atol=2e-4) if engine == "fused" else dict(rtol=1e-3, atol=1e-5)
+    tol = dict(rtol=1e-3, atol=1e-5) if engine == "generic" else dict(rtol=2e-3, atol=2e-4)
     for a, b in zip(w0, ws):
         np.testing.assert_allclose(a, b, **tol)
     np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-3)

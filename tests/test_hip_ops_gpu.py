@@ -1,0 +1,238 @@
+"""Numerics of the generic-path HIP kernels (csrc/kernels/gemm.hip, layer_ops.hip)
+against plain PyTorch fp32 references of the same ops (distributed_amd/ops/reference.py).
+
+bf16 operands are rounded once and then fed to BOTH sides, so the only differences are
+fp32 accumulation order (and the bf16 rounding of bf16 outputs).  Matrices are
+asymmetric and shapes ragged (M, N, K not multiples of the tiles) so transposed /
+swapped operand maps and tail handling are exercised (cdna_hip_programming.md §3)."""
+import pytest
+import torch
+
+from distributed_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+@pytest.fixture(scope="module")
+def H():
+    from distributed_amd.ops import hip
+
+    return hip
+
+
+def rb(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev)
+
+
+def close(a, b, rtol, atol_frac):
+    a, b = a.float(), b.float()
+    atol = atol_frac * b.abs().max().item() + 1e-12
+    err = (a - b).abs().max().item()
+    assert torch.allclose(a, b, rtol=rtol, atol=atol), f"max abs err {err:.3e} (atol {atol:.3e})"
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 512, 1000), (100, 72, 24), (300, 5408, 64), (1, 8, 8), (257, 96, 136)])
+@pytest.mark.parametrize("relu,bias,out_bf16", [(False, False, False), (True, True, True), (False, True, False)])
+def test_dense_fwd(H, M, K, N, relu, bias, out_bf16):
+    x = rb(rnd(M, K, seed=1))
+    w = rb(rnd(K, N, scale=0.1, seed=2))
+    b = rnd(N, seed=3) if bias else None
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    H.dense_fwd(x.bfloat16(), w.bfloat16(), out, bias=b, relu=relu)
+    r = x @ w
+    if bias:
+        r = r + b
+    if relu:
+        r = r.relu()
+    close(out, r, 1e-2 if out_bf16 else 1e-4, 4e-3 if out_bf16 else 1e-5)
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 512, 1000), (64, 5408, 64), (37, 24, 40)])
+def test_dense_backward(H, M, K, N):
+    x = rb(rnd(M, K, seed=4))
+    w = rb(rnd(K, N, scale=0.1, seed=5))
+    dy = rb(rnd(M, N, seed=6))
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    H.dense_dgrad(dy.bfloat16(), w.bfloat16(), dx)
+    close(dx, dy @ w.t(), 1e-2, 4e-3)
+    # accumulate mode adds onto what dx already holds
+    H.dense_dgrad(dy.bfloat16(), w.bfloat16(), dx, accumulate=True)
+    close(dx, 2 * (dy @ w.t()), 1e-2, 8e-3)
+    dw = torch.zeros(K, N, device=dev)
+    H.dense_wgrad(x.bfloat16(), dy.bfloat16(), dw)
+    close(dw, x.t() @ dy, 1e-4, 1e-5)
+
+
+CONV_CASES = [
+    # n, h, cin, cout, k, s, padding
+    (2, 9, 8, 16, 3, 1, "same"),
+    (2, 10, 16, 64, 3, 2, "same"),
+    (2, 14, 8, 64, 7, 2, "same"),
+    (3, 7, 64, 128, 1, 2, "valid"),
+    (2, 12, 24, 40, 3, 1, "valid"),
+    (1, 8, 128, 256, 3, 2, "same"),
+]
+
+
+@pytest.mark.parametrize("n,h,cin,cout,k,s,padding", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(H, n, h, cin, cout, k, s, padding):
+    x = rb(rnd(n, h, h, cin, seed=7)).requires_grad_(True)
+    w = rb(rnd(k, k, cin, cout, scale=0.2, seed=8)).requires_grad_(True)
+    y = ref.conv2d(x, w, None, (s, s), padding)
+    dy = rb(rnd(*y.shape, seed=9))
+    gx, gw = torch.autograd.grad(y, (x, w), dy)
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_fwd(x.detach().bfloat16(), w.detach().bfloat16(), out, (s, s), padding)
+    close(out, y.detach(), 1e-2, 4e-3)
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_dgrad(dy.bfloat16(), w.detach().bfloat16(), dx, (s, s), padding)
+    close(dx, gx, 1e-2, 4e-3)
+    dw = torch.zeros(w.shape, device=dev)
+    H.conv_wgrad(x.detach().bfloat16(), dy.bfloat16(), dw, (s, s), padding)
+    close(dw, gw, 1e-4, 2e-5)
+
+
+def test_conv_bias_relu_and_stats(H):
+    n, h, cin, cout = 4, 11, 16, 72
+    x = rb(rnd(n, h, h, cin, seed=10))
+    w = rb(rnd(3, 3, cin, cout, scale=0.2, seed=11))
+    b = rnd(cout, seed=12)
+    y = ref.conv2d(x, w, b, (1, 1), "same")
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", bias=b, relu=True)
+    close(out, y.relu(), 1e-2, 4e-3)
+    # BN statistics in the epilogue: per-M-tile partial column sums of the stored values
+    rows = H.tile_rows(H.pick_tile(cout))
+    T = -(-(n * h * h) // rows)
+    st = torch.zeros(T, 2, cout, device=dev)
+    H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", stats=st)
+    yb = out.float().reshape(-1, cout)
+    close(st[:, 0].sum(0), yb.sum(0), 1e-4, 1e-5)
+    close(st[:, 1].sum(0), (yb * yb).sum(0), 1e-4, 1e-5)
+
+
+@pytest.mark.parametrize("relu,res", [(False, None), (True, None), (True, "raw"), (True, "bn")])
+def test_batchnorm_train_fwd_bwd(H, relu, res):
+    n, h, C = 4, 6, 48
+    M = n * h * h
+    x = rb(rnd(n, h, h, C, scale=2.0, seed=13) + 0.5)
+    g = rnd(C, seed=14).abs() + 0.5
+    be = rnd(C, seed=15)
+    r = rb(rnd(n, h, h, C, seed=16))
+    g2, be2 = rnd(C, seed=17).abs() + 0.5, rnd(C, seed=18)
+    eps, mom = 1e-3, 0.99
+    # torch reference
+    xr = x.clone().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), be.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    yr = ref.batchnorm(xr, gr, br, rm, rv, True, mom, eps)
+    if res == "raw":
+        yr = yr + rr
+    elif res == "bn":
+        yr = yr + ref.batchnorm(rr, g2, be2, torch.zeros(C, device=dev), torch.ones(C, device=dev), True, mom, eps)
+    if relu:
+        yr = yr.relu()
+    dy = rb(rnd(*yr.shape, seed=19))
+    grads = torch.autograd.grad(yr, (xr, gr, br, rr) if res else (xr, gr, br), dy)
+    # HIP: stats from a plain column-sum pass (as the GEMM epilogue would give)
+    xf = x.reshape(M, C)
+    part = torch.stack([xf.sum(0), (xf * xf).sum(0)]).unsqueeze(0).contiguous()
+    st = torch.empty(4, C, device=dev)
+    mean = torch.zeros(C, device=dev)
+    var = torch.ones(C, device=dev)
+    H.bn_finalize(part, 1, C, M, g, be, eps, mom, mean, var, st)
+    close(mean, rm, 1e-5, 1e-6)
+    close(var, rv, 1e-5, 1e-6)
+    st2 = None
+    if res == "bn":
+        rf = r.reshape(M, C)
+        p2 = torch.stack([rf.sum(0), (rf * rf).sum(0)]).unsqueeze(0).contiguous()
+        st2 = torch.empty(4, C, device=dev)
+        H.bn_finalize(p2, 1, C, M, g2, be2, eps, mom, None, None, st2)
+    y = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.bn_apply(x.bfloat16(), st, y, relu=relu, r=r.bfloat16() if res else None, st2=st2)
+    close(y, yr.detach(), 1e-2, 5e-3)
+    from distributed_amd.native import require_C
+
+    T = require_C().bn_bwd_blocks(M, C)
+    bpart = torch.empty(T, 2, C, device=dev)
+    co = torch.empty(3, C, device=dev)
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    dg, db = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+    dz = torch.empty(x.shape, device=dev, dtype=torch.bfloat16) if res else None
+    # the HIP backward takes the relu mask from the bf16 block output y
+    H.bn_bwd(dy.bfloat16(), y, relu, x.bfloat16(), st, bpart, co, dx, dg, db, dz_out=dz)
+    if relu and res is None:
+        # mask from the kernel's own output (a bf16-rounded 0 can differ from fp32 sign)
+        pass
+    close(dx, grads[0], 2e-2, 1e-2)
+    close(dg, grads[1], 1e-3, 1e-3)
+    close(db, grads[2], 1e-3, 1e-3)
+    if res == "raw":
+        close(dz, grads[3], 1e-2, 4e-3)
+
+
+@pytest.mark.parametrize("pool,strides,padding,h", [((3, 3), (2, 2), "same", 12), ((2, 2), (2, 2), "valid", 26),
+                                                    ((3, 3), (2, 2), "same", 7)])
+def test_maxpool(H, pool, strides, padding, h):
+    C = 32
+    x = rb(rnd(2, h, h, C, seed=20)).requires_grad_(True)
+    y = ref.maxpool2d(x, pool, strides, padding)
+    dy = rb(rnd(*y.shape, seed=21))
+    (gx,) = torch.autograd.grad(y, (x,), dy)
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    arg = torch.empty(y.shape, device=dev, dtype=torch.uint8)
+    H.maxpool_fwd(x.detach().bfloat16(), out, arg, pool, strides, padding)
+    close(out, y.detach(), 0, 0)
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.maxpool_bwd(dy.bfloat16(), arg, dx, pool, strides, padding)
+    close(dx, gx, 1e-2, 4e-3)
+
+
+def test_gap_xent_colsum_sgd(H):
+    x = rb(rnd(3, 7, 7, 64, seed=22))
+    y32 = torch.empty(3, 64, device=dev)
+    H.gap_fwd(x.bfloat16(), y32)
+    close(y32, x.mean(dim=(1, 2)), 1e-4, 1e-5)
+    dy = rnd(3, 64, seed=23)
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.gap_bwd(dy, dx)
+    close(dx, (dy / 49)[:, None, None, :].expand(x.shape), 1e-2, 4e-3)
+    # softmax xent over a padded row pitch
+    B, K, ld = 5, 10, 16
+    z = rnd(B, ld, seed=24)
+    lab = torch.tensor([0, 3, 9, 9, 1], device=dev, dtype=torch.int32)
+    dl = torch.zeros(B, ld, device=dev, dtype=torch.bfloat16)
+    tail = torch.zeros(3, device=dev)
+    H.softmax_xent(z, lab, K, 0.5, dl, tail)
+    zz = z[:, :K].clone().requires_grad_(True)
+    loss = ref.sparse_softmax_xent(zz, lab)
+    (gz,) = torch.autograd.grad(loss.sum() * 0.5, (zz,))
+    close(dl[:, :K], gz, 1e-2, 4e-3)
+    assert dl[:, K:].abs().max().item() == 0
+    close(tail[0], loss.sum(), 1e-5, 1e-6)
+    assert tail[1].item() == ref.sparse_accuracy(z[:, :K], lab).sum().item()
+    assert tail[2].item() == B
+    # column sums (bias grads)
+    a = rb(rnd(300, 24, seed=25))
+    cs = torch.zeros(24, device=dev)
+    H.colsum(a.bfloat16(), cs)
+    close(cs, a.sum(0), 1e-4, 1e-5)
+    # flat SGD (+momentum, nesterov) with the bf16 shadow
+    n = 1001
+    P, G, V = rnd(n, seed=26), rnd(n, seed=27), rnd(n, seed=28)
+    Pb = torch.empty(n, device=dev, dtype=torch.bfloat16)
+    p0, v0 = P.clone(), V.clone()
+    H.sgd_flat(P, G, V, Pb, 0.1, 0.9, True)
+    vn = 0.9 * v0 - 0.1 * G
+    close(V, vn, 1e-6, 1e-7)
+    close(P, p0 + 0.9 * vn - 0.1 * G, 1e-6, 1e-7)
+    assert torch.equal(Pb, P.bfloat16())
