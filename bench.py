@@ -30,12 +30,17 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--per-gpu-batch", type=int, default=64)
-    ap.add_argument("--engine", choices=["auto", "fused", "generic"], default="auto")
+    ap.add_argument("--engine", choices=["auto", "fused", "native", "generic"], default="auto")
+    ap.add_argument("--model", choices=["mnist", "resnet18"], default="mnist",
+                    help="mnist = the headline config (BASELINE.json); resnet18 = BASELINE.json config 4")
+    ap.add_argument("--samples", type=int, default=None, help="synthetic dataset rows")
     ap.add_argument("--graph-steps", type=int, default=None)
     args = ap.parse_args()
 
-    if args.engine == "generic":
+    if args.engine in ("generic", "native"):
         os.environ["DAMD_FUSED"] = "0"
+    if args.engine == "generic":
+        os.environ["DAMD_NATIVE_GRAPH"] = "0"
     if args.graph_steps:
         os.environ["DAMD_GRAPH_STEPS"] = str(args.graph_steps)
 
@@ -57,23 +62,32 @@ def main():
     B = args.per_gpu_batch
     GB = B * n
 
-    (x, y), _ = tf.keras.datasets.mnist.load_data()
-    x = x.reshape(len(x), 28, 28, 1) / 255.0
-
-    with strategy.scope():
-        model = tf.models.mnist_cnn()
-        tf.models.compile_reference(model, 0.001)
+    if args.model == "mnist":
+        (x, y), _ = tf.keras.datasets.mnist.load_data()
+        x = x.reshape(len(x), 28, 28, 1) / 255.0
+        with strategy.scope():
+            model = tf.models.mnist_cnn()
+            tf.models.compile_reference(model, 0.001)
+    else:
+        rows = args.samples or max(4 * GB, 256)
+        rng = np.random.default_rng(1234)
+        x = (rng.integers(0, 256, size=(rows, 224, 224, 3), dtype=np.uint8) / np.float32(255.0)).astype(np.float32)
+        y = rng.integers(0, 1000, size=rows).astype(np.int64)
+        with strategy.scope():
+            model = tf.models.resnet18()
+            tf.models.compile_resnet(model, 0.1, 0.9)
     engine = model._get_engine(B, GB)
     engine.bind(x, y)
     wrap = len(x) // GB
-    if engine.name == "fused_convnet":
+    device_wrap = engine.name in ("fused_convnet", "native_graph")
+    if device_wrap:
         engine.start_epoch(0, True, wrap_steps=wrap)
     else:
         engine.start_epoch(0, True)
 
     def run(k):
         # generic engine has no device-side wrap: restart epochs on the host
-        if engine.name != "fused_convnet":
+        if not device_wrap:
             while k > 0:
                 left = wrap - engine.step_in_epoch
                 if left <= 0:
@@ -116,8 +130,9 @@ def main():
     ms = dt * 1e3 / args.steps
     value = GB * args.steps / dt
     if rt.rank == 0:
+        resnet = args.model == "resnet18"
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not resnet else "images/sec (whole node) ResNet-18 synthetic 224x224x3",
             "value": round(value, 1),
             "unit": "images/sec",
             "n_gpus": n,
@@ -126,17 +141,19 @@ def main():
             "ms_per_step": round(ms, 5),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_IMG_S, 2),
+            "vs_baseline": None if resnet else round(value / BASELINE_IMG_S, 2),
             "dtype": "bf16" if on_gpu else "fp32",
-            "data": "synthetic (28x28x1 MNIST-shaped, 60000 rows, random-init weights)",
+            "data": (f"synthetic ({len(x)} rows 224x224x3 k/255, 1000 classes, random-init weights)" if resnet else
+                     "synthetic (28x28x1 MNIST-shaped, 60000 rows, random-init weights)"),
             "config": {
-                "model": "MNIST CNN (Conv2D32-3x3-relu, MaxPool2, Dense64-relu, Dense10; 347,146 params)",
+                "model": ("ResNet-18 (11,689,512 params, BN, 1000 classes)" if resnet else
+                          "MNIST CNN (Conv2D32-3x3-relu, MaxPool2, Dense64-relu, Dense10; 347,146 params)"),
                 "global_batch": GB,
                 "per_gpu_batch": B,
                 "seq_len": None,
                 "parallelism": f"dp{n}",
                 "engine": engine.name,
-                "optimizer": "SGD(lr=1e-3), fp32 master weights",
+                "optimizer": ("SGD(lr=0.1, momentum=0.9)" if resnet else "SGD(lr=1e-3)") + ", fp32 master weights",
             },
             "final_epoch_loss": round(m.get("loss", float("nan")), 4),
         }

@@ -249,3 +249,19 @@ class BackupAndRestore(Callback):
             for p in (self._ckpt, self._meta):
                 if os.path.exists(p):
                     os.remove(p)
+
+
+class MirrorCheck(Callback):
+    """Assert after every ``every`` epochs that all replicas hold bitwise-identical
+    variables (distributed_amd/utils/debug.py); raises MirrorDivergenceError otherwise."""
+
+    def __init__(self, every: int = 1):
+        super().__init__()
+        self.every = max(1, int(every))
+        self.fingerprints = []
+
+    def on_epoch_end(self, epoch, logs=None):
+        if (epoch + 1) % self.every == 0:
+            from ..utils.debug import check_mirrored
+
+            self.fingerprints.append(check_mirrored(self.model, tag=f"epoch {epoch + 1}"))

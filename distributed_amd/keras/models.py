@@ -24,7 +24,9 @@ import torch
 
 from ..parallel import runtime as _runtime
 from ..parallel.strategy import MultiWorkerMirroredStrategy, get_strategy
+from ..utils import debug as _debug
 from ..utils import logging as dlog
+from ..utils import profile as _profile
 from . import backend as K
 from . import callbacks as cbks
 from . import layers as L
@@ -215,6 +217,7 @@ class Model(L.Layer):
             dlog.info("Collective batch_all_reduce: 1 all-reduces (%d grads + metric tail, %s), num_workers = %d",
                       len(self.trainable_weights), engine.name, world)
         per_hook = cl.needs_batch_hooks
+        mirror_every = _debug.mirror_check_every()
         refresh_s = 0.5
         global_step = 0
         try:
@@ -227,7 +230,12 @@ class Model(L.Layer):
                     k = min(chunk, steps - done)
                     if fail_at is not None and global_step <= fail_at < global_step + k:
                         raise RuntimeError(f"DAMD_FAIL_AT: injected failure at step {fail_at}")
+                    prof = _profile.active()
+                    rec = prof.begin(k, batch_size, st.device) if prof else None
                     engine.run(k)
+                    if rec is not None:
+                        prof.end(rec)
+                    _debug.debug_sync(st.device)
                     done += k
                     global_step += k
                     if per_hook or (verbose == 1 and time.time() - last_ui > refresh_s):
@@ -243,6 +251,8 @@ class Model(L.Layer):
                                          steps=validation_steps, _return_dict=True)
                     logs.update({"val_" + k: v for k, v in vres.items()})
                 cl.on_epoch_end(epoch, {k: v for k, v in logs.items()})
+                if mirror_every and (epoch + 1) % mirror_every == 0:
+                    _debug.check_mirrored(self, st, tag=f"epoch {epoch + 1}")
                 if self.stop_training:
                     break
         except BaseException:

@@ -51,6 +51,21 @@ def main():
                    "iterations": int(model.optimizer.iterations)}, f)
     if rank == 0:
         np.savez(os.path.join(out, "init0.npz"), *init)
+    if os.environ.get("DAMD_TEST_DIVERGE"):
+        from distributed_amd.utils.debug import MirrorDivergenceError, check_mirrored
+
+        check_mirrored(model)  # equal after training
+        if rank == 1:
+            w = model.get_weights()
+            w[1][0] += 1e-6
+            model.set_weights(w)
+        try:
+            check_mirrored(model)
+            verdict = "missed"
+        except MirrorDivergenceError:
+            verdict = "detected"
+        with open(os.path.join(out, f"diverge{rank}.txt"), "w") as f:
+            f.write(verdict)
     from distributed_amd.parallel import runtime
 
     runtime.shutdown()

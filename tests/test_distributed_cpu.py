@@ -32,7 +32,8 @@ def _load(out, r):
 def test_two_workers_mirror_and_match_single_worker(tmp_path):
     d2 = tmp_path / "w2"
     d2.mkdir()
-    res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=16), timeout=240)
+    res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=16, DAMD_CHECK_MIRRORS=1,
+                                                           DAMD_TEST_DIVERGE=1), timeout=240)
     assert res.ok, res.returncodes
     (w0, j0), (w1, j1) = _load(d2, 0), _load(d2, 1)
     assert j0["world"] == j1["world"] == 2
@@ -41,6 +42,10 @@ def test_two_workers_mirror_and_match_single_worker(tmp_path):
     # global metrics: identical History on every worker (README.md:229-231)
     assert j0["history"] == j1["history"]
     assert j0["iterations"] == 6
+    # the mirror-divergence detector ran every epoch inside fit (no error) and catches a
+    # 1e-6 perturbation of one replica's bias
+    for r in (0, 1):
+        assert open(d2 / f"diverge{r}.txt").read() == "detected"
     # N-worker DP at global batch B == 1 worker at batch B from the same initial weights
     d1 = tmp_path / "w1"
     d1.mkdir()

@@ -78,6 +78,145 @@ def _compare_updates(init, wa, wb, names, cos_min=0.98, rel_max=0.08):
         assert cos > cos_min and rel < rel_max, f"{nm}: cos {cos:.4f} rel {rel:.4f}"
 
 
+class _Q(torch.autograd.Function):
+    """Round to bf16 in forward AND backward: a tensor the native plan stores in bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+class _QW(torch.autograd.Function):
+    """bf16 weight shadow: rounded operand, straight-through gradient."""
+
+    @staticmethod
+    def forward(ctx, w):
+        return w.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
+class _QG(torch.autograd.Function):
+    """fp32 value, bf16-rounded gradient (the logits: fp32 out, bf16 dlogits)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+def _emulated_reference_grads(engine, model, x, y, global_batch):
+    """fp32 PyTorch re-execution of the engine's own (fused) plan with bf16 rounding at
+    exactly the tensors the plan stores in bf16.  Returns {variable id: grad}."""
+    from distributed_amd.ops import reference as ref
+
+    dev = engine.device
+    leaves = {}
+    for v in model.trainable_weights:
+        leaves[id(v)] = v.value.detach().clone().requires_grad_(True)
+    relu = torch.relu
+    vals = {}
+    x0 = torch.from_numpy(x).to(dev).float()
+    vals[id(engine.x0.root())] = _Q.apply(x0)
+    norm = {}
+
+    def get(t):
+        return vals[id(t.root())]
+
+    def bn_norm(nd, xin):
+        l = nd.layer
+        m = xin.mean(dim=(0, 1, 2))
+        v = xin.var(dim=(0, 1, 2), unbiased=False)
+        return (xin - m) * torch.rsqrt(v + l.epsilon) * leaves[id(l.gamma)] + leaves[id(l.beta)]
+
+    logits = None
+    for nd in engine.nodes:
+        if nd.attrs.get("dead"):
+            continue
+        l, k = nd.layer, nd.kind
+        if k == "Conv2D":
+            yv = ref.conv2d(get(nd.inputs[0])[..., :l.kernel.shape[2]], _QW.apply(leaves[id(l.kernel)]),
+                            leaves[id(l.bias)] if l.use_bias else None, l.strides, l.padding)
+            if getattr(l.activation, "__name__", "") == "relu":
+                yv = relu(yv)
+            vals[id(nd.out.root())] = _Q.apply(yv)
+        elif k == "BatchNormalization":
+            z = bn_norm(nd, get(nd.inputs[0]))
+            if nd.attrs.get("stats_only"):
+                norm[id(nd)] = z
+            else:
+                vals[id(nd.out.root())] = _Q.apply(relu(z) if nd.attrs.get("relu") else z)
+        elif k == "Add":
+            fused = nd.attrs.get("fused")
+            if fused is None:
+                z = get(nd.inputs[0]) + get(nd.inputs[1])
+            else:
+                main, (mode, other) = fused
+                z = norm[id(main)] + (get(other) if mode == "raw" else norm[id(other)])
+            vals[id(nd.out.root())] = _Q.apply(relu(z) if nd.attrs.get("relu") else z)
+        elif k in ("Activation", "ReLU"):
+            vals[id(nd.out.root())] = _Q.apply(relu(get(nd.inputs[0])))
+        elif k == "MaxPooling2D":
+            vals[id(nd.out.root())] = _Q.apply(ref.maxpool2d(get(nd.inputs[0]), l.pool_size, l.strides, l.padding))
+        elif k == "GlobalAveragePooling2D":
+            vals[id(nd.out.root())] = _Q.apply(get(nd.inputs[0]).mean(dim=(1, 2)))
+        elif k == "Dense":
+            xin = get(nd.inputs[0]).reshape(x.shape[0], -1)
+            z = xin @ _QW.apply(leaves[id(l.kernel)])
+            if l.use_bias:
+                z = z + leaves[id(l.bias)]
+            if nd.attrs.get("logits"):
+                logits = _QG.apply(z)
+            else:
+                vals[id(nd.out.root())] = _Q.apply(relu(z) if getattr(l.activation, "__name__", "") == "relu"
+                                                   else z)
+    loss = ref.sparse_softmax_xent(logits, torch.from_numpy(y).to(dev)).sum() / global_batch
+    ids = list(leaves)
+    grads = torch.autograd.grad(loss, [leaves[i] for i in ids], allow_unused=True)
+    return {i: g for i, g in zip(ids, grads)}, float(loss)
+
+
+def test_small_resnet_step_matches_bf16_emulated_reference():
+    """The plan's wiring (fusion, residual fan-in, BN backward, padding, split-K
+    accumulation) against an fp32 re-execution with the same bf16 storage points: after
+    one plain-SGD step every weight update must agree closely."""
+    x, y = _data(32, (32, 32, 3), 10, seed=4)
+    os.environ["DAMD_FUSED"] = "0"
+    try:
+        tf.keras.backend.clear_session()
+        m = _small_resnet()
+        lr = 0.1
+        m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tf.keras.optimizers.SGD(learning_rate=lr), metrics=["accuracy"])
+        e = m._get_engine(32, 32)
+        assert e.name == "native_graph"
+        e.bind(x, y)
+        e.start_epoch(0, False)
+        w0 = {id(v): v.value.detach().clone() for v in m.trainable_weights}
+        grads, ref_loss = _emulated_reference_grads(e, m, x, y, 32)
+        e.run(1)
+        e.sync()
+        met = e.metrics()
+        assert abs(met["loss"] - ref_loss) < 2e-3 * abs(ref_loss)
+        for v in m.trainable_weights:
+            d_native = (v.value.detach() - w0[id(v)]).double().ravel()
+            d_ref = (-lr * grads[id(v)]).double().ravel()
+            nref = d_ref.norm().item()
+            rel = (d_native - d_ref).norm().item() / max(nref, 1e-12)
+            assert rel < 2e-2, f"{v.name}: rel err {rel:.4f} (|d| {nref:.3e})"
+    finally:
+        os.environ.pop("DAMD_FUSED", None)
+
+
 def test_small_resnet_one_step_matches_fp32_reference():
     tf.keras.backend.clear_session()
     x, y = _data(64, (32, 32, 3), 10)
@@ -88,7 +227,11 @@ def test_small_resnet_one_step_matches_fp32_reference():
     wr, hr, er = _train(_small_resnet, x, y, init, 32, 1, native=False, device="cpu")
     assert en == "native_graph" and er == "generic"
     assert abs(hn["loss"][0] - hr["loss"][0]) < 2e-2 * abs(hr["loss"][0])
-    _compare_updates(init, wn, wr, names)
+    # bf16 storage of pre-BN activations and gradients vs a pure fp32 run: the head is
+    # tight, deep layers drift (|mean|/std of conv outputs amplifies bf16 rounding in
+    # x-hat, and BN backward cancellation amplifies it again); wiring is checked
+    # exactly by the emulated-reference test above
+    _compare_updates(init, wn, wr, names, cos_min=0.93, rel_max=0.4)
 
 
 def test_mnist_native_graph_tracks_reference_over_steps():
@@ -99,18 +242,22 @@ def test_mnist_native_graph_tracks_reference_over_steps():
     wr, hr, er = _train(_mnist, x, y, init, 64, 10, native=False, device="cpu", lr=0.05, momentum=0.9)
     assert en == "native_graph"
     np.testing.assert_allclose(hn["loss"], hr["loss"], rtol=1e-2)
-    _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=0.99, rel_max=0.05)
+    _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=0.97, rel_max=0.25)
 
 
 def test_graph_replay_equals_eager():
+    """Replaying the captured step == running it eagerly.  Two steps: step 1 eager in both,
+    step 2 replayed vs eager.  (Longer runs drift apart by run-to-run noise either way:
+    wgrad split-K partials are combined with fp32 atomics, and at lr 0.1 a 1-ulp weight
+    difference can flip a bf16 shadow rounding.)"""
     x, y = _data(128, (32, 32, 3), 10, seed=2)
     tf.keras.backend.clear_session()
     init = _small_resnet().get_weights()
-    wg, hg, _ = _train(_small_resnet, x, y, init, 32, 4, native=True, momentum=0.9, graph=True)
-    we, he, _ = _train(_small_resnet, x, y, init, 32, 4, native=True, momentum=0.9, graph=False)
+    wg, hg, _ = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9, graph=True)
+    we, he, _ = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9, graph=False)
     for a, b in zip(wg, we):
-        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
-    np.testing.assert_allclose(hg["loss"], he["loss"], rtol=1e-4)
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(hg["loss"], he["loss"], rtol=1e-5)
 
 
 def test_resnet18_full_size_trains():
