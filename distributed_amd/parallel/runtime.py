@@ -115,10 +115,15 @@ def describe() -> str:
 
 
 def fault_injection_step() -> Optional[int]:
-    """``DAMD_FAIL_AT=rank:step`` -> step index at which this rank must raise."""
+    """``DAMD_FAIL_AT=rank:step[:attempt]`` -> the global step at which this rank raises.
+    With ``attempt`` the failure fires only in that launcher attempt
+    (``DAMD_RESTART_COUNT``), so a gang restart can then run to completion."""
     v = os.environ.get("DAMD_FAIL_AT")
     if not v:
         return None
-    r, s = v.split(":")
+    parts = v.split(":")
+    r, s = int(parts[0]), int(parts[1])
+    if len(parts) > 2 and int(os.environ.get("DAMD_RESTART_COUNT", "0")) != int(parts[2]):
+        return None
     rt = get()
-    return int(s) if int(r) == rt.rank else None
+    return s if r == rt.rank else None

@@ -172,3 +172,28 @@ def test_bench_two_ranks_cpu(tmp_path):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["global_batch"] == 128 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and out["steps"] == 3 and out["scaling"] == "weak"
+
+
+@pytest.mark.timeout(400)
+def test_injected_failure_gang_restart_resumes_from_backup(tmp_path):
+    """Rank 1 dies mid-epoch-3 on the first attempt (DAMD_FAIL_AT=1:7:0); the launcher
+    restarts the gang, BackupAndRestore resumes after epoch 2, and the final weights equal
+    an uninterrupted run's (README.md:400 "Workers will need to restart training")."""
+    ft = os.path.join(ROOT, "tests", "helpers", "ft_worker.py")
+    ref = tmp_path / "ref"
+    ref.mkdir()
+    res = launch.launch_script([ft], nproc=2, env=_env(ref), timeout=240)
+    assert res.ok, res.returncodes
+    run = tmp_path / "ft"
+    run.mkdir()
+    res = launch.launch_script([ft], nproc=2, env=_env(run, DAMD_FAIL_AT="1:7:0"), timeout=240, max_restarts=1)
+    assert res.ok, res.returncodes
+    w_ref, j_ref = _load(ref, 0)
+    w_ft, j_ft = _load(run, 0)
+    assert j_ft["attempt"] == 1 and j_ref["attempt"] == 0
+    assert j_ft["iterations"] == j_ref["iterations"] == 12
+    for a, b in zip(w_ft, w_ref):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    # the resumed attempt trained epochs 3-4 only
+    assert len(j_ft["history"]["loss"]) == 2
+    np.testing.assert_allclose(j_ft["history"]["loss"], j_ref["history"]["loss"][2:], rtol=1e-6)
