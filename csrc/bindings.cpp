@@ -62,7 +62,7 @@ class ConvNetTrainer : public StepExecutor {
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
-    if (grad_allreduce_ && comm_ && comm_->nranks() > 1)
+    if (grad_allreduce_ && comm_)  // comm set only when a reduction is wanted
       comm_->allreduce(b_.G, b_.G, convnet_grad_count(PP_), 0, 0, stream_);
   }
 

@@ -130,7 +130,10 @@ class FusedConvNetEngine(Engine):
             self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)
             bufs["stamps"] = self.stamps.data_ptr()
         self.trainer = C.ConvNetTrainer(dev.index or 0, bufs, B, self.PP, 1)
-        native = strategy.communicator.native if self.world > 1 else None
+        # DAMD_FORCE_ALLREDUCE=1 keeps the (size-1) RCCL all-reduce inside the captured step
+        # at world 1: the multi-GPU graph path exercised on a single GPU
+        force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
+        native = strategy.communicator.native if (self.world > 1 or force) else None
         # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
         # time, the gradient/metric buffer all-reduced through the host between steps
         self.host_collective = self.world > 1 and native is None

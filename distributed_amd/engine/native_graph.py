@@ -200,12 +200,14 @@ class NativeGraphEngine(Engine):
         c[C_IT] = int(opt.iterations)
         self.ctrl.copy_(c.to(dev))
         self._write_hparams()
-        self.native_comm = strategy.communicator.native if self.world > 1 else None
+        force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)  # exercise the RCCL path at world 1
+        self.native_comm = strategy.communicator.native if (self.world > 1 or force) else None
         self.host_collective = self.world > 1 and self.native_comm is None
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph = None
         self.feed = None
         self._plan()
+        self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0))
         opt._iter_source = self._iterations
         torch.cuda.synchronize(dev)
         dlog.info("native graph engine: %d nodes, %d params, %.1f MB planned activations", len(self.nodes), n,
@@ -213,7 +215,33 @@ class NativeGraphEngine(Engine):
 
     # --- planning --------------------------------------------------------------------------
     def _plan(self):
-        model, dev, B = self.model, self.device, self.B
+        self._build()
+        self._allocate()
+
+    @classmethod
+    def plan_only(cls, model, batch: int):
+        """The fused plan of ``model`` at per-replica batch ``batch`` without touching a
+        device (planner inspection / CPU tests)."""
+        self = cls.__new__(cls)
+        self.model, self.B = model, batch
+        self._build()
+        return self
+
+    def describe_plan(self) -> dict:
+        live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
+        return {
+            "nodes": len(self.nodes),
+            "kernels_fwd": len(live),
+            "conv_bn_stats": sum(1 for nd in self.nodes if nd.attrs.get("stats")),
+            "bn_relu": sum(1 for nd in self.nodes if nd.kind == "BatchNormalization" and nd.attrs.get("relu")),
+            "add_fused_raw": sum(1 for nd in self.nodes if nd.attrs.get("fused") and nd.attrs["fused"][1][0] == "raw"),
+            "add_fused_bn": sum(1 for nd in self.nodes if nd.attrs.get("fused") and nd.attrs["fused"][1][0] == "bn"),
+            "add_relu": sum(1 for nd in self.nodes if nd.kind == "Add" and nd.attrs.get("relu")),
+            "dead": sum(1 for nd in self.nodes if nd.attrs.get("dead")),
+        }
+
+    def _build(self):
+        model, B = self.model, self.B
         seq, in_key, out_key, in_shape = _layer_graph(model)
         tensors: Dict[int, T] = {}
         h, w, c = in_shape
@@ -236,7 +264,6 @@ class NativeGraphEngine(Engine):
         self.logits_t = tensors[out_key]
         self.nodes = nodes
         self._fuse()
-        self._allocate()
 
     def _out_shape(self, kind, l, xs):
         x = xs[0].shape
@@ -397,6 +424,79 @@ class NativeGraphEngine(Engine):
         nbytes += big * 4
         self.act_bytes = nbytes
 
+    # --- gradient buckets (all-reduce overlapped with the rest of backward) ------------------
+    def _plan_buckets(self, bucket_mb: float):
+        """Contiguous ranges of G, filled from the END of the Keras weight order (backward
+        produces the last layers' gradients first); the metric tail rides in the first
+        bucket.  A bucket is all-reduced on a side stream as soon as the backward ops that
+        write its variables have been enqueued."""
+        writers = {}
+        for nd in self.nodes:
+            if nd.attrs.get("dead"):
+                continue
+            l = nd.layer
+            if nd.kind in ("Conv2D", "Dense"):
+                vs = [l.kernel] + ([l.bias] if l.use_bias else [])
+                writers[id(nd)] = vs
+            elif nd.kind == "BatchNormalization" and not nd.attrs.get("stats_only"):
+                writers[id(nd)] = [w for w in (l.gamma, l.beta) if w is not None]
+            elif nd.kind == "Add" and nd.attrs.get("fused"):
+                main, (mode, other) = nd.attrs["fused"]
+                vs = [w for w in (main.layer.gamma, main.layer.beta) if w is not None]
+                if mode == "bn":
+                    vs += [w for w in (other.layer.gamma, other.layer.beta) if w is not None]
+                writers[id(nd)] = vs
+        self._writes = {k: [id(v) for v in vs] for k, vs in writers.items()}
+        limit = max(1, int(bucket_mb * 2**20 / 4))
+        order = list(range(len(self.vars)))[::-1]
+        buckets, cur, cur_n = [], [], 0
+        for i in order:
+            cur.append(i)
+            cur_n += self.sizes[i]
+            if cur_n >= limit:
+                buckets.append(cur)
+                cur, cur_n = [], 0
+        if cur:
+            buckets.append(cur)
+        self._buckets = []
+        for bi, idxs in enumerate(buckets):
+            lo = min(self.offsets[i] for i in idxs)
+            hi = max(self.offsets[i] + self.sizes[i] for i in idxs)
+            hi = _pad8(hi)
+            if bi == 0:
+                hi = self.G.numel()  # + metric tail
+            self._buckets.append({"lo": lo, "hi": hi, "vars": {id(self.vars[i]) for i in idxs}})
+        # buckets must tile G exactly
+        spans = sorted((b["lo"], b["hi"]) for b in self._buckets)
+        assert spans[0][0] == 0 and all(a[1] == b[0] for a, b in zip(spans, spans[1:])), spans
+        self._comm_stream = None
+
+    def _bucket_begin(self):
+        for b in self._buckets:
+            b["left"] = set(b["vars"])
+            b["sent"] = False
+
+    def _bucket_progress(self, nd, final=False):
+        if self.native_comm is None:
+            return
+        done = set(self._writes.get(id(nd), ())) if nd is not None else set()
+        main = torch.cuda.current_stream(self.device)
+        for b in self._buckets:
+            if b["sent"]:
+                continue
+            b["left"] -= done
+            if b["left"] and not final:
+                continue
+            if self._comm_stream is None:
+                self._comm_stream = torch.cuda.Stream(self.device)
+            cs = self._comm_stream
+            cs.wait_stream(main)
+            self.native_comm.allreduce(self.G.data_ptr() + 4 * b["lo"], self.G.data_ptr() + 4 * b["lo"],
+                                       b["hi"] - b["lo"], 0, 0, cs.cuda_stream)
+            b["sent"] = True
+        if final:
+            main.wait_stream(self._comm_stream)
+
     def _all_tensors(self):
         out = [self.x0]
         for nd in self.nodes:
@@ -514,10 +614,11 @@ class NativeGraphEngine(Engine):
         H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:])
         for t in self._all_tensors():
             t.root().written = False
+        self._bucket_begin()
         for nd in reversed(live):
             getattr(self, "_bwd_" + nd.kind)(nd)
-        if self.native_comm is not None:
-            self.native_comm.allreduce(self.G.data_ptr(), self.G.data_ptr(), self.G.numel(), 0, 0, s)
+            self._bucket_progress(nd)
+        self._bucket_progress(None, final=True)
         if not self.host_collective:
             self._optimizer_step()
 

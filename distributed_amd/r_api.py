@@ -181,6 +181,20 @@ def write_bytes(data: bytes, path: str) -> str:
     return path
 
 
+def save_from_result(results, path: str = "model.hdf5") -> str:
+    """Driver side of README.md:240-247: take the per-partition results of a barrier
+    apply (a list of strings / rows, or one string), find the chief's non-empty base64
+    payload and write it to ``path``."""
+    if isinstance(results, str):
+        results = [results]
+    for r in results:
+        if isinstance(r, dict):
+            r = next(iter(r.values()), "")
+        if r:
+            return write_bytes(base64decode(r), path)
+    raise ValueError("no partition returned a model payload")
+
+
 # ---- TF_CONFIG helpers (README.md:84-113, 180-183) ---------------------------------------------
 def tf_config(workers, index) -> str:
     """``jsonlite::toJSON(list(cluster = list(worker = ...), task = list(type = 'worker', index = i)),

@@ -33,6 +33,8 @@ def get_str(name: str, default: str) -> str:
 # Documented knobs (README "Configuration"):
 #   DAMD_DEVICE            cpu | cuda          force the compute device
 #   DAMD_FUSED             0/1                 allow the fused native ConvNet engine (default 1)
+#   DAMD_BUCKET_MB         float               gradient all-reduce bucket size, native graph engine (8)
+#   DAMD_FORCE_ALLREDUCE   0/1                 keep the RCCL all-reduce in the step at world 1 (testing)
 #   DAMD_NATIVE_GRAPH      0/1                 allow the native graph engine (HIP plan + graph, default 1)
 #   DAMD_GRAPH             0/1                 capture steps into hipGraphs (default 1)
 #   DAMD_GRAPH_STEPS       int                 steps per captured graph (default 20)
@@ -40,9 +42,7 @@ def get_str(name: str, default: str) -> str:
 #   DAMD_DEBUG_SYNC        0/1                 synchronize + error-check after every engine chunk
 #   DAMD_COMM              rccl | torch | gloo | auto   data-plane communicator on GPU (default auto=rccl;
 #                          gloo stages device tensors through host memory: test/debug only)
-#   DAMD_BUCKET_MB         float               gradient bucket size for the generic engine
 #   DAMD_WATCHDOG_S        float               collective watchdog deadline (0 = off)
-#   DAMD_FAIL_AT           "rank:step"         fault injection (raise inside fit)
+#   DAMD_FAIL_AT           "rank:step[:attempt]"  fault injection (raise inside fit; only in that launcher attempt)
 #   DAMD_CHECK_MIRRORS     int                 mirror-divergence check every N epochs (0=off)
-#   DAMD_DEBUG             0/1                 synchronous launches + extra checks
 #   DAMD_LOCAL_RANK        int                 local GPU index (set by the launcher)

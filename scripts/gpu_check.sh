@@ -16,13 +16,18 @@ step() {  # step <name> <limit_s> <cmd...>   (stdout/err -> gpurun_out/<name>.lo
 }
 python -c "import torch;print(torch.cuda.get_device_name(0))"
 if [ "$STAGE" = all ] || [ "$STAGE" = test ]; then
-  step pytest_gpu 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider
+  step pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider
   step smoke 300 python __graft_entry__.py smoke
 fi
 if [ "$STAGE" = all ] || [ "$STAGE" = bench ]; then
   step stamps 300 python scripts/stamps.py 64
   step bench_n1 300 python bench.py --gpus 1 --steps 3000 --warmup 300
   step bench_n1_generic 300 python bench.py --gpus 1 --steps 200 --warmup 20 --engine generic
+fi
+if [ "$STAGE" = all ] || [ "$STAGE" = resnet ]; then
+  step bench_gemm 300 python scripts/bench_gemm.py 64
+  step bench_resnet 400 python bench.py --model resnet18 --steps 30 --warmup 5
+  step rocprof_resnet 500 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_resnet -o resnet -- python bench.py --model resnet18 --steps 10 --warmup 3
 fi
 if [ "$STAGE" = all ] || [ "$STAGE" = prof ]; then
   step rocprof 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python bench.py --gpus 1 --steps 500 --warmup 50

@@ -93,6 +93,10 @@ def test_base64_transport(tmp_path):
     out = k.write_bytes(k.base64decode(payload), str(tmp_path / "model.hdf5"))
     m2 = k.load_model_hdf5(out)
     assert all(np.array_equal(a, b) for a, b in zip(m.get_weights(), m2.get_weights()))
+    # collected barrier rows: chief carries the payload, the others return ""
+    rows = [{"address": payload}, {"address": ""}, {"address": ""}]
+    out2 = k.save_from_result(rows, str(tmp_path / "model2.hdf5"))
+    assert open(out2, "rb").read() == open(p, "rb").read()
 
 
 def test_model_checkpoint_and_backup_restore(tmp_path):

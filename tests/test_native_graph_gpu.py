@@ -30,8 +30,11 @@ def _mnist():
     ])
 
 
-def _train(build, x, y, init, batch, steps, native, lr=0.1, momentum=0.0, graph=True, device=None):
-    env = {"DAMD_NATIVE_GRAPH": "1" if native else "0", "DAMD_FUSED": "0", "DAMD_GRAPH": "1" if graph else "0"}
+def _train(build, x, y, init, batch, steps, native, lr=0.1, momentum=0.0, graph=True, device=None, extra_env=None,
+           fused=False):
+    env = {"DAMD_NATIVE_GRAPH": "1" if native else "0", "DAMD_FUSED": "1" if fused else "0",
+           "DAMD_GRAPH": "1" if graph else "0"}
+    env.update(extra_env or {})
     if device:
         env["DAMD_DEVICE"] = device
     old = {k: os.environ.get(k) for k in env}
@@ -274,3 +277,28 @@ def test_resnet18_full_size_trains():
     assert m._engine.name == "native_graph"
     assert all(np.isfinite(h.history["loss"]))
     assert h.history["loss"][-1] < h.history["loss"][0]
+
+
+@pytest.mark.parametrize("which", ["native_graph", "fused_convnet"])
+def test_rccl_allreduce_captured_in_step_graph(which):
+    """The multi-GPU step shape on one GPU: DAMD_FORCE_ALLREDUCE keeps the (size-1) RCCL
+    all-reduce inside the captured step — for the native engine as many small buckets on
+    a side stream (fork/join inside the graph).  Must equal the run without it."""
+    if which == "native_graph":
+        build, shape, batch, steps = _small_resnet, (32, 32, 3), 32, 2
+        x, y = _data(64, shape, 10, seed=5)
+    else:
+        build, shape, batch, steps = _mnist, (28, 28, 1), 64, 45  # 2 captured graphs of 20 + eager tail
+        x, y = _data(64 * 45, shape, 10, seed=5)
+    tf.keras.backend.clear_session()
+    init = build().get_weights()
+    kw = dict(native=which == "native_graph", fused=which == "fused_convnet",
+              lr=0.05 if which == "native_graph" else 0.005, momentum=0.9)
+    wa, ha, ea = _train(build, x, y, init, batch, steps,
+                        extra_env={"DAMD_FORCE_ALLREDUCE": "1", "DAMD_BUCKET_MB": "0.02"}, **kw)
+    wb, hb, eb = _train(build, x, y, init, batch, steps, **kw)
+    assert ea == eb == which
+    tol = dict(rtol=1e-4, atol=1e-5) if which == "native_graph" else dict(rtol=1e-3, atol=1e-4)
+    for a, b in zip(wa, wb):
+        np.testing.assert_allclose(a, b, **tol)
+    np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-4)

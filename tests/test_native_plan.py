@@ -1,0 +1,39 @@
+"""Native graph engine planner on CPU: graph lowering, fusion decisions and gradient
+buckets for ResNet-18 (BASELINE.json config 4) and the reference CNN — no device needed."""
+from distributed_amd import keras
+from distributed_amd.engine.native_graph import NativeGraphEngine
+from distributed_amd.models import mnist_cnn, resnet18
+
+
+def test_resnet18_plan_fusions():
+    keras.backend.clear_session()
+    p = NativeGraphEngine.plan_only(resnet18(), 64).describe_plan()
+    # 20 convs, each followed by a BN whose batch statistics come from the conv epilogue
+    assert p["conv_bn_stats"] == 20
+    # conv1 + the first BN of each of the 8 blocks apply ReLU in the BN pass
+    assert p["bn_relu"] == 9
+    # 8 residual adds fused into the second BN's apply: 5 identity, 3 projection (BN+BN)
+    assert p["add_fused_raw"] == 5 and p["add_fused_bn"] == 3
+    assert p["add_relu"] == 8
+    # 17 ReLU layers folded away
+    assert p["dead"] == 17
+
+
+def test_resnet18_shapes_and_eligibility_reasons():
+    keras.backend.clear_session()
+    pl = NativeGraphEngine.plan_only(resnet18(), 8)
+    out = {nd.layer.name: nd.out.shape for nd in pl.nodes}
+    assert out["conv1_conv"] == (8, 112, 112, 64)
+    assert out["pool1_pool"] == (8, 56, 56, 64)
+    assert out["conv3_block1_conv1"] == (8, 28, 28, 128)
+    assert out["conv5_block2_out"] == (8, 7, 7, 512)
+    assert out["avg_pool"] == (8, 512)
+    assert out["predictions"] == (8, 1000)
+    assert pl.cin_pad == 8  # RGB padded to 8 channels for 16-byte im2col chunks
+
+
+def test_mnist_plan():
+    keras.backend.clear_session()
+    pl = NativeGraphEngine.plan_only(mnist_cnn(), 64)
+    kinds = [nd.kind for nd in pl.nodes if not nd.attrs.get("dead")]
+    assert kinds == ["Conv2D", "MaxPooling2D", "Dense", "Dense"]  # Flatten is a view
