@@ -52,6 +52,37 @@ class GenericEngine(Engine):
                 comm.broadcast_(w.value.data if w.value.requires_grad else w.value, 0)
         self.feed = None
         self.step_in_epoch = 0
+        self._plan_buckets()
+
+    def _plan_buckets(self):
+        """Gradient buckets (SURVEY.md §3.3 / N3'): contiguous ranges of G filled from the
+        last layer backwards, the metric tail in the first one.  During backward each
+        parameter's gradient is copied into G by a hook; when a bucket is complete its
+        all-reduce starts asynchronously while autograd computes the earlier layers."""
+        from ..utils import env
+
+        self.bucketed = self.world > 1 and env.get_float("DAMD_BUCKET_MB", 8.0) > 0
+        limit = max(1, int(env.get_float("DAMD_BUCKET_MB", 8.0) * 2**20 / 4))
+        offs, off = [], 0
+        for sz in self.sizes:
+            offs.append(off)
+            off += sz
+        self.offs = offs
+        buckets, cur, n = [], [], 0
+        for i in reversed(range(len(self.sizes))):
+            cur.append(i)
+            n += self.sizes[i]
+            if n >= limit:
+                buckets.append(cur)
+                cur, n = [], 0
+        if cur:
+            buckets.append(cur)
+        self.buckets = []
+        for bi, idxs in enumerate(buckets):
+            lo = min(offs[i] for i in idxs)
+            hi = self.n + self.ntail if bi == 0 else max(offs[i] + self.sizes[i] for i in idxs)
+            self.buckets.append((lo, hi, set(idxs)))
+        self.bucket_of = {i: b for b, (_, _, idxs) in enumerate(self.buckets) for i in idxs}
 
     def bind(self, x, y):
         key = (id(x), id(y), len(x))
@@ -73,27 +104,66 @@ class GenericEngine(Engine):
         gcount = max(0, min(self.global_batch, feed.n - gstart))
         G = self.G
         G.zero_()
+        works = None
         if idx.numel() > 0 and gcount > 0:
             xb, yb = feed.x[idx], feed.y[idx]
             out = model(xb, training=True)
             ls = self.loss.per_sample(yb, out)
             loss = ls.sum() * (1.0 / gcount)
-            grads = torch.autograd.grad(loss, self.leaves, allow_unused=True)
-            off = 0
-            for g, sz in zip(grads, self.sizes):
-                if g is not None:
-                    G[off:off + sz].copy_(g.reshape(-1))
-                off += sz
             with torch.no_grad():
                 G[self.n] = ls.detach().sum()
                 G[self.n + 1] = float(idx.numel())
                 for i, m in enumerate(self.metric_objs):
                     G[self.n + 2 + i] = m.per_sample(yb, out.detach()).sum()
-        if self.world > 1:
+            if self.bucketed:
+                works = self._backward_bucketed(loss)
+            else:
+                grads = torch.autograd.grad(loss, self.leaves, allow_unused=True)
+                for g, sz, off in zip(grads, self.sizes, self.offs):
+                    if g is not None:
+                        G[off:off + sz].copy_(g.reshape(-1))
+        if works is not None:
+            for w in works:
+                w.wait()
+        elif self.world > 1:
             self.strategy.communicator.allreduce_(G, "sum")
         self.model.optimizer.apply_flat(self.P, G[: self.n])
         self.acc += G[self.n:].double()
         self.step_in_epoch += 1
+
+    def _backward_bucketed(self, loss):
+        comm, G = self.strategy.communicator, self.G
+        left = [set(idxs) for (_, _, idxs) in self.buckets]
+        works = [None] * len(self.buckets)
+
+        def launch(b):
+            lo, hi, _ = self.buckets[b]
+            works[b] = comm.allreduce_async(G[lo:hi], "sum")
+
+        def make_hook(i):
+            def hook(g):
+                off, sz = self.offs[i], self.sizes[i]
+                with torch.no_grad():
+                    G[off:off + sz].copy_(g.reshape(-1))
+                b = self.bucket_of[i]
+                left[b].discard(i)
+                if not left[b]:
+                    launch(b)
+                return g
+            return hook
+
+        handles = [leaf.register_hook(make_hook(i)) for i, leaf in enumerate(self.leaves)]
+        try:
+            torch.autograd.backward(loss, inputs=self.leaves)
+        finally:
+            for h in handles:
+                h.remove()
+        for b in range(len(self.buckets)):  # parameters that received no gradient
+            if works[b] is None:
+                launch(b)
+        for leaf in self.leaves:
+            leaf.grad = None
+        return works
 
     def run(self, n_steps):
         for _ in range(n_steps):

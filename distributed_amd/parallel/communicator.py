@@ -50,6 +50,11 @@ class Communicator:
     def broadcast_object(self, obj: Any, root: int = 0) -> Any:
         raise NotImplementedError
 
+    def allreduce_async(self, t: torch.Tensor, op: str = "sum"):
+        """Start an in-place all-reduce; returns a handle with ``wait()``."""
+        self.allreduce_(t, op)
+        return _Done()
+
     @property
     def native(self):
         """Native RCCL handle usable inside captured graphs (None if not RCCL)."""
@@ -57,6 +62,11 @@ class Communicator:
 
     def shutdown(self) -> None:
         pass
+
+
+class _Done:
+    def wait(self):
+        return True
 
 
 class LoopbackCommunicator(Communicator):
@@ -106,6 +116,11 @@ class TorchCommunicator(Communicator):
             return t
         dist.all_reduce(t, op=_TORCH_OPS[op], group=self._group_for(t))
         return t
+
+    def allreduce_async(self, t, op="sum"):
+        if self._staged(t) or op == "avg" or t.is_cuda:
+            return super().allreduce_async(t, op)
+        return dist.all_reduce(t, op=_TORCH_OPS[op], group=self._group_for(t), async_op=True)
 
     def broadcast_(self, t, root=0):
         if self._staged(t):

@@ -32,8 +32,9 @@ def _load(out, r):
 def test_two_workers_mirror_and_match_single_worker(tmp_path):
     d2 = tmp_path / "w2"
     d2.mkdir()
+    # small buckets: 3 asynchronous all-reduces per step overlapped with backward
     res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=16, DAMD_CHECK_MIRRORS=1,
-                                                           DAMD_TEST_DIVERGE=1), timeout=240)
+                                                           DAMD_TEST_DIVERGE=1, DAMD_BUCKET_MB=0.05), timeout=240)
     assert res.ok, res.returncodes
     (w0, j0), (w1, j1) = _load(d2, 0), _load(d2, 1)
     assert j0["world"] == j1["world"] == 2
