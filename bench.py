@@ -142,7 +142,9 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None if resnet else round(value / BASELINE_IMG_S, 2),
-            "dtype": "bf16" if on_gpu else "fp32",
+            # bf16 MFMA compute (fp32 master weights / accumulation) on the native engines;
+            # the PyTorch generic engine computes in fp32
+            "dtype": "bf16" if engine.name in ("fused_convnet", "native_graph") else "fp32",
             "data": (f"synthetic ({len(x)} rows 224x224x3 k/255, 1000 classes, random-init weights)" if resnet else
                      "synthetic (28x28x1 MNIST-shaped, 60000 rows, random-init weights)"),
             "config": {
