@@ -208,6 +208,8 @@ class NativeGraphEngine(Engine):
         self.feed = None
         self._plan()
         self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0))
+        # created up front: no stream creation while a graph is being captured
+        self._comm_stream = torch.cuda.Stream(dev) if self.native_comm is not None else None
         opt._iter_source = self._iterations
         torch.cuda.synchronize(dev)
         dlog.info("native graph engine: %d nodes, %d params, %.1f MB planned activations", len(self.nodes), n,
@@ -469,7 +471,6 @@ class NativeGraphEngine(Engine):
         # buckets must tile G exactly
         spans = sorted((b["lo"], b["hi"]) for b in self._buckets)
         assert spans[0][0] == 0 and all(a[1] == b[0] for a, b in zip(spans, spans[1:])), spans
-        self._comm_stream = None
 
     def _bucket_begin(self):
         for b in self._buckets:
@@ -487,8 +488,6 @@ class NativeGraphEngine(Engine):
             b["left"] -= done
             if b["left"] and not final:
                 continue
-            if self._comm_stream is None:
-                self._comm_stream = torch.cuda.Stream(self.device)
             cs = self._comm_stream
             cs.wait_stream(main)
             self.native_comm.allreduce(self.G.data_ptr() + 4 * b["lo"], self.G.data_ptr() + 4 * b["lo"],

@@ -37,3 +37,30 @@ def test_mnist_plan():
     pl = NativeGraphEngine.plan_only(mnist_cnn(), 64)
     kinds = [nd.kind for nd in pl.nodes if not nd.attrs.get("dead")]
     assert kinds == ["Conv2D", "MaxPooling2D", "Dense", "Dense"]  # Flatten is a view
+
+
+def test_gradient_buckets_tile_the_flat_buffer():
+    import numpy as np
+    import torch
+
+    keras.backend.clear_session()
+    m = resnet18()
+    pl = NativeGraphEngine.plan_only(m, 8)
+    pl.vars = m.trainable_weights
+    pl.sizes = [int(np.prod(v.shape)) for v in pl.vars]
+    pl.offsets, off = [], 0
+    for sz in pl.sizes:
+        pl.offsets.append(off)
+        off = -(-(off + sz) // 8) * 8
+    pl.G = torch.zeros(off + 8)
+    pl._plan_buckets(4.0)  # 4 MB buckets over 46.8 MB of grads
+    bs = pl._buckets
+    assert 5 <= len(bs) <= 16  # the 3x3x512x512 convs (9.4 MB) are buckets of their own
+    assert bs[0]["hi"] == off + 8  # the first bucket (last layers) carries the metric tail
+    covered = sorted((b["lo"], b["hi"]) for b in bs)
+    assert covered[0][0] == 0 and all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+    ids = [i for b in bs for i in b["vars"]]
+    assert sorted(ids) == sorted(id(v) for v in pl.vars)
+    # every trainable variable has exactly one writer node in the backward plan
+    written = [i for vs in pl._writes.values() for i in vs]
+    assert sorted(written) == sorted(id(v) for v in pl.vars)
