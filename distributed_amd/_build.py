@@ -97,23 +97,45 @@ def _build_C(verbose=False, jobs=None) -> Path:
     return out
 
 
+H5_SOURCES = [CSRC / "io" / "keras_h5.cpp", CSRC / "io" / "h5tree.cpp"]
+
+
+def hdf5_flags():
+    return ["-I", str(CSRC / "io"), "-I", str(HDF5_PREFIX / "include"), "-L", str(HDF5_PREFIX / "lib"), "-lhdf5",
+            f"-Wl,-rpath,{HDF5_PREFIX / 'lib'}"]
+
+
 def _build_h5(verbose=False) -> Path | None:
     out = PKG / f"_h5{EXT}"
-    src = CSRC / "io" / "keras_h5.cpp"
-    if not src.exists():
+    if not H5_SOURCES[0].exists():
         return None
     if not (HDF5_PREFIX / "include" / "hdf5.h").exists():
         raise RuntimeError(f"libhdf5 headers not found under {HDF5_PREFIX}")
-    if _deps_newer(out, [src]):
+    if _deps_newer(out, H5_SOURCES + [CSRC / "io" / "h5tree.h"]):
         inc = []
         for p in _pybind_includes():
             inc += ["-I", p]
-        cmd = [
-            "g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden", str(src), "-o", str(out),
-            "-I", str(HDF5_PREFIX / "include"), *inc,
-            "-L", str(HDF5_PREFIX / "lib"), "-lhdf5", f"-Wl,-rpath,{HDF5_PREFIX / 'lib'}",
-        ]
+        cmd = ["g++", "-O2", "-fPIC", "-shared", "-std=c++17", "-fvisibility=hidden", *map(str, H5_SOURCES), "-o",
+               str(out), *inc, *hdf5_flags()]
         _run(cmd, verbose)
+    return out
+
+
+def build_h5_selftest(out: Path, sanitize: bool = True, verbose: bool = False) -> Path:
+    """Standalone host executable of the HDF5 tree I/O self-test (ASan + UBSan)."""
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=all"] if sanitize else []
+    # link libhdf5 through a private directory holding only that library: putting the conda
+    # lib dir on the search path would also pull in its older libstdc++
+    libdir = Path(out).parent / "h5lib"
+    libdir.mkdir(parents=True, exist_ok=True)
+    so = sorted((HDF5_PREFIX / "lib").glob("libhdf5.so.[0-9]*"), key=lambda p: len(p.name))[0]
+    link = libdir / so.name
+    if not link.exists():
+        link.symlink_to(so.resolve())
+    cmd = ["g++", "-O1", "-g", "-std=c++17", *san, str(CSRC / "tests" / "h5_selftest.cpp"),
+           str(CSRC / "io" / "h5tree.cpp"), "-o", str(out), "-I", str(CSRC / "io"), "-I", str(HDF5_PREFIX / "include"),
+           str(link), f"-Wl,-rpath,{libdir}"]
+    _run(cmd, verbose)
     return out
 
 
