@@ -265,3 +265,44 @@ class MirrorCheck(Callback):
             from ..utils.debug import check_mirrored
 
             self.fingerprints.append(check_mirrored(self.model, tag=f"epoch {epoch + 1}"))
+
+
+class JSONMetricsLogger(Callback):
+    """One JSON line per epoch (SURVEY.md §5 observability): epoch, the global metrics,
+    images/sec and ms/step from the host wall clock of the epoch.  Written by the chief
+    only (metrics are already global) to ``path`` (appended) or stdout."""
+
+    def __init__(self, path=None, all_workers=False):
+        super().__init__()
+        self.path, self.all_workers = path, all_workers
+        self._t0 = None
+
+    def on_epoch_begin(self, epoch, logs=None):
+        import time
+
+        if self.model is not None and getattr(self.model, "_engine", None) is not None:
+            self.model._engine.sync()
+        self._t0 = time.perf_counter()
+
+    def on_epoch_end(self, epoch, logs=None):
+        import sys
+        import time
+
+        if not (self.all_workers or _is_chief(self.model)):
+            return
+        if getattr(self.model, "_engine", None) is not None:
+            self.model._engine.sync()
+        dt = time.perf_counter() - (self._t0 or time.perf_counter())
+        steps = int(self.params.get("steps") or 0)
+        bs = int(self.params.get("batch_size") or 0)
+        rec = {"epoch": epoch + 1, **{k: float(v) for k, v in (logs or {}).items() if k != "seen"},
+               "seconds": dt, "ms_per_step": 1e3 * dt / steps if steps else None,
+               "images_per_sec": steps * bs / dt if dt > 0 else None,
+               "engine": getattr(getattr(self.model, "_engine", None), "name", None)}
+        line = json.dumps(rec)
+        if self.path:
+            with open(self.path, "a") as f:
+                f.write(line + "\n")
+        else:
+            sys.stdout.write(line + "\n")
+            sys.stdout.flush()

@@ -53,7 +53,8 @@ def test_two_ranks_one_gpu_match_single_rank(tmp_path, engine):
                                                            DAMD_TEST_INIT_FROM=d2 / "init0.npz"), timeout=420)
     assert res.ok, res.returncodes
     ws, js = _load(d1, 0)
-    tol = dict(rtol=1e-3, atol=1e-5) if engine == "generic" else dict(rtol=2e-3, atol=2e-4)
+    tol = {"generic": dict(rtol=1e-3, atol=1e-5), "fused": dict(rtol=2e-3, atol=2e-4),
+           "native_graph": dict(rtol=5e-3, atol=5e-4)}[engine]
     for a, b in zip(w0, ws):
         np.testing.assert_allclose(a, b, **tol)
     np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-3)

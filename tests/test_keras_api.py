@@ -184,8 +184,17 @@ def test_functional_api_and_callbacks():
             lrs.append(self.model.optimizer.learning_rate)
 
     sched = tf.keras.callbacks.LearningRateScheduler(lambda e: 0.01 / (1 + e))
-    h = m.fit(x, y, batch_size=32, epochs=3, verbose=0, callbacks=[sched, Rec()], validation_split=0.25)
+    import json
+    import tempfile
+
+    jpath = tempfile.mktemp(suffix=".jsonl")
+    h = m.fit(x, y, batch_size=32, epochs=3, verbose=0, validation_split=0.25,
+              callbacks=[sched, Rec(), tf.keras.callbacks.JSONMetricsLogger(jpath)])
     assert lrs == pytest.approx([0.01, 0.005, 0.01 / 3])
+    recs = [json.loads(l) for l in open(jpath)]
+    assert [r["epoch"] for r in recs] == [1, 2, 3]
+    assert recs[-1]["loss"] == pytest.approx(h.history["loss"][-1])
+    assert recs[0]["images_per_sec"] > 0 and recs[0]["engine"] == "generic"
     assert "val_loss" in h.history and "val_accuracy" in h.history
     assert h.history["loss"][-1] < h.history["loss"][0]
 
