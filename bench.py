@@ -100,6 +100,8 @@ def main():
             engine.run(k)
 
     run(args.warmup)
+    # build the replayed HIP graph(s) now: capture is setup, not part of a timed step
+    engine.prepare(args.steps)
     engine.sync()
     comm = strategy.communicator
     on_gpu = rt.device.type == "cuda"

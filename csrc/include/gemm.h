@@ -6,7 +6,9 @@ namespace damd {
 
 enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4 };
 enum GemmBMode { B_NC = 0, B_KC = 1 };
-enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32 };
+// E_SLAB: split-K partial of split z stored (plain fp32 stores) to C + z * M * ldc; a
+// deterministic splitk_reduce then adds the slabs into the destination in fixed order.
+enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32, E_SLAB = 64 };
 
 struct GemmArgs {
   const void* A;       // bf16
@@ -28,5 +30,7 @@ struct GemmArgs {
 // tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)
 hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int splits, int tile, hipStream_t s);
 int gemm_stats_tile_rows(int tile);
+// dst[i] += sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order)
+hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s);
 
 }  // namespace damd

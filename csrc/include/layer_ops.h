@@ -54,10 +54,12 @@ hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hi
 // Loss --------------------------------------------------------------------------------------
 // Sparse softmax cross-entropy from fp32 logits [B][ld]: dlogits (bf16, [B][K]) =
 // (softmax - onehot) * scale; tail[0] += sum loss, tail[1] += sum correct (argmax ==
-// label, first max wins), tail[2] += B.  labels int32.
+// label, first max wins), tail[2] += B.  labels int32; a label < 0 masks the row (zero
+// gradient, no loss/metric).  ctrl != nullptr: scale = 1 / real rows of the global batch
+// (short final batch; see softmax_xent_k), else the given scale.
 // dlogits shares the row pitch ld of the logits; its padding columns are left untouched.
 hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale,
-                        uint16_t* dlogits, float* tail, hipStream_t s);
+                        const Ctrl* ctrl, uint16_t* dlogits, float* tail, hipStream_t s);
 
 // Optimizer ---------------------------------------------------------------------------------
 // flat multi-tensor Keras SGD over the master buffer: P, V fp32 updated from G; Pb = bf16(P)

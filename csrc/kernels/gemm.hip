@@ -525,7 +525,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs a) {
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
       }
       if (!ok) continue;
-      if constexpr (EPI & E_ATOMIC) {
+      if constexpr (EPI & E_SLAB) {
+        float* c = (float*)a.C + ((size_t)blockIdx.z * a.M + m) * a.ldc + n;
+        *reinterpret_cast<float4*>(c) = float4{v[0], v[1], v[2], v[3]};
+      } else if constexpr (EPI & E_ATOMIC) {
         float* c = (float*)a.C + (size_t)m * a.ldc + n;
 #pragma unroll
         for (int e = 0; e < 4; ++e) atomicAdd(c + e, v[e]);
@@ -598,6 +601,7 @@ hipError_t launch_epi(const GemmArgs& a, int epi, int splits, hipStream_t s) {
     case E_BIAS | E_BF16: return launch_t<BM, BN, AM, BMo, E_BIAS | E_BF16>(a, splits, s);
     case E_BIAS | E_RELU | E_BF16: return launch_t<BM, BN, AM, BMo, E_BIAS | E_RELU | E_BF16>(a, splits, s);
     case E_ATOMIC: return launch_t<BM, BN, AM, BMo, E_ATOMIC>(a, splits, s);
+    case E_SLAB: return launch_t<BM, BN, AM, BMo, E_SLAB>(a, splits, s);
     case E_BF16 | E_STATS: return launch_t<BM, BN, AM, BMo, E_BF16 | E_STATS>(a, splits, s);
     case E_BF16 | E_ADD: return launch_t<BM, BN, AM, BMo, E_BF16 | E_ADD>(a, splits, s);
     default: return hipErrorInvalidValue;
@@ -610,13 +614,36 @@ hipError_t launch_tile(const GemmArgs& a, int epi, int splits, int tile, hipStre
   return launch_epi<128, 128, AM, BMo>(a, epi, splits, s);
 }
 
+__global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__ slab, int splits, long n4,
+                                                     float4* __restrict__ dst) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
+    float4 acc = dst[i];
+    for (int sp = 0; sp < splits; ++sp) {
+      const float4 v = slab[(size_t)sp * n4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    dst[i] = acc;
+  }
+}
+
 }  // namespace
+
+hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s) {
+  if (n % 4 || splits < 1) return hipErrorInvalidValue;
+  const long n4 = n / 4;
+  long g = (n4 + NT - 1) / NT;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(splitk_reduce_k, dim3((int)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab), splits,
+                     n4, reinterpret_cast<float4*>(dst));
+  return hipGetLastError();
+}
 
 int gemm_stats_tile_rows(int tile) { return tile == 1 ? 256 : 128; }
 
 hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int splits, int tile, hipStream_t s) {
   if (splits < 1) return hipErrorInvalidValue;
   if ((epi & E_ATOMIC) && (epi & ~E_ATOMIC)) return hipErrorInvalidValue;
+  if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
   const int key = amode * 2 + bmode;
   switch (key) {
     case A_KC * 2 + B_NC: return launch_tile<A_KC, B_NC>(a, epi, splits, tile, s);

@@ -42,33 +42,55 @@ inline int grid_for(long work, int per_block = NT, int cap = 8192) {
 }
 
 // ---- BatchNorm -------------------------------------------------------------------------
-// reduce partials [T][2][C] over T in double: grid ceil(C/64), 256 threads (4 T-phases)
-__device__ __forceinline__ void reduce_partials(const float* part, int T, int C, double& s0, double& s1) {
-  __shared__ double red[2][4][64];
-  const int t = threadIdx.x, cl = t & 63, ph = t >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int i = ph; i < T; i += 4) {
-      a += part[(size_t)i * 2 * C + c];
-      b += part[(size_t)i * 2 * C + C + c];
-    }
-  red[0][ph][cl] = a;
-  red[1][ph][cl] = b;
+// Sum the partials [T][2][C] over T in fp64 for the 8 channels c0..c0+7 of this block:
+// every thread strides over T with 32-byte loads, then a wave butterfly and a 4-wave LDS
+// combine (fixed order: deterministic).  On return sums[j] (j < 8) is the channel sum and
+// sums[8 + j] the sum of squares (or of the second statistic).  Grid = C / 8 blocks, so
+// even C = 64 keeps 8 x 256 threads on a reduction over ~1.5k partials.
+__device__ __forceinline__ void reduce_partials8(const float* __restrict__ part, int T, int C, int c0,
+                                                 double* sums) {
+  __shared__ double red[NT / 64][16];
+  double a[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = 0.0;
+  for (int i = threadIdx.x; i < T; i += NT) {
+    const float* p = part + (size_t)i * 2 * C + c0;
+    const float4 s0 = *reinterpret_cast<const float4*>(p), s1 = *reinterpret_cast<const float4*>(p + 4);
+    const float4 q0 = *reinterpret_cast<const float4*>(p + C), q1 = *reinterpret_cast<const float4*>(p + C + 4);
+    a[0] += s0.x; a[1] += s0.y; a[2] += s0.z; a[3] += s0.w;
+    a[4] += s1.x; a[5] += s1.y; a[6] += s1.z; a[7] += s1.w;
+    a[8] += q0.x; a[9] += q0.y; a[10] += q0.z; a[11] += q0.w;
+    a[12] += q1.x; a[13] += q1.y; a[14] += q1.z; a[15] += q1.w;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j)
+#pragma unroll
+    for (int sft = 32; sft > 0; sft >>= 1) a[j] += __shfl_xor(a[j], sft);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red[wave][j] = a[j];
+  }
   __syncthreads();
-  s0 = red[0][0][cl] + red[0][1][cl] + red[0][2][cl] + red[0][3][cl];
-  s1 = red[1][0][cl] + red[1][1][cl] + red[1][2][cl] + red[1][3][cl];
+  if (threadIdx.x < 16) {
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < NT / 64; ++w) v += red[w][threadIdx.x];
+    sums[threadIdx.x] = v;
+  }
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(NT) void bn_finalize_k(const float* part, int T, int C, float count,
                                                     const float* gamma, const float* beta, float eps, float mom,
                                                     float* rmean, float* rvar, float* st) {
-  double s0, s1;
-  reduce_partials(part, T, C, s0, s1);
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  if (threadIdx.x >= 64 || c >= C) return;
-  const double mean = s0 / count;
-  double var = s1 / count - mean * mean;
+  __shared__ double sums[16];
+  const int c0 = blockIdx.x * 8;
+  reduce_partials8(part, T, C, c0, sums);
+  if (threadIdx.x >= 8) return;
+  const int c = c0 + threadIdx.x;
+  const double mean = sums[threadIdx.x] / count;
+  double var = sums[8 + threadIdx.x] / count - mean * mean;
   if (var < 0.0) var = 0.0;
   const float m = (float)mean, v = (float)var;
   const float inv = rsqrtf(v + eps);
@@ -173,11 +195,12 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
 
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_k(const float* part, int T, int C, float count,
                                                         const float* st, float* dgamma, float* dbeta, float* co) {
-  double s0, s1;
-  reduce_partials(part, T, C, s0, s1);
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  if (threadIdx.x >= 64 || c >= C) return;
-  const float db = (float)s0, dg = (float)s1;
+  __shared__ double sums[16];
+  const int c0 = blockIdx.x * 8;
+  reduce_partials8(part, T, C, c0, sums);
+  if (threadIdx.x >= 8) return;
+  const int c = c0 + threadIdx.x;
+  const float db = (float)sums[threadIdx.x], dg = (float)sums[8 + threadIdx.x];
   if (dbeta) dbeta[c] += db;
   if (dgamma) dgamma[c] += dg;
   const float a = st[2 * C + c];
@@ -384,12 +407,27 @@ __global__ __launch_bounds__(NT) void colsum_k(const void* x, int x_f32, int M, 
 }
 
 // ---- loss ------------------------------------------------------------------------------------
+// Rows with label < 0 (past the end of the dataset in a short final batch) get a zero
+// gradient and no loss / metric contribution.  With ctrl != nullptr the gradient scale is
+// 1 / (rows of this global batch that exist): Keras' SUM_OVER_BATCH_SIZE on the real
+// final batch; benchmark wrap mode (ctrl->wrap > 0) always has full batches.
 __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ logits, int ld,
                                                      const int32_t* __restrict__ labels, int K, float scale,
-                                                     uint16_t* __restrict__ dl, float* tail) {
+                                                     const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ dl,
+                                                     float* tail) {
   __shared__ float sv[NT];
   __shared__ int si[NT];
   const int b = blockIdx.x, t = threadIdx.x;
+  const int y = labels[b];
+  if (y < 0) {
+    for (int k = t; k < K; k += NT) dl[(size_t)b * ld + k] = 0;
+    return;
+  }
+  if (ctrl) {
+    const int gb = ctrl->global_batch;
+    const int left = ctrl->nsamples - ctrl->cursor * gb;
+    scale = 1.f / (float)(ctrl->wrap > 0 ? gb : max(1, min(gb, left)));
+  }
   const float* z = logits + (size_t)b * ld;
   float mx = -INFINITY;
   int mi = 0x7fffffff;
@@ -420,7 +458,6 @@ __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ l
     __syncthreads();
   }
   const float sum = sv[0];
-  const int y = labels[b];
   const float inv = 1.f / sum;
   for (int k = t; k < K; k += NT) {
     const float p = __expf(z[k] - zmax) * inv;
@@ -477,18 +514,21 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
   const long total = (long)per * HW * Cp;
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
+  const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
     const int c = (int)(i % Cp);
     const long pr = i / Cp;
     const int p = (int)(pr % HW), r = (int)(pr / HW);
-    const long row = (base + r) % n;
+    // rows past the end of a short final batch: zero image, label -1 (masked downstream)
+    const bool valid = wrap || base + r < n;
+    const long row = valid ? (base + r) % n : 0;
     float v = 0.f;
-    if (c < Cin) {
+    if (c < Cin && valid) {
       const long si = (row * HW + p) * Cin + c;
       v = x_u8 ? (float)((const uint8_t*)x)[si] / scale : ((const float*)x)[si];
     }
     xb[i] = f2bf(v);
-    if (p == 0 && c == 0) yb[r] = labels[row];
+    if (p == 0 && c == 0) yb[r] = valid ? labels[row] : -1;
   }
 }
 
@@ -541,7 +581,8 @@ hipError_t unpad_add(const float* src, int R, int C1, int C2, int C1p, int C2p, 
 
 hipError_t bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
                        float momentum, float* rmean, float* rvar, float* st, hipStream_t s) {
-  hipLaunchKernelGGL(bn_finalize_k, dim3((C + 63) / 64), dim3(NT), 0, s, part, T, C, count, gamma, beta, eps,
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_finalize_k, dim3(C / 8), dim3(NT), 0, s, part, T, C, count, gamma, beta, eps,
                      momentum, rmean, rvar, st);
   return hipGetLastError();
 }
@@ -571,7 +612,8 @@ hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, c
 hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const float* st, const float* gamma,
                            float* dgamma, float* dbeta, float* co, hipStream_t s) {
   (void)gamma;
-  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3((C + 63) / 64), dim3(NT), 0, s, part, T, C, count, st, dgamma, dbeta,
+  if (C % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3(C / 8), dim3(NT), 0, s, part, T, C, count, st, dgamma, dbeta,
                      co);
   return hipGetLastError();
 }
@@ -641,9 +683,9 @@ hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hi
   return hipGetLastError();
 }
 
-hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale,
+hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale, const Ctrl* ctrl,
                         uint16_t* dlogits, float* tail, hipStream_t s) {
-  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, dlogits, tail);
+  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, ctrl, dlogits, tail);
   return hipGetLastError();
 }
 

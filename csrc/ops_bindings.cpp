@@ -54,6 +54,10 @@ void register_kernel_ops(py::module_& m) {
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
       py::arg("stream"));
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
+  m.def("splitk_reduce", [](uintptr_t slab, int splits, long n, uintptr_t dst, uintptr_t stream) {
+    check(damd::splitk_reduce(P_<const float>(slab), splits, n, P_<float>(dst), P_<ihipStream_t>(stream)),
+          "splitk_reduce");
+  });
 
   using U = uintptr_t;
   using u16 = uint16_t;
@@ -117,9 +121,9 @@ void register_kernel_ops(py::module_& m) {
   m.def("colsum", [](U x, int x_f32, int M, int N, int ld, U out, U s) {
     check(damd::colsum(P_<const void>(x), x_f32, M, N, ld, P_<float>(out), P_<ihipStream_t>(s)), "colsum");
   });
-  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U dl, U tail, U s) {
-    check(damd::softmax_xent(P_<const float>(logits), ld, P_<const int32_t>(labels), B, K, scale, P_<u16>(dl),
-                             P_<float>(tail), P_<ihipStream_t>(s)),
+  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U ctrl, U dl, U tail, U s) {
+    check(damd::softmax_xent(P_<const float>(logits), ld, P_<const int32_t>(labels), B, K, scale,
+                             P_<const damd::Ctrl>(ctrl), P_<u16>(dl), P_<float>(tail), P_<ihipStream_t>(s)),
           "softmax_xent");
   });
   m.def("sgd_step", [](U P, U G, U V, U Pb, long n, U ctrl, U tail, U s) {

@@ -33,6 +33,10 @@ class Engine:
     def run(self, n_steps: int):
         raise NotImplementedError
 
+    def prepare(self, n_steps: int):
+        """Build whatever ``run(n_steps)`` will replay (HIP graphs) without executing a
+        step, so a timed ``run`` measures replay only."""
+
     def metrics(self) -> dict:
         """Global epoch-so-far averages, e.g. {'loss':..., 'accuracy':...} (syncs)."""
         raise NotImplementedError
@@ -51,6 +55,22 @@ class Engine:
 
     def sync(self):
         pass
+
+    def _own_variables(self, variables):
+        """Route host writes of these variables (set_weights, load_weights, layer-level
+        assign) through before/after_external_write."""
+        import weakref
+
+        ref = weakref.ref(self)
+        for v in variables:
+            v._engine_ref = ref
+
+    def before_external_write(self):
+        """A model variable is about to be overwritten from the host."""
+        self.sync()
+
+    def after_external_write(self):
+        """A model variable was overwritten from the host (refresh derived copies)."""
 
 
 def select_engine(model, strategy, per_replica: int, global_batch: int) -> Engine:

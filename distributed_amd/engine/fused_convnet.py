@@ -110,6 +110,7 @@ class FusedConvNetEngine(Engine):
             n = int(np.prod(shp))
             v._rebind(self.P[off:off + n].view(shp))
             off += n
+        self._own_variables(self.vars)
         opt = model.optimizer
         if opt.momentum and "momentum" in opt.slots and opt.slots["momentum"].numel() == NPARAM:
             self.V[:NPARAM].copy_(opt.slots["momentum"].to(dev))
@@ -246,6 +247,10 @@ class FusedConvNetEngine(Engine):
         self._pending = True
         self.steps_done += n_steps
 
+    def prepare(self, n_steps):
+        if self.use_graph and not self.host_collective and n_steps >= self.graph_steps:
+            self.trainer.capture(self.graph_steps)
+
     def _flush(self):
         if self._pending:
             self.trainer.flush()
@@ -277,4 +282,7 @@ class FusedConvNetEngine(Engine):
         torch.cuda.synchronize(self.device)
 
     def sync(self):
+        # host readers (get_weights, checkpoints, callbacks) see the trained values: the
+        # deferred update of the last step is applied first
+        self._flush()
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()

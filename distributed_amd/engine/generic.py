@@ -122,6 +122,11 @@ class GenericEngine(Engine):
                 for g, sz, off in zip(grads, self.sizes, self.offs):
                     if g is not None:
                         G[off:off + sz].copy_(g.reshape(-1))
+        elif self.bucketed:
+            # a replica with no rows (short last batch) still issues the same bucket
+            # sequence as the others: one all-reduce per bucket, in bucket order
+            comm = self.strategy.communicator
+            works = [comm.allreduce_async(G[lo:hi], "sum") for (lo, hi, _) in self.buckets]
         if works is not None:
             for w in works:
                 w.wait()
@@ -140,15 +145,23 @@ class GenericEngine(Engine):
             lo, hi, _ = self.buckets[b]
             works[b] = comm.allreduce_async(G[lo:hi], "sum")
 
+        nxt = [0]
+
+        def launch_ready():
+            # buckets start strictly in index order (a complete bucket waits for the
+            # earlier ones), so every rank issues the identical collective sequence even
+            # if autograd finishes parameters in a different order
+            while nxt[0] < len(self.buckets) and not left[nxt[0]]:
+                launch(nxt[0])
+                nxt[0] += 1
+
         def make_hook(i):
             def hook(g):
                 off, sz = self.offs[i], self.sizes[i]
                 with torch.no_grad():
                     G[off:off + sz].copy_(g.reshape(-1))
-                b = self.bucket_of[i]
-                left[b].discard(i)
-                if not left[b]:
-                    launch(b)
+                left[self.bucket_of[i]].discard(i)
+                launch_ready()
                 return g
             return hook
 
@@ -158,9 +171,8 @@ class GenericEngine(Engine):
         finally:
             for h in handles:
                 h.remove()
-        for b in range(len(self.buckets)):  # parameters that received no gradient
-            if works[b] is None:
-                launch(b)
+        for b in range(nxt[0], len(self.buckets)):  # parameters that received no gradient
+            launch(b)
         for leaf in self.leaves:
             leaf.grad = None
         return works

@@ -183,6 +183,7 @@ class NativeGraphEngine(Engine):
             self.views[id(v)] = self.P[off:off + sz].view(v.shape)
             self.bviews[id(v)] = self.Pb[off:off + sz].view(v.shape)
             self.gviews[id(v)] = self.G[off:off + sz].view(v.shape)
+        self._own_variables(self.vars)
         # non-trainable (BN moving statistics) live on the device as fp32
         for w in model.non_trainable_weights:
             if w.value.device != dev:
@@ -379,6 +380,7 @@ class NativeGraphEngine(Engine):
         self.st_ident = torch.cat([torch.zeros(1, 1), torch.ones(1, 1), torch.ones(1, 1), torch.zeros(1, 1)])
         self._ident_cache = {}
         maxM_C = 0
+        ws = 0  # fp32 weight-gradient split-K slabs, shared by every wgrad GEMM (serial on one stream)
         for nd in self.nodes:
             if nd.attrs.get("dead"):
                 continue
@@ -387,6 +389,8 @@ class NativeGraphEngine(Engine):
                 l = nd.layer
                 cin = nd.inputs[0].root().shape[3]
                 kh, kw, cin0, cout = l.kernel.shape
+                ws = max(ws, H.conv_wgrad_workspace_elems(nd.inputs[0].root().shape, (kh, kw, cin, cout), l.strides,
+                                                          l.padding))
                 nd.attrs["cin_pad"] = cin
                 if cin != cin0:
                     nd.attrs["w_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.bfloat16, device=dev)
@@ -411,6 +415,7 @@ class NativeGraphEngine(Engine):
             elif k == "Dense":
                 l = nd.layer
                 kin, units = l.kernel.shape
+                ws = max(ws, H.wgrad_workspace_elems(kin, _pad8(units), self.B))
                 if nd.attrs.get("logits") and units % 8:
                     up = _pad8(units)
                     nd.attrs["w_pad"] = torch.zeros(kin, up, dtype=torch.bfloat16, device=dev)
@@ -424,6 +429,8 @@ class NativeGraphEngine(Engine):
         self.scratch = torch.zeros(big, dtype=torch.bfloat16, device=dev)
         self.scratch2 = torch.zeros(big, dtype=torch.bfloat16, device=dev)
         nbytes += big * 4
+        self.wgrad_ws = torch.zeros(max(ws, 4), dtype=torch.float32, device=dev)
+        nbytes += self.wgrad_ws.numel() * 4
         self.act_bytes = nbytes
 
     # --- gradient buckets (all-reduce overlapped with the rest of backward) ------------------
@@ -610,7 +617,8 @@ class NativeGraphEngine(Engine):
         live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
         for nd in live:
             getattr(self, "_fwd_" + nd.kind)(nd)
-        H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:])
+        H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:],
+                       ctrl=self.ctrl)
         for t in self._all_tensors():
             t.root().written = False
         self._bucket_begin()
@@ -728,11 +736,11 @@ class NativeGraphEngine(Engine):
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
             dwp.zero_()
-            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding)
+            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=self.wgrad_ws)
             kh, kw, cin, cout = l.kernel.shape
             H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
         else:
-            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding)
+            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=self.wgrad_ws)
         if xt.needs_grad:
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written
@@ -851,11 +859,11 @@ class NativeGraphEngine(Engine):
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
             dwp.zero_()
-            H.dense_wgrad(x2, dy, dwp)
+            H.dense_wgrad(x2, dy, dwp, workspace=self.wgrad_ws)
             kin = l.kernel.shape[0]
             H.unpad_add(dwp, 1, kin, units, kin, dwp.shape[1], self.gviews[id(l.kernel)])
         else:
-            H.dense_wgrad(x2, dy, self.gviews[id(l.kernel)])
+            H.dense_wgrad(x2, dy, self.gviews[id(l.kernel)], workspace=self.wgrad_ws)
         if xt.needs_grad:
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written
@@ -897,6 +905,10 @@ class NativeGraphEngine(Engine):
                 self._capture_safe()
             self.graph.replay()
 
+    def prepare(self, n_steps):
+        if self.use_graph and not self.host_collective and self.graph is None and n_steps > 0:
+            self._capture_safe()
+
     def _capture_safe(self):
         # capturing would run allocator/stream ops; make sure no work is pending
         torch.cuda.synchronize(self.device)
@@ -935,4 +947,10 @@ class NativeGraphEngine(Engine):
                 o += sz
 
     def sync(self):
+        torch.cuda.synchronize(self.device)
+
+    def after_external_write(self):
+        # the forward/backward GEMMs read the bf16 shadow Pb: re-derive it from the
+        # overwritten fp32 masters before the next step
+        H.cast_bf16(self.P, self.Pb)
         torch.cuda.synchronize(self.device)

@@ -40,6 +40,9 @@ class Variable:
         self.name = name
         self._t = value
         self.trainable = trainable
+        # weakref to the engine whose flat buffer holds this variable: host writes go
+        # through its before/after hooks (flush a deferred update, refresh bf16 shadows)
+        self._engine_ref = None
 
     @property
     def value(self) -> torch.Tensor:
@@ -60,8 +63,13 @@ class Variable:
         t = torch.as_tensor(np.asarray(v), dtype=self._t.dtype)
         if tuple(t.shape) != self.shape:
             raise ValueError(f"assign shape {tuple(t.shape)} != {self.shape} for {self.name}")
+        eng = self._engine_ref() if self._engine_ref is not None else None
+        if eng is not None:
+            eng.before_external_write()
         with torch.no_grad():
             self._t.copy_(t.to(self._t.device))
+        if eng is not None:
+            eng.after_external_write()
 
     def _rebind(self, storage: torch.Tensor) -> None:
         """Point this variable at ``storage`` (same shape), copying the current value."""

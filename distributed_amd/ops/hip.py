@@ -22,7 +22,7 @@ from ..native import require_C
 
 A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD = range(5)
 B_NC, B_KC = 0, 1
-E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD = 1, 2, 4, 8, 16, 32
+E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB = 1, 2, 4, 8, 16, 32, 64
 BK = 32
 
 
@@ -83,6 +83,44 @@ def pick_splits(M: int, N: int, K: int, tile: int, target_wg: int = 1024) -> Tup
     return splits, kps
 
 
+# weight-gradient split-K: every split stores its fp32 partial tile to a slab and one
+# reduce kernel adds the slabs into the gradient in fixed order (deterministic; fp32
+# atomics from hundreds of blocks on the same addresses serialise at the memory side)
+WGRAD_TARGET_WG = 512          # 2 workgroups per CU
+WGRAD_SLAB_MAX = 64 << 20      # bytes of slab per GEMM
+
+
+def wgrad_plan(M: int, N: int, K: int) -> Tuple[int, int, int]:
+    """(tile, splits, k_per_split) of a weight-gradient GEMM [M,N] summed over K."""
+    t = pick_tile(N)
+    bm, bn = (256, 64) if t == 1 else (128, 128)
+    tiles = -(-M // bm) * -(-N // bn)
+    cap = max(1, WGRAD_SLAB_MAX // (M * N * 4))
+    splits = max(1, min(-(-WGRAD_TARGET_WG // tiles), max(1, K // 256), cap))
+    kps = -(-K // splits)
+    kps = -(-kps // BK) * BK
+    return t, -(-K // kps), kps
+
+
+def wgrad_workspace_elems(M: int, N: int, K: int) -> int:
+    _, splits, _ = wgrad_plan(M, N, K)
+    return splits * M * N if splits > 1 else 0
+
+
+def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
+    t, splits, kps = wgrad_plan(M, N, K)
+    if splits == 1:  # one writer per element: the atomic epilogue is an uncontended add
+        gemm(A, B, dw, amode=amode, bmode=B_NC, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N, epi=E_ATOMIC, geo=geo,
+             tile=t)
+        return
+    need = splits * M * N
+    if workspace is None or workspace.numel() < need or workspace.dtype != torch.float32:
+        raise ValueError(f"weight-gradient GEMM needs an fp32 workspace of {need} elements")
+    gemm(A, B, workspace, amode=amode, bmode=B_NC, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N, epi=E_SLAB,
+         splits=splits, k_per_split=kps, tile=t, geo=geo)
+    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle())
+
+
 def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
          geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None):
     t = pick_tile(N) if tile is None else tile
@@ -121,18 +159,17 @@ def dense_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, accumulate=
          R=dx if accumulate else None)
 
 
-def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor):
-    """dw[K,N] += x[M,K]^T @ dy[M,N] (fp32, atomically accumulated; split over M)."""
+def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, workspace: Optional[torch.Tensor] = None):
+    """dw[K,N] += x[M,K]^T @ dy[M,N] (fp32; split over M, slabs reduced in fixed order)."""
     M, K = x.shape
     M2, N = dy.shape
     assert M == M2 and tuple(dw.shape) == (K, N)
     _chk(x, torch.bfloat16, "x")
     _chk(dy, torch.bfloat16, "dy")
     _chk(dw, torch.float32, "dw")
-    t = pick_tile(N)
-    splits, kps = pick_splits(K, N, M, t)
-    gemm(x, dy, dw, amode=A_MC, bmode=B_NC, M=K, N=N, K=M, lda=K, ldb=N, ldc=N, epi=E_ATOMIC, splits=splits,
-         k_per_split=kps, tile=t)
+    if workspace is None and wgrad_workspace_elems(K, N, M):
+        workspace = torch.empty(wgrad_workspace_elems(K, N, M), device=x.device)
+    _wgrad_gemm(x, dy, dw, workspace, amode=A_MC, M=K, N=N, K=M, lda=K, ldb=N)
 
 
 # ---- conv ---------------------------------------------------------------------------------
@@ -175,8 +212,14 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False):
          geo=(h, wd, cout, ho, wo, kh, kw, s, pad), R=dx if accumulate else None)
 
 
-def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid"):
-    """dw [KH,KW,Cin,Cout] += sum over pixels of im2col(x)^T dy (fp32 atomics, split-K)."""
+def conv_wgrad_workspace_elems(x_shape, w_shape, strides=(1, 1), padding="valid") -> int:
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
+    return wgrad_workspace_elems(kh * kw * cin, cout, n * ho * wo)
+
+
+def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid", workspace: Optional[torch.Tensor] = None):
+    """dw [KH,KW,Cin,Cout] += sum over pixels of im2col(x)^T dy (split-K over pixels, fp32
+    slabs in ``workspace`` (conv_wgrad_workspace_elems) reduced in fixed order)."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, dw.shape, strides, padding)
     _chk(x, torch.bfloat16, "x")
     _chk(dy, torch.bfloat16, "dy")
@@ -184,10 +227,10 @@ def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid"):
     if cin % 8 or cout % 8:
         raise ValueError("conv_wgrad: Cin and Cout must be multiples of 8")
     M, N, K = kh * kw * cin, cout, n * ho * wo
-    t = pick_tile(N)
-    splits, kps = pick_splits(M, N, K, t)
-    gemm(x, dy, dw, amode=A_WGRAD, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=cout, epi=E_ATOMIC, splits=splits,
-         k_per_split=kps, tile=t, geo=(h, wd, cin, ho, wo, kh, kw, s, pad))
+    if workspace is None and wgrad_workspace_elems(M, N, K):
+        workspace = torch.empty(wgrad_workspace_elems(M, N, K), device=x.device)
+    _wgrad_gemm(x, dy, dw, workspace, amode=A_WGRAD, M=M, N=N, K=K, ldb=cout,
+                geo=(h, wd, cin, ho, wo, kh, kw, s, pad))
 
 
 # ---- BN / pooling / loss / optimizer -------------------------------------------------------------
@@ -260,9 +303,11 @@ def colsum(x, out):
     _C().colsum(_ptr(x), int(x.dtype == torch.float32), M, N, N, _ptr(out), stream_handle())
 
 
-def softmax_xent(logits, labels, K, scale, dlogits, tail):
+def softmax_xent(logits, labels, K, scale, dlogits, tail, ctrl=None):
+    """ctrl (the engine's device control block) makes the scale 1 / real rows of the global
+    batch; labels < 0 mark padding rows of a short final batch."""
     B, ld = logits.shape
-    _C().softmax_xent(_ptr(logits), ld, _ptr(labels), B, K, float(scale), _ptr(dlogits), _ptr(tail),
+    _C().softmax_xent(_ptr(logits), ld, _ptr(labels), B, K, float(scale), _ptr(ctrl), _ptr(dlogits), _ptr(tail),
                       stream_handle())
 
 

@@ -15,7 +15,8 @@ import distributed_amd as tf  # noqa: E402
 
 def main():
     out = os.environ["DAMD_TEST_OUT"]
-    steps = int(os.environ.get("DAMD_TEST_STEPS", "3"))
+    steps = int(os.environ.get("DAMD_TEST_STEPS", "3")) or None  # 0 -> full epochs
+    rows = int(os.environ.get("DAMD_TEST_ROWS", "4096"))
     epochs = int(os.environ.get("DAMD_TEST_EPOCHS", "2"))
     per = int(os.environ.get("DAMD_TEST_PER_REPLICA", "16"))
     strategy = tf.distribute.experimental.MultiWorkerMirroredStrategy()
@@ -26,8 +27,8 @@ def main():
     tf.set_seed(100 + rank)
     mnist = tf.keras.datasets.mnist
     (x_train, y_train), _ = mnist.load_data()
-    x_train = x_train[:4096].reshape(4096, 28, 28, 1) / 255.0
-    y_train = y_train[:4096]
+    x_train = x_train[:rows].reshape(rows, 28, 28, 1) / 255.0
+    y_train = y_train[:rows]
     with strategy.scope():
         model = tf.keras.Sequential([
             tf.keras.layers.Conv2D(32, 3, activation='relu', input_shape=(28, 28, 1)),

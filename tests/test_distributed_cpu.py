@@ -59,6 +59,32 @@ def test_two_workers_mirror_and_match_single_worker(tmp_path):
     np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-5)
 
 
+@pytest.mark.timeout(300)
+def test_short_last_batch_with_many_buckets(tmp_path):
+    """70 rows at global batch 64: the second step has 6 rows, all on rank 0, so rank 1
+    has no rows but must issue the same per-bucket all-reduce sequence (tiny buckets:
+    one per parameter).  Replicas stay mirrored and match one worker at batch 64."""
+    d2 = tmp_path / "w2"
+    d2.mkdir()
+    res = launch.launch_script([WORKER], nproc=2, env=_env(d2, DAMD_TEST_PER_REPLICA=32, DAMD_TEST_ROWS=70,
+                                                           DAMD_TEST_STEPS=0, DAMD_BUCKET_MB=0.001), timeout=240)
+    assert res.ok, res.returncodes
+    (w0, j0), (w1, j1) = _load(d2, 0), _load(d2, 1)
+    assert all(np.array_equal(a, b) for a, b in zip(w0, w1))
+    assert j0["history"] == j1["history"]
+    assert j0["iterations"] == 4  # 2 epochs x ceil(70 / 64) steps
+    d1 = tmp_path / "w1"
+    d1.mkdir()
+    res = launch.launch_script([WORKER], nproc=1, env=_env(d1, DAMD_TEST_PER_REPLICA=64, DAMD_TEST_ROWS=70,
+                                                           DAMD_TEST_STEPS=0, DAMD_TEST_INIT_FROM=d2 / "init0.npz"),
+                               timeout=240)
+    assert res.ok, res.returncodes
+    ws, js = _load(d1, 0)
+    for a, b in zip(w0, ws):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-5)
+
+
 def _ranked(df, barrier):
     import os as _os
 

@@ -221,6 +221,17 @@ def test_gap_xent_colsum_sgd(H):
     close(tail[0], loss.sum(), 1e-5, 1e-6)
     assert tail[1].item() == ref.sparse_accuracy(z[:, :K], lab).sum().item()
     assert tail[2].item() == B
+    # a label < 0 masks its row: zero gradient, no loss / metric contribution
+    lab2 = lab.clone()
+    lab2[2] = -1
+    dl2 = torch.ones(B, ld, device=dev, dtype=torch.bfloat16)
+    tail2 = torch.zeros(3, device=dev)
+    H.softmax_xent(z, lab2, K, 0.5, dl2, tail2)
+    keep = torch.tensor([0, 1, 3, 4], device=dev)
+    close(dl2[keep, :K], gz[keep], 1e-2, 4e-3)
+    assert dl2[2, :K].abs().max().item() == 0
+    close(tail2[0], loss[keep].sum(), 1e-5, 1e-6)
+    assert tail2[2].item() == B - 1
     # column sums (bias grads)
     a = rb(rnd(300, 24, seed=25))
     cs = torch.zeros(24, device=dev)

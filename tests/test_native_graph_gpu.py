@@ -248,6 +248,52 @@ def test_mnist_native_graph_tracks_reference_over_steps():
     _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=0.97, rel_max=0.25)
 
 
+def test_short_final_batch_is_masked_like_keras():
+    """100 rows at batch 64: the second step has 36 real rows.  The native engine masks the
+    28 padding rows (zero gradient, no loss/metric) and scales by 1/36, like the fp32
+    generic engine on its real 36-row batch (it used to wrap around)."""
+    x, y = _data(100, (28, 28, 1), 10, seed=8)
+    tf.keras.backend.clear_session()
+    init = _mnist().get_weights()
+    wn, hn, en = _train(_mnist, x, y, init, 64, None, native=True, lr=0.05)
+    wr, hr, er = _train(_mnist, x, y, init, 64, None, native=False, device="cpu", lr=0.05)
+    assert en == "native_graph" and er == "generic"
+    np.testing.assert_allclose(hn["loss"], hr["loss"], rtol=1e-2)
+    np.testing.assert_allclose(hn["accuracy"], hr["accuracy"], atol=1.5 / 100)
+    _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=0.97, rel_max=0.25)
+
+
+def test_set_weights_refreshes_bf16_shadow():
+    """set_weights on a model whose native engine is cached: the next step must use the new
+    weights (the bf16 shadow the GEMMs read is re-derived), i.e. equal a fresh engine."""
+    x, y = _data(128, (32, 32, 3), 10, seed=9)
+    os.environ["DAMD_FUSED"] = "0"
+    try:
+        tf.keras.backend.clear_session()
+        init_a = _small_resnet().get_weights()
+        init_b = _small_resnet().get_weights()
+        res = []
+        for warm in (True, False):
+            tf.keras.backend.clear_session()
+            m = _small_resnet()
+            m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tf.keras.optimizers.SGD(learning_rate=0.05), metrics=["accuracy"])
+            if warm:
+                m.set_weights(init_a)
+                m.fit(x, y, batch_size=32, epochs=1, steps_per_epoch=1, shuffle=False, verbose=0)
+                assert m._engine is not None
+            m.set_weights(init_b)
+            h = m.fit(x, y, batch_size=32, epochs=1, steps_per_epoch=1, shuffle=False, verbose=0)
+            assert m._engine.name == "native_graph"
+            res.append((m.get_weights(), h.history["loss"][0]))
+        (wa, la), (wb, lb) = res
+        assert abs(la - lb) < 1e-4 * abs(lb)
+        for a, b in zip(wa, wb):
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    finally:
+        os.environ.pop("DAMD_FUSED", None)
+
+
 def test_graph_replay_equals_eager():
     """Replaying the captured step == running it eagerly.  Two steps: step 1 eager in both,
     step 2 replayed vs eager.  (Longer runs drift apart by run-to-run noise either way:
