@@ -98,16 +98,26 @@ class Strategy:
 
     # --- collectives on host values -------------------------------------------
     def reduce(self, op, value, axis=None):
-        """Reduce a per-replica value across replicas (tf.distribute.Strategy.reduce)."""
+        """Reduce a per-replica value across replicas (tf.distribute.Strategy.reduce).
+
+        With ``axis`` the value is first reduced along that axis on each replica (SUM/MAX/MIN),
+        and MEAN is the mean over every element along ``axis`` on every replica."""
         t = torch.as_tensor(value, dtype=torch.float64).clone()
+        key = {ReduceOp.SUM: "sum", ReduceOp.MEAN: "mean"}.get(op, op)
+        if key not in ("sum", "mean", "max", "min"):
+            raise ValueError(f"unsupported reduce op {op!r}")
+        count = 1.0
         if axis is not None:
-            t = t.sum(dim=axis) if op in (ReduceOp.SUM, "sum", ReduceOp.MEAN, "mean") else t
-        comm = self.communicator
-        if op in (ReduceOp.MEAN, "mean"):
-            comm.allreduce_(t, "sum")
-            t = t / self.num_replicas_in_sync
-        else:
-            comm.allreduce_(t, {"sum": "sum", "max": "max", "min": "min"}[op])
+            if key in ("sum", "mean"):
+                count = float(t.shape[axis])
+                t = t.sum(dim=axis)
+            else:
+                t = t.amax(dim=axis) if key == "max" else t.amin(dim=axis)
+        n = self.num_replicas_in_sync
+        if n > 1:  # world 1 has no process group: nothing to combine
+            self.communicator.allreduce_(t, "sum" if key == "mean" else key)
+        if key == "mean":
+            t = t / (count * n)
         return t
 
     def broadcast_tensor_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:

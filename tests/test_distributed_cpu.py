@@ -85,6 +85,38 @@ def test_short_last_batch_with_many_buckets(tmp_path):
     np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-5)
 
 
+def _reduce_fn(df, barrier):
+    import json as _json
+    import os as _os
+
+    _os.environ["DAMD_DEVICE"] = "cpu"
+    _os.environ["TF_CONFIG"] = _json.dumps({"cluster": {"worker": barrier["address"]},
+                                            "task": {"type": "worker", "index": barrier["partition"]}})
+    import distributed_amd as tf
+    from distributed_amd.parallel import runtime
+
+    s = tf.distribute.experimental.MultiWorkerMirroredStrategy()
+    r = s.rank
+    v = [[r + 1.0, 10.0 * r], [2.0, -r - 1.0]]
+    out = {k: s.reduce(k, v).tolist() for k in ("sum", "mean", "max", "min")}
+    out["mean_axis0"] = s.reduce(tf.distribute.ReduceOp.MEAN, v, axis=0).tolist()
+    out["max_axis1"] = s.reduce("max", v, axis=1).tolist()
+    runtime.shutdown()
+    return out
+
+
+def test_strategy_reduce_two_ranks():
+    a, b = launch.barrier_apply(_reduce_fn, 2, on_error="raise")
+    assert a == b
+    assert a["sum"] == [[3.0, 10.0], [4.0, -3.0]]
+    assert a["mean"] == [[1.5, 5.0], [2.0, -1.5]]
+    assert a["max"] == [[2.0, 10.0], [2.0, -1.0]]
+    assert a["min"] == [[1.0, 0.0], [2.0, -2.0]]
+    # mean over both rows of both replicas: col0 (1+2+2+2)/4, col1 (0-1+10-2)/4
+    assert a["mean_axis0"] == [1.75, 1.75]
+    assert a["max_axis1"] == [10.0, 2.0]
+
+
 def _ranked(df, barrier):
     import os as _os
 

@@ -59,3 +59,19 @@ def test_two_ranks_one_gpu_match_single_rank(tmp_path, engine):
         np.testing.assert_allclose(a, b, **tol)
     np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-3)
     np.testing.assert_allclose(j0["history"]["accuracy"], js["history"]["accuracy"], atol=1.5 / 64)
+
+
+def test_strategy_reduce_world1_gpu():
+    """World 1 on a GPU runs a size-1 RCCL communicator with no process group: host-value
+    reduce must not reach torch.distributed."""
+    import distributed_amd as tf
+    from distributed_amd.parallel import runtime
+
+    runtime.shutdown()
+    s = tf.distribute.experimental.MultiWorkerMirroredStrategy()
+    try:
+        assert s.num_replicas_in_sync == 1 and s.device.type == "cuda"
+        assert s.reduce("sum", [1.0, 2.0]).tolist() == [1.0, 2.0]
+        assert s.reduce("mean", [[1.0, 3.0]], axis=1).tolist() == [2.0]
+    finally:
+        runtime.shutdown()

@@ -244,3 +244,15 @@ def test_r_style_verbs_and_history_metrics():
     res = k.fit(model, x, mnist["train"]["y"][:640], batch_size=64, epochs=2, steps_per_epoch=3, verbose=0)
     assert len(res.metrics["accuracy"]) == 2
     assert model.count_params() == 347146
+
+
+def test_strategy_reduce_single_replica():
+    """World 1 (no process group): reduce applies only the axis reduction."""
+    import distributed_amd as tf
+
+    s = tf.distribute.experimental.MultiWorkerMirroredStrategy()
+    assert s.num_replicas_in_sync == 1
+    v = [[1.0, 2.0], [3.0, 5.0]]
+    assert s.reduce("sum", v).tolist() == v
+    assert s.reduce(tf.distribute.ReduceOp.MEAN, v, axis=0).tolist() == [2.0, 3.5]
+    assert s.reduce("min", v, axis=1).tolist() == [1.0, 3.0]
