@@ -13,6 +13,7 @@
 #include "convnet.h"
 #include "damd_common.h"
 #include "kernels_api.h"
+#include "peer_comm.h"
 #include "step_executor.h"
 
 namespace py = pybind11;
@@ -62,7 +63,10 @@ class ConvNetTrainer : public StepExecutor {
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
-    if (grad_allreduce_ && comm_)  // comm set only when a reduction is wanted
+    if (!grad_allreduce_) return;
+    if (peer_)  // native xGMI two-shot all-reduce
+      peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_);
+    else if (comm_)  // comm set only when a reduction is wanted
       comm_->allreduce(b_.G, b_.G, convnet_grad_count(PP_), 0, 0, stream_);
   }
 
@@ -116,12 +120,36 @@ PYBIND11_MODULE(_C, m) {
     return stream_wait_with_deadline(P_<ihipStream_t>(st), timeout_s, nullptr);
   });
 
+  py::class_<PeerAllreduce>(m, "PeerAllreduce")
+      .def(py::init<int, int, int, long, int, double>(), py::arg("world"), py::arg("rank"), py::arg("device"),
+           py::arg("capacity"), py::arg("blocks") = 64, py::arg("timeout_s") = 120.0)
+      .def("handles", [](PeerAllreduce& p) { return py::bytes(p.handles()); })
+      .def("open",
+           [](PeerAllreduce& p, std::vector<py::bytes> hs) {
+             std::vector<std::string> v;
+             for (auto& h : hs) v.emplace_back(std::string(h));
+             p.open(v);
+           })
+      .def("allreduce",
+           [](PeerAllreduce& p, uintptr_t data, long n, uintptr_t st) {
+             p.allreduce(P_<float>(data), n, P_<ihipStream_t>(st));
+           })
+      .def("link_local", &PeerAllreduce::link_local)
+      .def("status", &PeerAllreduce::status)
+      .def("clear_status", &PeerAllreduce::clear_status)
+      .def("set_timeout", &PeerAllreduce::set_timeout)
+      .def_property_readonly("ready", &PeerAllreduce::ready)
+      .def_property_readonly("capacity", &PeerAllreduce::capacity)
+      .def_property_readonly("world", &PeerAllreduce::world)
+      .def_property_readonly("rank", &PeerAllreduce::rank);
+
   py::class_<ConvNetTrainer>(m, "ConvNetTrainer")
       .def(py::init<int, py::dict, int, int, int>(), py::arg("device"), py::arg("buffers"),
            py::arg("batch"), py::arg("positions_per_slice") = 4, py::arg("grad_allreduce") = 1)
       .def("set_data", &ConvNetTrainer::set_data, py::arg("x"), py::arg("labels"), py::arg("x_u8") = 0)
       .def("set_comm", [](ConvNetTrainer& t, RcclComm* c) { t.set_comm(c); },
            py::keep_alive<1, 2>())
+      .def("set_peer", [](ConvNetTrainer& t, PeerAllreduce* p) { t.set_peer(p); }, py::keep_alive<1, 2>())
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
       .def("capture", &ConvNetTrainer::capture)
       .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())

@@ -1,0 +1,135 @@
+// xGMI peer-to-peer two-shot all-reduce kernel (algorithm and safety argument:
+// csrc/runtime/peer_comm.h).
+//
+// Memory-model notes (gfx950):
+//  - `in`, `out` and the flag words are allocated uncached (hipDeviceMallocUncached,
+//    MTYPE UC): every access goes to the owning GPU's memory, nothing is held in any
+//    L1/L2, so cross-device visibility needs no L2 write-back or invalidate (a
+//    system-scope release/acquire costs a whole-L2 buffer_wbl2 / buffer_inv per block:
+//    ~2-6 us each, measured as 21 us per call with them vs the UC form below).
+//  - Publish: every wave drains its stores (s_waitcnt vmcnt(0)) -> workgroup barrier ->
+//    thread 0 stores the flag (relaxed, system scope) into every rank's flag array.
+//  - Consume: threads 0..W-1 poll one source each (relaxed system-scope loads + s_sleep)
+//    -> workgroup barrier -> loads (the barrier also keeps the compiler from hoisting them).
+//  - The local gradient itself is ordinary (cached) memory: it is only read and written
+//    by this device, in stream order with the kernels around this one.
+//  - Reductions are in a fixed peer order, so all ranks end bitwise identical.
+#include "peer_comm.h"
+
+namespace damd {
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ unsigned* flag_slot(unsigned* base, int phase, int src, int blk) {
+  return base + ((size_t)phase * kPeerMaxRanks + src) * kPeerMaxBlocks + blk;
+}
+
+// thread 0: publish this block's phase to every rank (own flags included: uniform waits)
+__device__ __forceinline__ void signal_all(const PeerArgs& a, int phase, unsigned e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's UC stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int p = 0; p < a.world; ++p)
+      __hip_atomic_store(flag_slot(a.flags[p], phase, a.rank, blockIdx.x), e, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// threads 0..world-1 each wait for one source rank's flag of this block
+__device__ __forceinline__ void wait_all(const PeerArgs& a, int phase, unsigned e) {
+  const int t = threadIdx.x;
+  if (t < a.world) {
+    unsigned* f = flag_slot(a.flags[a.rank], phase, t, blockIdx.x);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+        __hip_atomic_fetch_or(a.status, 1u << phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __restrict__ data, long n) {
+  const int b = blockIdx.x, t = threadIdx.x, W = a.world;
+  const long chunk = a.chunk, shard = chunk * a.nblk;
+  const unsigned e = a.epoch[b] + 1;
+  const long c4 = chunk / 4;
+
+  // A: local gradient -> own `in` (chunk set b), zero beyond n
+  float4* in_own = reinterpret_cast<float4*>(a.in[a.rank]);
+  for (int s = 0; s < W; ++s) {
+    const long base = s * shard + (long)b * chunk;
+    for (long i = t; i < c4; i += NT) {
+      const long g = base + 4 * i;
+      float4 v;
+      if (g + 3 < n) {
+        v = *reinterpret_cast<const float4*>(data + g);
+      } else {
+        v.x = g < n ? data[g] : 0.f;
+        v.y = g + 1 < n ? data[g + 1] : 0.f;
+        v.z = g + 2 < n ? data[g + 2] : 0.f;
+        v.w = 0.f;
+      }
+      in_own[base / 4 + i] = v;
+    }
+  }
+  signal_all(a, 0, e);
+  wait_all(a, 0, e);
+
+  // B: reduce chunk (rank, b) over every rank's `in`, broadcast into every `out`
+  {
+    const long base4 = (a.rank * shard + (long)b * chunk) / 4;
+    for (long i = t; i < c4; i += NT) {
+      float4 v[kPeerMaxRanks];
+#pragma unroll
+      for (int p = 0; p < kPeerMaxRanks; ++p)
+        if (p < W) v[p] = reinterpret_cast<const float4*>(a.in[p])[base4 + i];
+      float4 acc = v[0];
+#pragma unroll
+      for (int p = 1; p < kPeerMaxRanks; ++p)
+        if (p < W) {
+          acc.x += v[p].x; acc.y += v[p].y; acc.z += v[p].z; acc.w += v[p].w;
+        }
+#pragma unroll
+      for (int p = 0; p < kPeerMaxRanks; ++p)
+        if (p < W) reinterpret_cast<float4*>(a.out[p])[base4 + i] = acc;
+    }
+  }
+  signal_all(a, 1, e);
+  wait_all(a, 1, e);
+
+  // D: own `out` (chunk set b) -> local gradient
+  const float4* out_own = reinterpret_cast<const float4*>(a.out[a.rank]);
+  for (int s = 0; s < W; ++s) {
+    const long base = s * shard + (long)b * chunk;
+    for (long i = t; i < c4; i += NT) {
+      const long g = base + 4 * i;
+      const float4 v = out_own[base / 4 + i];
+      if (g + 3 < n) {
+        *reinterpret_cast<float4*>(data + g) = v;
+      } else {
+        if (g < n) data[g] = v.x;
+        if (g + 1 < n) data[g + 1] = v.y;
+        if (g + 2 < n) data[g + 2] = v.z;
+      }
+    }
+  }
+  if (t == 0) a.epoch[b] = e;
+}
+
+}  // namespace
+
+hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, hipStream_t st) {
+  if (a.world < 1 || a.world > kPeerMaxRanks || a.nblk < 1 || a.nblk > kPeerMaxBlocks || a.chunk % 4)
+    return hipErrorInvalidValue;
+  if ((long)a.world * a.nblk * a.chunk < n) return hipErrorInvalidValue;
+  if (reinterpret_cast<uintptr_t>(data) % 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, data, n);
+  return hipGetLastError();
+}
+
+}  // namespace damd

@@ -51,6 +51,9 @@ void StepExecutor::capture(int k) {
   hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
   hipGraphDestroy(g);
   HIP_CHECK(e);
+  // upload now, so the first replay inside a timed loop does not pay for it
+  HIP_CHECK(hipGraphUpload(ge, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
   graphs_[k] = ge;
 }
 

@@ -11,6 +11,7 @@
 #include <memory>
 
 #include "comm.h"
+#include "peer_comm.h"
 
 namespace damd {
 
@@ -24,6 +25,9 @@ class StepExecutor {
   hipStream_t stream() const { return stream_; }
   void set_comm(RcclComm* comm) { comm_ = comm; invalidate_graphs(); }
   RcclComm* comm() const { return comm_; }
+  // native xGMI all-reduce for the per-step gradient (takes precedence over RCCL)
+  void set_peer(PeerAllreduce* p) { peer_ = p; invalidate_graphs(); }
+  PeerAllreduce* peer() const { return peer_; }
 
   // Enqueue k steps eagerly (one host launch per kernel).
   void step(int k);
@@ -40,6 +44,7 @@ class StepExecutor {
   virtual void enqueue_one_step() = 0;
   hipStream_t stream_ = nullptr;
   RcclComm* comm_ = nullptr;
+  PeerAllreduce* peer_ = nullptr;
   int device_;
 
  private:

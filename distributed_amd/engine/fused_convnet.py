@@ -135,11 +135,28 @@ class FusedConvNetEngine(Engine):
         # at world 1: the multi-GPU graph path exercised on a single GPU
         force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
         native = strategy.communicator.native if (self.world > 1 or force) else None
+        # per-step gradient all-reduce: the native xGMI peer-to-peer kernel when every rank
+        # can map every peer (DAMD_ALLREDUCE=auto|xgmi), else RCCL inside the captured step
+        self.peer = None
+        mode = env.get_str("DAMD_ALLREDUCE", "auto").lower()
+        if self.world > 1 and mode in ("auto", "xgmi"):
+            from ..parallel.communicator import make_peer_allreduce
+
+            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, C.convnet_grad_count(self.PP),
+                                            blocks=env.get_int("DAMD_PEER_BLOCKS", 64))
+            if self.peer is None and mode == "xgmi":
+                raise RuntimeError("DAMD_ALLREDUCE=xgmi but the peer-to-peer all-reduce is unavailable")
         # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
         # time, the gradient/metric buffer all-reduced through the host between steps
-        self.host_collective = self.world > 1 and native is None
-        if native is not None:
+        self.host_collective = self.world > 1 and native is None and self.peer is None
+        if self.peer is not None:
+            self.trainer.set_peer(self.peer)
+        elif native is not None:
             self.trainer.set_comm(native)
+        if self.world > 1:
+            dlog.info("fused ConvNet engine: gradient all-reduce via %s",
+                      "xGMI peer-to-peer kernel" if self.peer is not None else
+                      ("RCCL" if native is not None else "host (gloo)"))
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph_steps = max(1, env.get_int("DAMD_GRAPH_STEPS", 20))
         self.watchdog_s = env.get_float("DAMD_WATCHDOG_S", 0.0)
@@ -152,7 +169,12 @@ class FusedConvNetEngine(Engine):
     # --- host <-> ctrl ---------------------------------------------------------------
     def _ctrl_host(self):
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        self._check_peer()
         return self.ctrl.cpu().tolist()
+
+    def _check_peer(self):
+        if self.peer is not None and self.peer.status():
+            raise RuntimeError("xGMI peer all-reduce: a wait for a peer timed out (peer missing or wedged)")
 
     def _ctrl_write(self, updates: dict):
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()

@@ -215,6 +215,64 @@ class RcclCommunicator(TorchCommunicator):
         self._comm = None
 
 
+def make_peer_allreduce(comm: Communicator, device: int, capacity: int, blocks: int = 64,
+                        timeout_s: float = 120.0, selftest: bool = True):
+    """Native xGMI two-shot all-reduce (csrc/runtime/peer_comm.h) for ``capacity`` fp32
+    values per call, or None.  Every step is agreed by all ranks over the control plane
+    (IPC export, mapping, and a device self-test against a closed-form result), so either
+    every rank gets a working instance or every rank falls back to RCCL."""
+    W, r = comm.world_size, comm.rank
+    if W < 2:
+        return None
+    from ..native import require_C
+
+    C = require_C()
+    pa, h = None, None
+    try:
+        pa = C.PeerAllreduce(W, r, device, int(capacity), int(blocks), float(timeout_s))
+        h = pa.handles()
+    except Exception as e:  # pragma: no cover - exercised on hardware only
+        dlog.warning("peer all-reduce unavailable on rank %d: %s", r, e)
+    hs = comm.allgather_object(h)
+    if any(x is None for x in hs):
+        return None
+    ok = True
+    try:
+        pa.open(list(hs))
+    except Exception as e:  # pragma: no cover
+        dlog.warning("peer all-reduce: mapping peer buffers failed on rank %d: %s", r, e)
+        ok = False
+    if not all(comm.allgather_object(ok)):
+        return None
+    if selftest:
+        ok = _peer_selftest(pa, device, int(capacity), W, r)
+        if not all(comm.allgather_object(ok)):
+            dlog.warning("peer all-reduce self-test failed; using RCCL")
+            return None
+    pa.set_timeout(float(timeout_s))
+    return pa
+
+
+def _peer_selftest(pa, device: int, n: int, W: int, r: int) -> bool:
+    """Three back-to-back all-reduces of rank-dependent data (exercises the per-block
+    epochs) with a short wait deadline; exact comparison with the closed form."""
+    dev = torch.device("cuda", device)
+    pa.set_timeout(10.0)
+    base = (torch.arange(n, device=dev, dtype=torch.float32) % 251) - 125.0
+    s = torch.cuda.current_stream(dev)
+    ok = True
+    for it in range(3):
+        x = base * float(r + 1 + it)
+        pa.allreduce(x.data_ptr(), n, s.cuda_stream)
+        torch.cuda.synchronize(dev)
+        want = base * float(W * (W + 1) // 2 + W * it)
+        ok = ok and bool(torch.equal(x, want))
+    st = pa.status()
+    pa.clear_status()
+    torch.cuda.synchronize(dev)
+    return ok and st == 0
+
+
 def init_process_group(world_size: int, rank: int, init_method: str, timeout_s: float = 600.0) -> None:
     if dist.is_initialized():
         return

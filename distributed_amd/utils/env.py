@@ -42,6 +42,10 @@ def get_str(name: str, default: str) -> str:
 #   DAMD_DEBUG_SYNC        0/1                 synchronize + error-check after every engine chunk
 #   DAMD_COMM              rccl | torch | gloo | auto   data-plane communicator on GPU (default auto=rccl;
 #                          gloo stages device tensors through host memory: test/debug only)
+#   DAMD_ALLREDUCE         auto | xgmi | off    per-step gradient all-reduce of the fused trainer: native
+#                          xGMI peer-to-peer two-shot kernel (IPC-mapped peers, self-tested at start; auto
+#                          falls back if any rank cannot use it) or off = the communicator's own (RCCL)
+#   DAMD_PEER_BLOCKS       int                 workgroups of the xGMI all-reduce kernel (64)
 #   DAMD_WATCHDOG_S        float               collective watchdog deadline (0 = off)
 #   DAMD_FAIL_AT           "rank:step[:attempt]"  fault injection (raise inside fit; only in that launcher attempt)
 #   DAMD_CHECK_MIRRORS     int                 mirror-divergence check every N epochs (0=off)

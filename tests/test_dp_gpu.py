@@ -19,7 +19,9 @@ pytestmark = [pytest.mark.gpu, pytest.mark.dist]
 
 
 def _env(out, **kw):
-    e = {"DAMD_DEVICE": "cuda:0", "DAMD_COMM": "gloo", "DAMD_TEST_OUT": str(out), "PYTHONPATH": ROOT,
+    # DAMD_ALLREDUCE=off: the host-staged gloo all-reduce (the xGMI peer kernel has its own
+    # tests in test_peer_allreduce_gpu.py)
+    e = {"DAMD_DEVICE": "cuda:0", "DAMD_COMM": "gloo", "DAMD_ALLREDUCE": "off", "DAMD_TEST_OUT": str(out), "PYTHONPATH": ROOT,
          "OMP_NUM_THREADS": "2", "DAMD_LOG_LEVEL": "WARNING"}
     e.update({k: str(v) for k, v in kw.items()})
     return e
