@@ -32,5 +32,10 @@ hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int spl
 int gemm_stats_tile_rows(int tile);
 // dst[i] += sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order)
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s);
+// bf16 split-K epilogue: out = relu?(sum_s slab[s] + bias + R) (R bf16 [M][ldc], may alias
+// out); stats (optional) = per-column sum / sumsq of the stored pre-ReLU values per block
+// of rows_per_block rows: [ceil(M / rows_per_block)][2][N]
+hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
+                         float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s);
 
 }  // namespace damd

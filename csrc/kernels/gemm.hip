@@ -603,6 +603,7 @@ hipError_t launch_epi(const GemmArgs& a, int epi, int splits, hipStream_t s) {
     case E_ATOMIC: return launch_t<BM, BN, AM, BMo, E_ATOMIC>(a, splits, s);
     case E_SLAB: return launch_t<BM, BN, AM, BMo, E_SLAB>(a, splits, s);
     case E_BF16 | E_STATS: return launch_t<BM, BN, AM, BMo, E_BF16 | E_STATS>(a, splits, s);
+    case E_BIAS | E_BF16 | E_STATS: return launch_t<BM, BN, AM, BMo, E_BIAS | E_BF16 | E_STATS>(a, splits, s);
     case E_BF16 | E_ADD: return launch_t<BM, BN, AM, BMo, E_BF16 | E_ADD>(a, splits, s);
     default: return hipErrorInvalidValue;
   }
@@ -614,15 +615,110 @@ hipError_t launch_tile(const GemmArgs& a, int epi, int splits, int tile, hipStre
   return launch_epi<128, 128, AM, BMo>(a, epi, splits, s);
 }
 
+// dst[i] += sum_s slab[s][i].  Block = 16 float4 columns x 16 split groups: thread
+// (g, e) sums splits g, g+16, ... of element e, then the 16 partials are combined in LDS
+// in fixed order (deterministic), so even a 9k-float4 gradient with 170 splits keeps
+// ~600 blocks streaming the slabs.
+constexpr int RED_E = 16, RED_G = NT / RED_E;
 __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__ slab, int splits, long n4,
                                                      float4* __restrict__ dst) {
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n4; i += (long)gridDim.x * NT) {
-    float4 acc = dst[i];
-    for (int sp = 0; sp < splits; ++sp) {
+  __shared__ float4 part[RED_G][RED_E];
+  const int e = threadIdx.x % RED_E, g = threadIdx.x / RED_E;
+  const long i = blockIdx.x * (long)RED_E + e;
+  float4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (i < n4) {
+#pragma unroll 4
+    for (int sp = g; sp < splits; sp += RED_G) {
       const float4 v = slab[(size_t)sp * n4 + i];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    dst[i] = acc;
+  }
+  part[g][e] = acc;
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 d = dst[i];
+#pragma unroll
+    for (int q = 0; q < RED_G; ++q) {
+      d.x += part[q][e].x; d.y += part[q][e].y; d.z += part[q][e].z; d.w += part[q][e].w;
+    }
+    dst[i] = d;
+  }
+}
+
+// Split-K epilogue for the bf16-output GEMMs (conv fwd, conv dgrad): out[m][n] =
+// relu?( sum_s slab[s][m][n] + bias[n] + R[m][n] ) as bf16, plus per-column sum / sum of
+// squares of the stored (pre-ReLU, bf16-rounded) values per block of `rb` rows
+// (BatchNorm batch statistics: stats[blk][2][N]).  Thread = 8 columns of one row.
+__global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ slab, int S, int M, int N,
+                                                      const float* __restrict__ bias, const uint16_t* R, int relu,
+                                                      float* __restrict__ stats, int rb, uint16_t* out, int ldc) {
+  __shared__ float red[2][NT * 8];
+  const int cg = N / 8, rp = NT / cg;  // column groups, rows per pass
+  const int t = threadIdx.x, g = t % cg, r0 = t / cg;
+  const int n = 8 * g;
+  const long row0 = (long)blockIdx.x * rb, row1 = min((long)M, row0 + rb);
+  float cs[8], cq[8], bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    cs[e] = cq[e] = 0.f;
+    bv[e] = 0.f;
+  }
+  if (bias && r0 < rp) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = bias[n + e];
+  }
+  const size_t plane = (size_t)M * N;
+  if (r0 < rp) {
+    for (long m = row0 + r0; m < row1; m += rp) {
+      float v[8];
+      const float* p = slab + (size_t)m * N + n;
+      float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      for (int sp = 1; sp < S; ++sp) {
+        const float* q = p + sp * plane;
+        a = *reinterpret_cast<const float4*>(q);
+        b = *reinterpret_cast<const float4*>(q + 4);
+        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+      }
+      if (R) {
+        const uint4 r = *reinterpret_cast<const uint4*>(R + (size_t)m * ldc + n);
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[2 * k] += __uint_as_float(w[k] << 16);
+          v[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+        }
+      }
+      uint32_t pk[4];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint16_t h = f2bf(v[e] + bv[e]);
+        const float x = bf2f(h);  // statistics of the stored value
+        cs[e] += x;
+        cq[e] += x * x;
+        const uint16_t o = relu ? f2bf(fmaxf(x, 0.f)) : h;
+        if (e & 1) pk[e >> 1] |= (uint32_t)o << 16;
+        else pk[e >> 1] = o;
+      }
+      *reinterpret_cast<uint4*>(out + (size_t)m * ldc + n) = uint4{pk[0], pk[1], pk[2], pk[3]};
+    }
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][t * 8 + e] = r0 < rp ? cs[e] : 0.f;
+    red[1][t * 8 + e] = r0 < rp ? cq[e] : 0.f;
+  }
+  __syncthreads();
+  for (int c = t; c < N; c += NT) {
+    const int gg = c / 8, e = c % 8;
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < rp; ++q) {
+      a += red[0][(q * cg + gg) * 8 + e];
+      b += red[1][(q * cg + gg) * 8 + e];
+    }
+    stats[(size_t)blockIdx.x * 2 * N + c] = a;
+    stats[(size_t)blockIdx.x * 2 * N + N + c] = b;
   }
 }
 
@@ -631,10 +727,18 @@ __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s) {
   if (n % 4 || splits < 1) return hipErrorInvalidValue;
   const long n4 = n / 4;
-  long g = (n4 + NT - 1) / NT;
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(splitk_reduce_k, dim3((int)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab), splits,
-                     n4, reinterpret_cast<float4*>(dst));
+  const long g = (n4 + RED_E - 1) / RED_E;
+  hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab),
+                     splits, n4, reinterpret_cast<float4*>(dst));
+  return hipGetLastError();
+}
+
+hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
+                         float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s) {
+  if (splits < 1 || N % 8 || N / 8 > NT || ldc % 8 || rows_per_block < 1) return hipErrorInvalidValue;
+  const int grid = (M + rows_per_block - 1) / rows_per_block;
+  hipLaunchKernelGGL(splitk_finish_k, dim3(grid), dim3(NT), 0, s, slab, splits, M, N, bias, R, relu, stats,
+                     rows_per_block, out, ldc);
   return hipGetLastError();
 }
 

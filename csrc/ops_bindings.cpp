@@ -54,6 +54,12 @@ void register_kernel_ops(py::module_& m) {
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
       py::arg("stream"));
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
+  m.def("splitk_finish", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, uintptr_t R, int relu,
+                            uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream) {
+    check(damd::splitk_finish(P_<const float>(slab), splits, M, N, P_<const float>(bias), P_<const uint16_t>(R), relu,
+                              P_<float>(stats), rb, P_<uint16_t>(out), ldc, P_<ihipStream_t>(stream)),
+          "splitk_finish");
+  });
   m.def("splitk_reduce", [](uintptr_t slab, int splits, long n, uintptr_t dst, uintptr_t stream) {
     check(damd::splitk_reduce(P_<const float>(slab), splits, n, P_<float>(dst), P_<ihipStream_t>(stream)),
           "splitk_reduce");

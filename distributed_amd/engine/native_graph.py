@@ -380,7 +380,7 @@ class NativeGraphEngine(Engine):
         self.st_ident = torch.cat([torch.zeros(1, 1), torch.ones(1, 1), torch.ones(1, 1), torch.zeros(1, 1)])
         self._ident_cache = {}
         maxM_C = 0
-        ws = 0  # fp32 weight-gradient split-K slabs, shared by every wgrad GEMM (serial on one stream)
+        ws = 0  # fp32 split-K slabs, shared by every split GEMM (they run in order on one stream)
         for nd in self.nodes:
             if nd.attrs.get("dead"):
                 continue
@@ -395,10 +395,11 @@ class NativeGraphEngine(Engine):
                 if cin != cin0:
                     nd.attrs["w_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.bfloat16, device=dev)
                     nd.attrs["dw_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.float32, device=dev)
+                xshape, wshape = nd.inputs[0].root().shape, (kh, kw, cin, cout)
+                fplan = H.conv_fwd_plan(xshape, wshape, l.strides, l.padding)
+                ws = max(ws, fplan["ws"], H.conv_dgrad_plan(xshape, wshape, l.strides, l.padding)["ws"])
                 if nd.attrs.get("stats"):
-                    M = int(np.prod(nd.out.shape[:3]))
-                    rows = H.tile_rows(H.pick_tile(cout))
-                    nd.attrs["stats_buf"] = torch.zeros(-(-M // rows), 2, cout, device=dev)
+                    nd.attrs["stats_buf"] = torch.zeros(fplan["stats_T"], 2, cout, device=dev)
                 if getattr(l.activation, "__name__", "linear") == "relu":
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
             elif k == "BatchNormalization":
@@ -429,8 +430,8 @@ class NativeGraphEngine(Engine):
         self.scratch = torch.zeros(big, dtype=torch.bfloat16, device=dev)
         self.scratch2 = torch.zeros(big, dtype=torch.bfloat16, device=dev)
         nbytes += big * 4
-        self.wgrad_ws = torch.zeros(max(ws, 4), dtype=torch.float32, device=dev)
-        nbytes += self.wgrad_ws.numel() * 4
+        self.gemm_ws = torch.zeros(max(ws, 4), dtype=torch.float32, device=dev)
+        nbytes += self.gemm_ws.numel() * 4
         self.act_bytes = nbytes
 
     # --- gradient buckets (all-reduce overlapped with the rest of backward) ------------------
@@ -648,7 +649,7 @@ class NativeGraphEngine(Engine):
         bias = self.views[id(l.bias)] if l.use_bias else None
         relu = getattr(l.activation, "__name__", "linear") == "relu"
         H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
-                   stats=nd.attrs.get("stats_buf"))
+                   stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
 
     def _fwd_BatchNormalization(self, nd):
         l = nd.layer
@@ -736,16 +737,16 @@ class NativeGraphEngine(Engine):
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
             dwp.zero_()
-            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=self.wgrad_ws)
+            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=self.gemm_ws)
             kh, kw, cin, cout = l.kernel.shape
             H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
         else:
-            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=self.wgrad_ws)
+            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=self.gemm_ws)
         if xt.needs_grad:
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written
             xt.written = True
-            H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc)
+            H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
 
     def _bn_backward(self, bn, dy, ymask, relu, dz_out=None):
         """BatchNorm backward of node ``bn`` for upstream gradient dy (masked by
@@ -859,11 +860,11 @@ class NativeGraphEngine(Engine):
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
             dwp.zero_()
-            H.dense_wgrad(x2, dy, dwp, workspace=self.wgrad_ws)
+            H.dense_wgrad(x2, dy, dwp, workspace=self.gemm_ws)
             kin = l.kernel.shape[0]
             H.unpad_add(dwp, 1, kin, units, kin, dwp.shape[1], self.gviews[id(l.kernel)])
         else:
-            H.dense_wgrad(x2, dy, self.gviews[id(l.kernel)], workspace=self.wgrad_ws)
+            H.dense_wgrad(x2, dy, self.gviews[id(l.kernel)], workspace=self.gemm_ws)
         if xt.needs_grad:
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written

@@ -102,6 +102,30 @@ def wgrad_plan(M: int, N: int, K: int) -> Tuple[int, int, int]:
     return t, -(-K // kps), kps
 
 
+# bf16-output GEMMs (conv fwd / dgrad) whose tile count leaves CUs idle are split over K
+# into fp32 slabs; splitk_finish then applies the epilogue (bias, residual, ReLU, BN
+# statistics per FINISH_RB rows, bf16 store)
+SPLIT_MIN_TILES = 320
+SPLIT_TARGET_WG = 384
+FINISH_RB = 16
+
+
+def split_plan(M: int, N: int, K: int, tile: int) -> Tuple[int, int]:
+    """(splits, k_per_split) for a bf16-output GEMM; splits == 1: the fused epilogue."""
+    bm, bn = (256, 64) if tile == 1 else (128, 128)
+    tiles = -(-M // bm) * -(-N // bn)
+    kfull = -(-K // BK) * BK
+    if tiles >= SPLIT_MIN_TILES:
+        return 1, kfull
+    cap = max(1, WGRAD_SLAB_MAX // (M * N * 4))
+    splits = max(1, min(-(-SPLIT_TARGET_WG // tiles), K // (BK * 8), cap))
+    if splits == 1:
+        return 1, kfull
+    kps = -(-K // splits)
+    kps = -(-kps // BK) * BK
+    return -(-K // kps), kps
+
+
 def wgrad_workspace_elems(M: int, N: int, K: int) -> int:
     _, splits, _ = wgrad_plan(M, N, K)
     return splits * M * N if splits > 1 else 0
@@ -184,20 +208,67 @@ def conv_geo(x_shape, w_shape, strides, padding):
     return n, h, w_, cin, ho, wo, kh, kw, strides[0], pad, cout
 
 
-def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, stats=None):
-    """out [N,Ho,Wo,Cout] = conv(x [N,H,W,Cin], w [KH,KW,Cin,Cout]); bf16 in/out."""
+def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
+    """Launch plan of conv_fwd: tile, split-K, number of BN-statistics partials and the
+    fp32 workspace it needs (0 when not split)."""
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
+    M, N, K = n * ho * wo, cout, kh * kw * cin
+    t = pick_tile(N)
+    splits, kps = split_plan(M, N, K, t)
+    return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,
+            "stats_T": -(-M // (FINISH_RB if splits > 1 else tile_rows(t))),
+            "ws": splits * M * N if splits > 1 else 0}
+
+
+def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, stats=None,
+             workspace: Optional[torch.Tensor] = None):
+    """out [N,Ho,Wo,Cout] = conv(x [N,H,W,Cin], w [KH,KW,Cin,Cout]); bf16 in/out.  stats
+    (BN batch statistics partials) must have conv_fwd_plan(...)["stats_T"] rows."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, w.shape, strides, padding)
     _chk(x, torch.bfloat16, "x")
     _chk(w, torch.bfloat16, "w")
     if cin % 8 or cout % 8:
         raise ValueError("conv_fwd: Cin and Cout must be multiples of 8 (pad the channels)")
     assert tuple(out.shape) == (n, ho, wo, cout)
-    epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | (E_STATS if stats is not None else 0)
-    gemm(x, w, out, amode=A_IM2COL, bmode=B_NC, M=n * ho * wo, N=cout, K=kh * kw * cin, ldb=cout, ldc=cout, epi=epi,
-         bias=bias, stats=stats, geo=(h, wd, cin, ho, wo, kh, kw, s, pad))
+    plan = conv_fwd_plan(x.shape, w.shape, strides, padding)
+    M, K = plan["M"], plan["K"]
+    if stats is not None and stats.shape[0] != plan["stats_T"]:
+        raise ValueError(f"conv_fwd: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
+    geo = (h, wd, cin, ho, wo, kh, kw, s, pad)
+    if plan["splits"] == 1:
+        epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | \
+            (E_STATS if stats is not None else 0)
+        gemm(x, w, out, amode=A_IM2COL, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=epi, bias=bias,
+             stats=stats, geo=geo, tile=plan["tile"])
+        return
+    ws = _workspace(workspace, plan["ws"], x.device)
+    gemm(x, w, ws, amode=A_IM2COL, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
+         splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo)
+    _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), _ptr(stats), FINISH_RB,
+                       _ptr(out), cout, stream_handle())
 
 
-def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False):
+def _workspace(ws, need, device):
+    if need == 0:
+        return None
+    if ws is None:
+        return torch.empty(need, device=device)
+    if ws.dtype != torch.float32 or ws.numel() < need:
+        raise ValueError(f"split-K GEMM needs an fp32 workspace of {need} elements")
+    return ws
+
+
+def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx_shape, w_shape, strides, padding)
+    M, N, K = n * h * wd, cin, kh * kw * cout
+    t = pick_tile(N)
+    splits, kps = split_plan(M, N, K, t)
+    return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,
+            "ws": splits * M * N if splits > 1 else 0}
+
+
+def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
+               workspace: Optional[torch.Tensor] = None):
     """dx [N,H,W,Cin] (+)= backprop-input of dy [N,Ho,Wo,Cout] through w."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx.shape, w.shape, strides, padding)
     if s not in (1, 2):
@@ -207,9 +278,19 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False):
     _chk(dx, torch.bfloat16, "dx")
     if cin % 8 or cout % 8:
         raise ValueError("conv_dgrad: Cin and Cout must be multiples of 8")
-    epi = E_BF16 | (E_ADD if accumulate else 0)
-    gemm(dy, w, dx, amode=A_DGRAD, bmode=B_KC, M=n * h * wd, N=cin, K=kh * kw * cout, ldc=cin, epi=epi, kc=cout,
-         geo=(h, wd, cout, ho, wo, kh, kw, s, pad), R=dx if accumulate else None)
+    plan = conv_dgrad_plan(dx.shape, w.shape, strides, padding)
+    M, K = plan["M"], plan["K"]
+    geo = (h, wd, cout, ho, wo, kh, kw, s, pad)
+    if plan["splits"] == 1:
+        epi = E_BF16 | (E_ADD if accumulate else 0)
+        gemm(dy, w, dx, amode=A_DGRAD, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=epi, kc=cout, geo=geo,
+             R=dx if accumulate else None, tile=plan["tile"])
+        return
+    ws = _workspace(workspace, plan["ws"], dx.device)
+    gemm(dy, w, ws, amode=A_DGRAD, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_SLAB, kc=cout, geo=geo,
+         splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"])
+    _C().splitk_finish(_ptr(ws), plan["splits"], M, cin, 0, _ptr(dx) if accumulate else 0, 0, 0, FINISH_RB,
+                       _ptr(dx), cin, stream_handle())
 
 
 def conv_wgrad_workspace_elems(x_shape, w_shape, strides=(1, 1), padding="valid") -> int:

@@ -109,13 +109,45 @@ def test_conv_bias_relu_and_stats(H):
     H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", bias=b, relu=True)
     close(out, y.relu(), 1e-2, 4e-3)
     # BN statistics in the epilogue: per-M-tile partial column sums of the stored values
-    rows = H.tile_rows(H.pick_tile(cout))
-    T = -(-(n * h * h) // rows)
+    T = H.conv_fwd_plan(x.shape, w.shape, (1, 1), "same")["stats_T"]
     st = torch.zeros(T, 2, cout, device=dev)
     H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", stats=st)
     yb = out.float().reshape(-1, cout)
     close(st[:, 0].sum(0), yb.sum(0), 1e-4, 1e-5)
     close(st[:, 1].sum(0), (yb * yb).sum(0), 1e-4, 1e-5)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_conv_split_k_epilogues(H, monkeypatch, split):
+    """Both bf16-output GEMM paths: fused epilogue (no split) and split-K slabs + the
+    finishing kernel (bias / ReLU / BN statistics / dgrad accumulation)."""
+    monkeypatch.setattr(H, "SPLIT_MIN_TILES", 1 << 30 if split else 0)
+    n, h, cin, cout = 2, 7, 128, 64
+    plan = H.conv_fwd_plan((n, h, h, cin), (3, 3, cin, cout), (1, 1), "same")
+    assert (plan["splits"] > 1) == split
+    x = rb(rnd(n, h, h, cin, seed=40))
+    w = rb(rnd(3, 3, cin, cout, scale=0.1, seed=41))
+    b = rnd(cout, seed=42)
+    y = ref.conv2d(x, w, b, (1, 1), "same")
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(plan["stats_T"], 2, cout, device=dev)
+    H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", bias=b, stats=st)
+    close(out, y, 1e-2, 4e-3)
+    yb = out.float().reshape(-1, cout)
+    close(st[:, 0].sum(0), yb.sum(0), 1e-4, 1e-5)
+    close(st[:, 1].sum(0), (yb * yb).sum(0), 1e-4, 1e-5)
+    H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", bias=b, relu=True)
+    close(out, y.relu(), 1e-2, 4e-3)
+    # dgrad (+accumulate) through the same two paths (dx has Cin = 128 columns)
+    dy = rb(rnd(n, h, h, cout, seed=43)).requires_grad_(False)
+    xx = x.clone().requires_grad_(True)
+    gx, = torch.autograd.grad(ref.conv2d(xx, w, None, (1, 1), "same"), (xx,), dy)
+    assert (H.conv_dgrad_plan(x.shape, w.shape, (1, 1), "same")["splits"] > 1) == split
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (1, 1), "same")
+    close(dx, gx, 1e-2, 4e-3)
+    H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (1, 1), "same", accumulate=True)
+    close(dx, 2 * gx, 1e-2, 8e-3)
 
 
 @pytest.mark.parametrize("relu,res", [(False, None), (True, None), (True, "raw"), (True, "bn")])
