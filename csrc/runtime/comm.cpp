@@ -85,18 +85,24 @@ void RcclComm::abort() {
 }
 
 bool stream_wait_with_deadline(hipStream_t st, double timeout_s, RcclComm* comm) {
+  // No deadline: the runtime's own wait returns as soon as the stream drains (a sleeping
+  // poll overshoots a ~30 us training step by up to its sleep quantum).
+  if (timeout_s <= 0) {
+    HIP_CHECK(hipStreamSynchronize(st));
+    return true;
+  }
   auto t0 = std::chrono::steady_clock::now();
-  int spins = 0;
   for (;;) {
     hipError_t q = hipStreamQuery(st);
     if (q == hipSuccess) return true;
     if (q != hipErrorNotReady) HIP_CHECK(q);
     double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (timeout_s > 0 && el > timeout_s) {
+    if (el > timeout_s) {
       if (comm) comm->abort();
       return false;
     }
-    if (++spins > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    // busy-poll the first 2 ms (step-sized waits), then back off to 20 us sleeps
+    if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }
 
