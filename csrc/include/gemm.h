@@ -4,7 +4,10 @@
 
 namespace damd {
 
-enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4 };
+enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4,
+                 // glds-staged BK=64 conv kernels (csrc/kernels/conv_gemm.hip): gathered
+                 // channel count % 64 == 0; A_DGRAD64 stride 1 only
+                 A_CONV64 = 5, A_DGRAD64 = 6 };
 enum GemmBMode { B_NC = 0, B_KC = 1 };
 // E_SLAB: split-K partial of split z stored (plain fp32 stores) to C + z * M * ldc; a
 // deterministic splitk_reduce then adds the slabs into the destination in fixed order.
@@ -29,6 +32,8 @@ struct GemmArgs {
 
 // tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)
 hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int splits, int tile, hipStream_t s);
+// conv_gemm.hip: A_CONV64 (with B_NC weights) / A_DGRAD64 (with B_KC weights)
+hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, int tile, hipStream_t s);
 int gemm_stats_tile_rows(int tile);
 // dst[i] += sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order)
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s);

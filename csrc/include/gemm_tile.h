@@ -1,0 +1,169 @@
+// Device-side building blocks shared by the MFMA GEMM kernels (csrc/kernels/gemm.hip,
+// csrc/kernels/conv_gemm.hip): LDS image layouts, fragment reads and the common epilogue.
+//
+// Output layout: the MFMAs are issued with swapped operands (C^T = B^T A^T), so after a
+// 16x16x32 MFMA lane l holds C[row 16i + (l & 15)][cols 16j + 4(l >> 4) .. +3] of the
+// wave's 64x64 block -- 4 consecutive columns of one row: 8/16-byte epilogue stores.
+#pragma once
+#include "damd_common.h"
+#include "gemm.h"
+
+namespace damd {
+namespace tile {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+// gfx950 transpose read ds_read_b64_tr_b16 (lane gets 4 bf16 of one column)
+__device__ __forceinline__ s16x4 ds_tr16(const void* lds_byte_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)((__attribute__((address_space(3))) char*)(
+          (uintptr_t)lds_byte_ptr)));
+}
+
+// MC image: [k rows][COLS] bf16 (mn-contiguous operand); the 16-byte chunk ch of row r is
+// stored at chunk ch ^ mc_swz(r).  The swizzle depends on r mod 32 only (k-steps of 32
+// rows are images of their own) and is an involution per row, so a lane-linear
+// global->LDS DMA fills it by reading source chunk (slot ^ mc_swz(r)).
+template <int COLS>
+__device__ __forceinline__ int mc_swz(int r) {
+  if constexpr (COLS == 64) return (r & 3) ^ ((r >> 1) & 7);
+  else return (((r & 3) << 2) ^ ((r >> 2) & 3)) & (COLS / 8 - 1);
+}
+template <int COLS>
+__device__ __forceinline__ int mc_off(int r, int ch) {
+  return r * (COLS * 2) + 16 * (ch ^ mc_swz<COLS>(r));
+}
+// fragment of columns c0..c0+15, k rows 0..31 of an MC image (two transpose reads)
+template <int COLS>
+__device__ __forceinline__ bf16x8 frag_mc(const char* img, int c0, int lane) {
+  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  int ch = (c0 >> 3) + (p >> 1);
+  s16x4 lo = ds_tr16(img + mc_off<COLS>(8 * g + q, ch) + 8 * (p & 1));
+  s16x4 hi = ds_tr16(img + mc_off<COLS>(8 * g + 4 + q, ch) + 8 * (p & 1));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// ---- epilogue --------------------------------------------------------------------------
+// acc[i][j]: the wave's 64x64 block (wave grid position wm, wn) of the BMxBN tile at
+// (m0, n0), M-tile index tm.  red: >= 2*4*64 floats of LDS, free to use (all staging reads
+// done).  Flags (gemm.h): +bias[n], +R[m][n] (bf16), BatchNorm statistics of the stored
+// pre-ReLU values per (M-tile, split), ReLU, and bf16 / fp32 / atomic / slab stores.
+template <int BM, int BN, int EPI>
+__device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], int m0, int n0, int tm, int wm,
+                                         int wn, int wave, int lane, float* red) {
+  constexpr int WN = BN / 64, WM = 4 / WN;
+  float csum[4][4], csq[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) csum[j][e] = csq[j][e] = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+    const bool mok = m < a.M;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+      const bool ok = mok && n < a.N;
+      f32x4 v = acc[i][j];
+      if constexpr (EPI & E_BIAS) {
+        if (n < a.N) {
+          float4 b = *reinterpret_cast<const float4*>(a.bias + n);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+      }
+      if constexpr (EPI & E_ADD) {
+        if (ok) {
+          const uint2 r = *reinterpret_cast<const uint2*>((const uint16_t*)a.R + (size_t)m * a.ldc + n);
+          v[0] += __uint_as_float(r.x << 16);
+          v[1] += __uint_as_float(r.x & 0xffff0000u);
+          v[2] += __uint_as_float(r.y << 16);
+          v[3] += __uint_as_float(r.y & 0xffff0000u);
+        }
+      }
+      if constexpr (EPI & E_STATS) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = ok ? v[e] : 0.f;
+          if constexpr (EPI & E_BF16) x = bf2f(f2bf(x));  // statistics of the stored values
+          csum[j][e] += x;
+          csq[j][e] += x * x;
+        }
+      }
+      if constexpr (EPI & E_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (!ok) continue;
+      if constexpr (EPI & E_SLAB) {
+        float* c = (float*)a.C + ((size_t)blockIdx.z * a.M + m) * a.ldc + n;
+        *reinterpret_cast<float4*>(c) = float4{v[0], v[1], v[2], v[3]};
+      } else if constexpr (EPI & E_ATOMIC) {
+        float* c = (float*)a.C + (size_t)m * a.ldc + n;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) atomicAdd(c + e, v[e]);
+      } else if constexpr (EPI & E_BF16) {
+        uint2 pk;
+        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>((uint16_t*)a.C + (size_t)m * a.ldc + n) = pk;
+      } else {
+        *reinterpret_cast<float4*>((float*)a.C + (size_t)m * a.ldc + n) = float4{v[0], v[1], v[2], v[3]};
+      }
+    }
+  }
+  if constexpr (EPI & E_STATS) {
+    // reduce over the 16 rows held by lanes l&15 (xor 1,2,4,8), then over the wave grid's
+    // M direction through LDS; one partial per column per M-tile: stats[tm][z][2][N]
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int s = 1; s < 16; s <<= 1) {
+          csum[j][e] += __shfl_xor(csum[j][e], s);
+          csq[j][e] += __shfl_xor(csq[j][e], s);
+        }
+      }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int c = j * 16 + 4 * (lane >> 4) + e;  // column within the wave's 64
+          red[(0 * 4 + wave) * 64 + c] = csum[j][e];
+          red[(1 * 4 + wave) * 64 + c] = csq[j][e];
+        }
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < BN) {
+      const int wnn = t / 64, c = t % 64;
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        s += red[(0 * 4 + w * WN + wnn) * 64 + c];
+        q += red[(1 * 4 + w * WN + wnn) * 64 + c];
+      }
+      const int n = n0 + t;
+      if (n < a.N) {
+        float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
+        st[n] = s;
+        st[a.N + n] = q;
+      }
+    }
+  }
+}
+
+// XCD-aware tile order: consecutive workgroups are dispatched round-robin over the 8
+// XCDs; remap (bijectively, any tile count) so that the N-tiles of one M-panel -- which
+// share the A rows -- run on the same XCD (same L2).  Returns the linear tile index.
+__device__ __forceinline__ int xcd_tile(int lin, int tiles) {
+  const int q = tiles >> 3, r = tiles & 7, xcd = lin & 7, idx = lin >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+}  // namespace tile
+}  // namespace damd

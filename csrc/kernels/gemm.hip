@@ -30,6 +30,7 @@
 // M-block (BatchNorm batch statistics without re-reading the activation).
 #include "damd_common.h"
 #include "gemm.h"
+#include "gemm_tile.h"
 
 namespace damd {
 namespace {
@@ -37,24 +38,13 @@ namespace {
 constexpr int BK = 32;
 constexpr int NT = 256;
 
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ s16x4 ds_tr16(const void* lds_byte_ptr) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)((__attribute__((address_space(3))) char*)(
-          (uintptr_t)lds_byte_ptr)));
-}
+using tile::ds_tr16;
+using tile::frag_mc;
+using tile::mc_off;
 
 // ---- LDS images --------------------------------------------------------------------
 // KC image: [rows][32] bf16, 64-B rows; 16-B chunk c of row r stored at chunk c^((r>>1)&3).
 __device__ __forceinline__ int kc_off(int r, int c) { return r * 64 + 16 * (c ^ ((r >> 1) & 3)); }
-// MC image: [32][COLS] bf16; chunk (8 cols) ch of row r stored at ch ^ f(r).
-template <int COLS>
-__device__ __forceinline__ int mc_off(int r, int ch) {
-  if constexpr (COLS == 64) return r * 128 + 16 * (ch ^ (((r & 3)) ^ ((r >> 1) & 7)));
-  else return r * (COLS * 2) + 16 * (ch ^ ((((r & 3) << 2) ^ ((r >> 2) & 3)) & (COLS / 8 - 1)));
-}
-
 // ---- per-thread operand loaders ----------------------------------------------------
 // Each loader owns CH chunks (16 B each) of the tile; `load(kt)` fills registers for
 // k-tile starting at k0, `store(lds)` writes them into the LDS image.
@@ -396,18 +386,6 @@ template <int MODE> struct IsKC { static constexpr bool v = (MODE == A_KC || MOD
 __device__ __forceinline__ bf16x8 frag_kc(const char* img, int r0, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + kc_off(r0 + (lane & 15), lane >> 4));
 }
-// same fragment from an MC image ([32][COLS], column c0 .. c0+15) via two transpose reads
-template <int COLS>
-__device__ __forceinline__ bf16x8 frag_mc(const char* img, int c0, int lane) {
-  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  int ch = (c0 >> 3) + (p >> 1);
-  s16x4 lo = ds_tr16(img + mc_off<COLS>(8 * g + q, ch) + 8 * (p & 1));
-  s16x4 hi = ds_tr16(img + mc_off<COLS>(8 * g + 4 + q, ch) + 8 * (p & 1));
-  typedef short s16x8 __attribute__((ext_vector_type(8)));
-  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8, v);
-}
-
 template <int BM, int BN, int AMODE, int BMODE, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs a) {
   constexpr int WN = BN / 64, WM = 4 / WN;  // wave grid (each wave 64x64)
@@ -481,107 +459,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs a) {
     lds_barrier();
   }
 
-  // ---- epilogue: lane holds C[m = rowbase + (l&15)][n = colbase + 4(l>>4) + j] ----
-  float csum[4][4], csq[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) csum[j][e] = csq[j][e] = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + (lane & 15);
-    const bool mok = m < a.M;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
-      const bool ok = mok && n < a.N;
-      f32x4 v = acc[i][j];
-      if constexpr (EPI & E_BIAS) {
-        if (n < a.N) {
-          float4 b = *reinterpret_cast<const float4*>(a.bias + n);
-          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-        }
-      }
-      if constexpr (EPI & E_ADD) {
-        if (ok) {
-          const uint2 r = *reinterpret_cast<const uint2*>((const uint16_t*)a.R + (size_t)m * a.ldc + n);
-          v[0] += __uint_as_float(r.x << 16);
-          v[1] += __uint_as_float(r.x & 0xffff0000u);
-          v[2] += __uint_as_float(r.y << 16);
-          v[3] += __uint_as_float(r.y & 0xffff0000u);
-        }
-      }
-      if constexpr (EPI & E_STATS) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float x = ok ? v[e] : 0.f;
-          if constexpr (EPI & E_BF16) x = bf2f(f2bf(x));  // statistics of the stored values
-          csum[j][e] += x;
-          csq[j][e] += x * x;
-        }
-      }
-      if constexpr (EPI & E_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      if (!ok) continue;
-      if constexpr (EPI & E_SLAB) {
-        float* c = (float*)a.C + ((size_t)blockIdx.z * a.M + m) * a.ldc + n;
-        *reinterpret_cast<float4*>(c) = float4{v[0], v[1], v[2], v[3]};
-      } else if constexpr (EPI & E_ATOMIC) {
-        float* c = (float*)a.C + (size_t)m * a.ldc + n;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) atomicAdd(c + e, v[e]);
-      } else if constexpr (EPI & E_BF16) {
-        uint2 pk;
-        pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>((uint16_t*)a.C + (size_t)m * a.ldc + n) = pk;
-      } else {
-        *reinterpret_cast<float4*>((float*)a.C + (size_t)m * a.ldc + n) = float4{v[0], v[1], v[2], v[3]};
-      }
-    }
-  }
-  if constexpr (EPI & E_STATS) {
-    // reduce over the 16 rows held by lanes l&15 (xor 1,2,4,8), then over the wave grid's
-    // M direction through LDS; one partial per column per M-tile: stats[tm][2][N]
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int s = 1; s < 16; s <<= 1) {
-          csum[j][e] += __shfl_xor(csum[j][e], s);
-          csq[j][e] += __shfl_xor(csq[j][e], s);
-        }
-      }
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int c = j * 16 + 4 * (lane >> 4) + e;  // column within the wave's 64
-          red[0][wave][c] = csum[j][e];
-          red[1][wave][c] = csq[j][e];
-        }
-    }
-    __syncthreads();
-    if (t < BN) {
-      const int wnn = t / 64, c = t % 64;
-      float s = 0.f, q = 0.f;
-#pragma unroll
-      for (int w = 0; w < WM; ++w) {
-        s += red[0][w * WN + wnn][c];
-        q += red[1][w * WN + wnn][c];
-      }
-      const int n = n0 + t;
-      if (n < a.N) {
-        float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
-        st[n] = s;
-        st[a.N + n] = q;
-      }
-    }
-  }
+  tile::epilogue<BM, BN, EPI>(a, acc, m0, n0, tm, wm, wn, wave, lane, &red[0][0][0]);
 }
 
 template <int BM, int BN, int AM, int BMo, int EPI>
@@ -748,6 +626,10 @@ hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int spl
   if (splits < 1) return hipErrorInvalidValue;
   if ((epi & E_ATOMIC) && (epi & ~E_ATOMIC)) return hipErrorInvalidValue;
   if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
+  if (amode == A_CONV64 || amode == A_DGRAD64) {
+    if (bmode != (amode == A_CONV64 ? B_NC : B_KC)) return hipErrorInvalidValue;
+    return conv_gemm_launch(a, amode, epi, splits, tile, s);
+  }
   const int key = amode * 2 + bmode;
   switch (key) {
     case A_KC * 2 + B_NC: return launch_tile<A_KC, B_NC>(a, epi, splits, tile, s);

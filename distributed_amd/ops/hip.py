@@ -20,10 +20,20 @@ import torch
 
 from ..native import require_C
 
-A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD = range(5)
+A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64 = range(7)
 B_NC, B_KC = 0, 1
 E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB = 1, 2, 4, 8, 16, 32, 64
 BK = 32
+BK64 = 64  # k-step of the LDS-DMA conv kernels (csrc/kernels/conv_gemm.hip)
+
+
+def use_glds(gathered_channels: int) -> bool:
+    """The LDS-DMA conv kernels take a conv whose gathered tensor has C % 64 == 0 (one
+    filter tap x 64 channels per k-step); DAMD_CONV_GLDS=0 forces the register-staged
+    kernel (A/B comparisons)."""
+    import os
+
+    return gathered_channels % BK64 == 0 and os.environ.get("DAMD_CONV_GLDS", "1") != "0"
 
 
 def _C():
@@ -110,11 +120,12 @@ SPLIT_TARGET_WG = 384
 FINISH_RB = 16
 
 
-def split_plan(M: int, N: int, K: int, tile: int) -> Tuple[int, int]:
-    """(splits, k_per_split) for a bf16-output GEMM; splits == 1: the fused epilogue."""
+def split_plan(M: int, N: int, K: int, tile: int, bk: int = BK) -> Tuple[int, int]:
+    """(splits, k_per_split) for a bf16-output GEMM; splits == 1: the fused epilogue.
+    k_per_split is a multiple of the kernel's k-step ``bk``."""
     bm, bn = (256, 64) if tile == 1 else (128, 128)
     tiles = -(-M // bm) * -(-N // bn)
-    kfull = -(-K // BK) * BK
+    kfull = -(-K // bk) * bk
     if tiles >= SPLIT_MIN_TILES:
         return 1, kfull
     cap = max(1, WGRAD_SLAB_MAX // (M * N * 4))
@@ -122,7 +133,7 @@ def split_plan(M: int, N: int, K: int, tile: int) -> Tuple[int, int]:
     if splits == 1:
         return 1, kfull
     kps = -(-K // splits)
-    kps = -(-kps // BK) * BK
+    kps = -(-kps // bk) * bk
     return -(-K // kps), kps
 
 
@@ -214,8 +225,10 @@ def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
     M, N, K = n * ho * wo, cout, kh * kw * cin
     t = pick_tile(N)
-    splits, kps = split_plan(M, N, K, t)
+    glds = use_glds(cin)
+    splits, kps = split_plan(M, N, K, t, BK64 if glds else BK)
     return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,
+            "amode": A_CONV64 if glds else A_IM2COL,
             "stats_T": -(-M // (FINISH_RB if splits > 1 else tile_rows(t))),
             "ws": splits * M * N if splits > 1 else 0}
 
@@ -238,11 +251,11 @@ def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, 
     if plan["splits"] == 1:
         epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | \
             (E_STATS if stats is not None else 0)
-        gemm(x, w, out, amode=A_IM2COL, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=epi, bias=bias,
-             stats=stats, geo=geo, tile=plan["tile"])
+        gemm(x, w, out, amode=plan["amode"], bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=epi,
+             bias=bias, stats=stats, geo=geo, tile=plan["tile"])
         return
     ws = _workspace(workspace, plan["ws"], x.device)
-    gemm(x, w, ws, amode=A_IM2COL, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
+    gemm(x, w, ws, amode=plan["amode"], bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo)
     _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), _ptr(stats), FINISH_RB,
                        _ptr(out), cout, stream_handle())
@@ -262,8 +275,10 @@ def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx_shape, w_shape, strides, padding)
     M, N, K = n * h * wd, cin, kh * kw * cout
     t = pick_tile(N)
-    splits, kps = split_plan(M, N, K, t)
+    glds = s == 1 and use_glds(cout)
+    splits, kps = split_plan(M, N, K, t, BK64 if glds else BK)
     return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,
+            "amode": A_DGRAD64 if glds else A_DGRAD,
             "ws": splits * M * N if splits > 1 else 0}
 
 
@@ -283,11 +298,11 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
     geo = (h, wd, cout, ho, wo, kh, kw, s, pad)
     if plan["splits"] == 1:
         epi = E_BF16 | (E_ADD if accumulate else 0)
-        gemm(dy, w, dx, amode=A_DGRAD, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=epi, kc=cout, geo=geo,
+        gemm(dy, w, dx, amode=plan["amode"], bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=epi, kc=cout, geo=geo,
              R=dx if accumulate else None, tile=plan["tile"])
         return
     ws = _workspace(workspace, plan["ws"], dx.device)
-    gemm(dy, w, ws, amode=A_DGRAD, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_SLAB, kc=cout, geo=geo,
+    gemm(dy, w, ws, amode=plan["amode"], bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_SLAB, kc=cout, geo=geo,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"])
     _C().splitk_finish(_ptr(ws), plan["splits"], M, cin, 0, _ptr(dx) if accumulate else 0, 0, 0, FINISH_RB,
                        _ptr(dx), cin, stream_handle())

@@ -1,6 +1,8 @@
 """Micro-benchmark of the generic-path MFMA kernels on the ResNet-18 conv shapes
-(batch 64, bf16): our implicit-GEMM fwd / dgrad / wgrad vs torch's (MIOpen) conv in
-channels_last bf16, reported in TFLOP/s.  Usage: python scripts/bench_gemm.py [B]"""
+(batch 64, bf16): our implicit-GEMM fwd / dgrad / wgrad -- the LDS-DMA kernels
+(conv_gemm.hip) where they apply and the register-staged ones (gemm.hip,
+DAMD_CONV_GLDS=0) -- vs torch's (MIOpen) conv in channels_last bf16, in ms / TFLOP/s.
+Usage: python scripts/bench_gemm.py [B]"""
 import os
 import sys
 import time
@@ -20,10 +22,14 @@ SHAPES = [  # h, cin, cout, k, s
     (56, 64, 128, 1, 2),
     (28, 128, 128, 3, 1),
     (28, 128, 256, 3, 2),
+    (28, 128, 256, 1, 2),
     (14, 256, 256, 3, 1),
     (14, 256, 512, 3, 2),
+    (14, 256, 512, 1, 2),
     (7, 512, 512, 3, 1),
 ]
+# instances of each shape in one ResNet-18 step (for the weighted sum)
+COUNT = [1, 4, 1, 1, 3, 1, 1, 3, 1, 1, 3]
 
 
 def timeit(fn, n=20):
@@ -36,9 +42,20 @@ def timeit(fn, n=20):
     return (time.perf_counter() - t) / n
 
 
-print(f"B={B}  (ms / TFLOP/s)   ours: fwd dgrad wgrad | torch channels_last: fwd dgrad wgrad")
-tot = [0.0, 0.0]
-for h, cin, cout, k, s in SHAPES:
+def ours(x, w, y, dy, dx, dw, s, pad, glds):
+    os.environ["DAMD_CONV_GLDS"] = "1" if glds else "0"
+    ws = torch.empty(max(H.conv_fwd_plan(x.shape, w.shape, (s, s), pad)["ws"],
+                         H.conv_dgrad_plan(x.shape, w.shape, (s, s), pad)["ws"],
+                         H.conv_wgrad_workspace_elems(x.shape, w.shape, (s, s), pad), 4), device=dev)
+    tf = timeit(lambda: H.conv_fwd(x, w, y, (s, s), pad, workspace=ws))
+    td = timeit(lambda: H.conv_dgrad(dy, w, dx, (s, s), pad, workspace=ws)) if x.shape[1] != 224 else float("nan")
+    tw = timeit(lambda: H.conv_wgrad(x, dy, dw, (s, s), pad, workspace=ws))
+    return [tf, td, tw]
+
+
+print(f"B={B}  (ms / TFLOP/s)  fwd dgrad wgrad:  glds | register-staged | torch channels_last", flush=True)
+tot = {"glds": 0.0, "reg": 0.0, "torch": 0.0}
+for (h, cin, cout, k, s), cnt in zip(SHAPES, COUNT):
     pad = "same" if k > 1 else "valid"
     ho, p = H.conv_out(h, k, s, pad)
     x = torch.randn(B, h, h, cin, device=dev).bfloat16()
@@ -48,10 +65,8 @@ for h, cin, cout, k, s in SHAPES:
     dx = torch.empty_like(x)
     dw = torch.zeros(k, k, cin, cout, device=dev)
     flop = 2.0 * B * ho * ho * cout * k * k * cin
-    tf = timeit(lambda: H.conv_fwd(x, w, y, (s, s), pad))
-    td = timeit(lambda: H.conv_dgrad(dy, w, dx, (s, s), pad)) if cin % 8 == 0 and h != 224 else float("nan")
-    tw = timeit(lambda: H.conv_wgrad(x, dy, dw, (s, s), pad))
-    # torch reference (NCHW logical, channels_last memory)
+    g = ours(x, w, y, dy, dx, dw, s, pad, True)
+    r = ours(x, w, y, dy, dx, dw, s, pad, False)
     xc = x.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last).requires_grad_(True)
     wc = w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last).requires_grad_(True)
     tp = (k - 1) // 2 if k > 1 else 0
@@ -62,11 +77,11 @@ for h, cin, cout, k, s in SHAPES:
                                                               [0, 0], 1, [True, False, False]))
     rw = timeit(lambda: torch.ops.aten.convolution_backward(dyc, xc, wc, None, [s, s], [tp, tp], [1, 1], False,
                                                               [0, 0], 1, [False, True, False]))
-    ours = [tf, td, tw]
-    ref = [rf, rd, rw]
-    tot[0] += sum(t for t in ours if t == t)
-    tot[1] += sum(ref)
-    fmt = lambda t: f"{t * 1e3:7.3f}/{flop / t / 1e12:6.1f}" if t == t else "    n/a       "
-    print(f"{h:3d}x{h:<3d} {cin:3d}->{cout:3d} k{k} s{s}: " + " ".join(fmt(t) for t in ours) + " | " +
-          " ".join(fmt(t) for t in ref), flush=True)
-print(f"sum of layers (one instance each): ours {tot[0] * 1e3:.3f} ms, torch {tot[1] * 1e3:.3f} ms")
+    t_ = [rf, rd, rw]
+    for key, v in (("glds", g), ("reg", r), ("torch", t_)):
+        tot[key] += cnt * sum(t for t in v if t == t)
+    fmt = lambda t: f"{t * 1e3:6.3f}/{flop / t / 1e12:5.0f}" if t == t else "   n/a      "
+    print(f"{h:3d}x{h:<3d} {cin:3d}->{cout:3d} k{k} s{s} x{cnt}: " + " ".join(fmt(t) for t in g) + " | " +
+          " ".join(fmt(t) for t in r) + " | " + " ".join(fmt(t) for t in t_), flush=True)
+print("ResNet-18 step-weighted sum of conv GEMMs: " +
+      ", ".join(f"{k} {v * 1e3:.3f} ms" for k, v in tot.items()), flush=True)

@@ -1,0 +1,118 @@
+"""The LDS-DMA (global_load_lds) implicit-GEMM conv kernels (csrc/kernels/conv_gemm.hip):
+forward for any conv whose input has C % 64 == 0, backprop-input for stride-1 convs
+whose output has C % 64 == 0.
+
+Checked two ways: against the plain PyTorch fp32 conv (same bf16-rounded operands), and
+BITWISE against the register-staged kernel (csrc/kernels/gemm.hip, DAMD_CONV_GLDS=0): with
+no K split both accumulate the same 32-deep MFMA chunks in the same k order, so any
+difference is a staging / swizzle / padding bug, not rounding.  Shapes are ragged (M and
+N not multiples of the tiles, odd image sizes, zero padding on every side)."""
+import pytest
+import torch
+
+from distributed_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+dev = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+@pytest.fixture(scope="module")
+def H():
+    from distributed_amd.ops import hip
+
+    return hip
+
+
+def rb(t):
+    return t.to(torch.bfloat16).float()
+
+
+def rnd(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev)
+
+
+def close(a, b, rtol, atol_frac):
+    a, b = a.float(), b.float()
+    atol = atol_frac * b.abs().max().item() + 1e-12
+    err = (a - b).abs().max().item()
+    assert torch.allclose(a, b, rtol=rtol, atol=atol), f"max abs err {err:.3e} (atol {atol:.3e})"
+
+
+CASES = [
+    # n, h, cin, cout, k, s, padding
+    (2, 9, 64, 64, 3, 1, "same"),      # 256x64 tiles, ragged M
+    (3, 11, 64, 200, 3, 1, "same"),    # 128x128 tiles, ragged N (200 = 128 + 72)
+    (2, 10, 128, 128, 3, 2, "same"),   # stride 2 (forward only on the DMA path)
+    (3, 7, 64, 128, 1, 2, "valid"),    # 1x1 projection
+    (2, 12, 192, 64, 3, 1, "valid"),   # valid padding, Cin = 3 x 64
+    (1, 7, 512, 512, 3, 1, "same"),    # ResNet layer4 shape
+]
+
+
+@pytest.mark.parametrize("n,h,cin,cout,k,s,padding", CASES)
+def test_glds_conv_matches_reference_and_regstaged_kernel(H, monkeypatch, n, h, cin, cout, k, s, padding):
+    monkeypatch.setattr(H, "SPLIT_MIN_TILES", 0)  # fused epilogue (split-K: the test below)
+    x = rb(rnd(n, h, h, cin, seed=1)).requires_grad_(True)
+    w = rb(rnd(k, k, cin, cout, scale=0.1, seed=2)).requires_grad_(True)
+    y = ref.conv2d(x, w, None, (s, s), padding)
+    dy = rb(rnd(*y.shape, seed=3))
+    gx, = torch.autograd.grad(y, (x,), dy)
+    xb, wb, dyb = x.detach().bfloat16(), w.detach().bfloat16(), dy.bfloat16()
+
+    fplan = H.conv_fwd_plan(x.shape, w.shape, (s, s), padding)
+    assert fplan["amode"] == H.A_CONV64
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_fwd(xb, wb, out, (s, s), padding)
+    close(out, y.detach(), 1e-2, 4e-3)
+    dplan = H.conv_dgrad_plan(x.shape, w.shape, (s, s), padding)
+    assert (dplan["amode"] == H.A_DGRAD64) == (s == 1 and cout % 64 == 0)
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_dgrad(dyb, wb, dx, (s, s), padding)
+    close(dx, gx, 1e-2, 4e-3)
+
+    monkeypatch.setenv("DAMD_CONV_GLDS", "0")
+    assert H.conv_fwd_plan(x.shape, w.shape, (s, s), padding)["amode"] == H.A_IM2COL
+    assert fplan["splits"] == 1 and dplan["splits"] == 1
+    out0 = torch.empty_like(out)
+    H.conv_fwd(xb, wb, out0, (s, s), padding)
+    assert torch.equal(out, out0)
+    dx0 = torch.empty_like(dx)
+    H.conv_dgrad(dyb, wb, dx0, (s, s), padding)
+    assert torch.equal(dx, dx0)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_glds_conv_epilogues(H, monkeypatch, split):
+    """bias + ReLU, BN statistics, dgrad accumulation; fused epilogue and split-K slabs
+    (k_per_split a multiple of the 64-deep k-step) + the finishing kernel."""
+    monkeypatch.setattr(H, "SPLIT_MIN_TILES", 1 << 30 if split else 0)
+    n, h, cin, cout = 2, 7, 128, 64
+    plan = H.conv_fwd_plan((n, h, h, cin), (3, 3, cin, cout), (1, 1), "same")
+    assert plan["amode"] == H.A_CONV64 and (plan["splits"] > 1) == split
+    assert plan["kps"] % 64 == 0
+    x = rb(rnd(n, h, h, cin, seed=40))
+    w = rb(rnd(3, 3, cin, cout, scale=0.1, seed=41))
+    b = rnd(cout, seed=42)
+    y = ref.conv2d(x, w, b, (1, 1), "same")
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(plan["stats_T"], 2, cout, device=dev)
+    H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", bias=b, stats=st)
+    close(out, y, 1e-2, 4e-3)
+    yb = out.float().reshape(-1, cout)
+    close(st[:, 0].sum(0), yb.sum(0), 1e-4, 1e-5)
+    close(st[:, 1].sum(0), (yb * yb).sum(0), 1e-4, 1e-5)
+    H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", bias=b, relu=True)
+    close(out, y.relu(), 1e-2, 4e-3)
+    # dgrad of a conv with 64 output channels: gathered tensor dy has C = 64
+    dy = rb(rnd(n, h, h, cout, seed=43))
+    xx = x.clone().requires_grad_(True)
+    gx, = torch.autograd.grad(ref.conv2d(xx, w, None, (1, 1), "same"), (xx,), dy)
+    dplan = H.conv_dgrad_plan(x.shape, w.shape, (1, 1), "same")
+    assert dplan["amode"] == H.A_DGRAD64 and (dplan["splits"] > 1) == split
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (1, 1), "same")
+    close(dx, gx, 1e-2, 4e-3)
+    H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (1, 1), "same", accumulate=True)
+    close(dx, 2 * gx, 1e-2, 8e-3)
