@@ -7,7 +7,9 @@ namespace damd {
 enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4,
                  // glds-staged BK=64 conv kernels (csrc/kernels/conv_gemm.hip): gathered
                  // channel count % 64 == 0; A_DGRAD64 stride 1 only
-                 A_CONV64 = 5, A_DGRAD64 = 6 };
+                 A_CONV64 = 5, A_DGRAD64 = 6,
+                 // weight gradient over "virtual rows" (conv_gemm.hip): K = virtual rows
+                 A_WGRAD64 = 7 };
 enum GemmBMode { B_NC = 0, B_KC = 1 };
 // E_SLAB: split-K partial of split z stored (plain fp32 stores) to C + z * M * ldc; a
 // deterministic splitk_reduce then adds the slabs into the destination in fixed order.
@@ -28,12 +30,19 @@ struct GemmArgs {
   int H, W, Cin, Ho, Wo, KH, KW, stride, pad;
   int kc;              // B_KC: inner k length per tap
   int k_per_split;     // multiple of 32
+  int kstep;           // conv_gemm.hip k-step depth: 32 | 64 (0: DAMD_CONV_KB / 64)
 };
 
 // tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)
 hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int splits, int tile, hipStream_t s);
-// conv_gemm.hip: A_CONV64 (with B_NC weights) / A_DGRAD64 (with B_KC weights)
+// conv_gemm.hip: A_CONV64 (with B_NC weights) / A_DGRAD64 (with B_KC weights) /
+// A_WGRAD64 (B_NC = dy; K = wgrad64_rows, k_per_split a multiple of wgrad64_rows_per_step)
 hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, int tile, hipStream_t s);
+int wgrad64_rows(int N, int Ho, int Wo, int kstep);
+int wgrad64_rows_per_step(int Wo, int kstep);
+// k-step depth of those kernels (32 or 64, env DAMD_CONV_KB): the gathered channel count
+// must be a multiple of it for A_CONV64 / A_DGRAD64
+int conv_gemm_kstep();
 int gemm_stats_tile_rows(int tile);
 // dst[i] += sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order)
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s);

@@ -29,7 +29,7 @@ void register_kernel_ops(py::module_& m) {
       "gemm",
       [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,
          uintptr_t stats, uintptr_t R, int M, int N, int K, int lda, int ldb, int ldc, std::vector<int> geo, int kc,
-         int k_per_split, uintptr_t stream) {
+         int k_per_split, uintptr_t stream, int kstep) {
         damd::GemmArgs a{};
         a.A = P_<const void>(A);
         a.B = P_<const void>(B);
@@ -47,13 +47,15 @@ void register_kernel_ops(py::module_& m) {
         }
         a.kc = kc;
         a.k_per_split = k_per_split;
+        a.kstep = kstep;
         check(damd::gemm_launch(a, amode, bmode, epi, splits, tile, P_<ihipStream_t>(stream)), "gemm");
       },
       py::arg("amode"), py::arg("bmode"), py::arg("epi"), py::arg("splits"), py::arg("tile"), py::arg("A"),
       py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("stats"), py::arg("R"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
-      py::arg("stream"));
+      py::arg("stream"), py::arg("kstep") = 0);
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
+  m.def("conv_gemm_kstep", &damd::conv_gemm_kstep);
   m.def("splitk_finish", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, uintptr_t R, int relu,
                             uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream) {
     check(damd::splitk_finish(P_<const float>(slab), splits, M, N, P_<const float>(bias), P_<const uint16_t>(R), relu,

@@ -14,26 +14,30 @@ dense kernels ``[in, out]``, TF 'same' padding (the extra pixel at bottom/right)
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
 
 from ..native import require_C
 
-A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64 = range(7)
+A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64, A_WGRAD64 = range(8)
 B_NC, B_KC = 0, 1
 E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB = 1, 2, 4, 8, 16, 32, 64
 BK = 32
-BK64 = 64  # k-step of the LDS-DMA conv kernels (csrc/kernels/conv_gemm.hip)
+
+
+def conv_kstep() -> int:
+    """k-step depth of the LDS-DMA conv kernels (csrc/kernels/conv_gemm.hip): 64 (default)
+    or 32 (DAMD_CONV_KB=32); the same rule as the C++ side."""
+    return 32 if os.environ.get("DAMD_CONV_KB") == "32" else 64
 
 
 def use_glds(gathered_channels: int) -> bool:
-    """The LDS-DMA conv kernels take a conv whose gathered tensor has C % 64 == 0 (one
-    filter tap x 64 channels per k-step); DAMD_CONV_GLDS=0 forces the register-staged
+    """The LDS-DMA conv kernels take a conv whose gathered tensor has C % kstep == 0 (one
+    filter tap x kstep channels per k-step); DAMD_CONV_GLDS=0 forces the register-staged
     kernel (A/B comparisons)."""
-    import os
-
-    return gathered_channels % BK64 == 0 and os.environ.get("DAMD_CONV_GLDS", "1") != "0"
+    return gathered_channels % conv_kstep() == 0 and os.environ.get("DAMD_CONV_GLDS", "1") != "0"
 
 
 def _C():
@@ -142,6 +146,45 @@ def wgrad_workspace_elems(M: int, N: int, K: int) -> int:
     return splits * M * N if splits > 1 else 0
 
 
+def wgrad64_geo(n: int, ho: int, wo: int, kb: int) -> Tuple[int, int]:
+    """(virtual rows, virtual rows per k-step) of the LDS-DMA weight-gradient kernel at
+    k-step depth kb (mirror of csrc/kernels/conv_gemm.hip wgrad64_rows / _rows_per_step)."""
+    nseg = -(-wo // kb)
+    wv = -(-wo // nseg)
+    s = 1
+    while s < wv:
+        s <<= 1
+    return n * ho * nseg, kb // s
+
+
+def conv_wgrad_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
+    """Launch plan of conv_wgrad.  The LDS-DMA kernel over virtual rows (conv_gemm.hip)
+    for layers with N = Cout > 64, k-step 32 for images of <= 16 columns (4 blocks/CU:
+    the small-image layers are bound by per-block overheads) else 64; the register-staged
+    kernel over pixels for N <= 64 (measured faster there: scripts/bench_gemm.py)."""
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
+    M, N = kh * kw * cin, cout
+    kb = int(os.environ.get("DAMD_CONV_KB", "0")) or (32 if wo <= 16 else 64)
+    vr, g = wgrad64_geo(n, ho, wo, kb)
+    pick = os.environ.get("DAMD_WGRAD_KERNEL", "auto")  # auto | glds | reg (tests, A/B runs)
+    glds = N > 64 if pick == "auto" else pick == "glds"
+    if os.environ.get("DAMD_CONV_GLDS", "1") != "0" and glds and vr < (1 << 21):
+        t = pick_tile(N)
+        bm, bn = (256, 64) if t == 1 else (128, 128)
+        tiles = -(-M // bm) * -(-N // bn)
+        steps = -(-vr // g)
+        cap = max(1, WGRAD_SLAB_MAX // (M * N * 4))
+        splits = max(1, min(-(-WGRAD_TARGET_WG // tiles), max(1, steps // 4), cap))
+        kps = -(-steps // splits) * g
+        splits = -(-vr // kps)
+        return {"amode": A_WGRAD64, "M": M, "N": N, "K": vr, "tile": t, "splits": splits, "kps": kps, "kstep": kb,
+                "ws": splits * M * N if splits > 1 else 0}
+    K = n * ho * wo
+    t, splits, kps = wgrad_plan(M, N, K)
+    return {"amode": A_WGRAD, "M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps, "kstep": 0,
+            "ws": splits * M * N if splits > 1 else 0}
+
+
 def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
     t, splits, kps = wgrad_plan(M, N, K)
     if splits == 1:  # one writer per element: the atomic epilogue is an uncontended add
@@ -157,11 +200,11 @@ def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
 
 
 def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
-         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None):
+         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0):
     t = pick_tile(N) if tile is None else tile
     kps = k_per_split if k_per_split is not None else -(-K // BK) * BK
     _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), _ptr(stats), _ptr(R), M, N, K,
-              lda, ldb, ldc, list(geo), kc, kps, stream_handle())
+              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep)
 
 
 # ---- dense -------------------------------------------------------------------------------
@@ -226,7 +269,7 @@ def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     M, N, K = n * ho * wo, cout, kh * kw * cin
     t = pick_tile(N)
     glds = use_glds(cin)
-    splits, kps = split_plan(M, N, K, t, BK64 if glds else BK)
+    splits, kps = split_plan(M, N, K, t, conv_kstep() if glds else BK)
     return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,
             "amode": A_CONV64 if glds else A_IM2COL,
             "stats_T": -(-M // (FINISH_RB if splits > 1 else tile_rows(t))),
@@ -276,7 +319,7 @@ def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     M, N, K = n * h * wd, cin, kh * kw * cout
     t = pick_tile(N)
     glds = s == 1 and use_glds(cout)
-    splits, kps = split_plan(M, N, K, t, BK64 if glds else BK)
+    splits, kps = split_plan(M, N, K, t, conv_kstep() if glds else BK)
     return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,
             "amode": A_DGRAD64 if glds else A_DGRAD,
             "ws": splits * M * N if splits > 1 else 0}
@@ -309,8 +352,7 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
 
 
 def conv_wgrad_workspace_elems(x_shape, w_shape, strides=(1, 1), padding="valid") -> int:
-    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
-    return wgrad_workspace_elems(kh * kw * cin, cout, n * ho * wo)
+    return conv_wgrad_plan(x_shape, w_shape, strides, padding)["ws"]
 
 
 def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid", workspace: Optional[torch.Tensor] = None):
@@ -322,11 +364,17 @@ def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid", workspace: Optional[t
     _chk(dw, torch.float32, "dw")
     if cin % 8 or cout % 8:
         raise ValueError("conv_wgrad: Cin and Cout must be multiples of 8")
-    M, N, K = kh * kw * cin, cout, n * ho * wo
-    if workspace is None and wgrad_workspace_elems(M, N, K):
-        workspace = torch.empty(wgrad_workspace_elems(M, N, K), device=x.device)
-    _wgrad_gemm(x, dy, dw, workspace, amode=A_WGRAD, M=M, N=N, K=K, ldb=cout,
-                geo=(h, wd, cin, ho, wo, kh, kw, s, pad))
+    plan = conv_wgrad_plan(x.shape, dw.shape, strides, padding)
+    M, N, K, splits = plan["M"], plan["N"], plan["K"], plan["splits"]
+    geo = (h, wd, cin, ho, wo, kh, kw, s, pad)
+    if splits == 1:  # one writer per element: the atomic epilogue is an uncontended add
+        gemm(x, dy, dw, amode=plan["amode"], bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_ATOMIC, geo=geo,
+             k_per_split=plan["kps"], tile=plan["tile"], kstep=plan["kstep"])
+        return
+    workspace = _workspace(workspace, plan["ws"], x.device)
+    gemm(x, dy, workspace, amode=plan["amode"], bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_SLAB,
+         splits=splits, k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=plan["kstep"])
+    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle())
 
 
 # ---- BN / pooling / loss / optimizer -------------------------------------------------------------

@@ -42,8 +42,9 @@ def timeit(fn, n=20):
     return (time.perf_counter() - t) / n
 
 
-def ours(x, w, y, dy, dx, dw, s, pad, glds):
+def ours(x, w, y, dy, dx, dw, s, pad, glds, cfg="32:2"):
     os.environ["DAMD_CONV_GLDS"] = "1" if glds else "0"
+    os.environ["DAMD_CONV_KB"], os.environ["DAMD_CONV_STAGES"] = cfg.split(":")
     ws = torch.empty(max(H.conv_fwd_plan(x.shape, w.shape, (s, s), pad)["ws"],
                          H.conv_dgrad_plan(x.shape, w.shape, (s, s), pad)["ws"],
                          H.conv_wgrad_workspace_elems(x.shape, w.shape, (s, s), pad), 4), device=dev)
@@ -53,8 +54,11 @@ def ours(x, w, y, dy, dx, dw, s, pad, glds):
     return [tf, td, tw]
 
 
-print(f"B={B}  (ms / TFLOP/s)  fwd dgrad wgrad:  glds | register-staged | torch channels_last", flush=True)
-tot = {"glds": 0.0, "reg": 0.0, "torch": 0.0}
+CFGS = os.environ.get("BENCH_CFG", "32:2").split(",")  # LDS-DMA kernels: kstep:stages
+print(f"B={B}  (ms / TFLOP/s)  fwd dgrad wgrad:  glds {CFGS} | register-staged | torch channels_last",
+      flush=True)
+tot = {f"glds{c}": 0.0 for c in CFGS}
+tot.update({"reg": 0.0, "torch": 0.0})
 for (h, cin, cout, k, s), cnt in zip(SHAPES, COUNT):
     pad = "same" if k > 1 else "valid"
     ho, p = H.conv_out(h, k, s, pad)
@@ -65,7 +69,7 @@ for (h, cin, cout, k, s), cnt in zip(SHAPES, COUNT):
     dx = torch.empty_like(x)
     dw = torch.zeros(k, k, cin, cout, device=dev)
     flop = 2.0 * B * ho * ho * cout * k * k * cin
-    g = ours(x, w, y, dy, dx, dw, s, pad, True)
+    gs = [ours(x, w, y, dy, dx, dw, s, pad, True, c) for c in CFGS]
     r = ours(x, w, y, dy, dx, dw, s, pad, False)
     xc = x.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last).requires_grad_(True)
     wc = w.permute(3, 2, 0, 1).contiguous(memory_format=torch.channels_last).requires_grad_(True)
@@ -78,10 +82,11 @@ for (h, cin, cout, k, s), cnt in zip(SHAPES, COUNT):
     rw = timeit(lambda: torch.ops.aten.convolution_backward(dyc, xc, wc, None, [s, s], [tp, tp], [1, 1], False,
                                                               [0, 0], 1, [False, True, False]))
     t_ = [rf, rd, rw]
-    for key, v in (("glds", g), ("reg", r), ("torch", t_)):
+    rows = [(f"glds{c}", g) for c, g in zip(CFGS, gs)] + [("reg", r), ("torch", t_)]
+    for key, v in rows:
         tot[key] += cnt * sum(t for t in v if t == t)
-    fmt = lambda t: f"{t * 1e3:6.3f}/{flop / t / 1e12:5.0f}" if t == t else "   n/a      "
-    print(f"{h:3d}x{h:<3d} {cin:3d}->{cout:3d} k{k} s{s} x{cnt}: " + " ".join(fmt(t) for t in g) + " | " +
-          " ".join(fmt(t) for t in r) + " | " + " ".join(fmt(t) for t in t_), flush=True)
+    fmt = lambda t: f"{t * 1e3:6.3f}/{flop / t / 1e12:4.0f}" if t == t else "  n/a      "
+    print(f"{h:3d}x{h:<3d} {cin:3d}->{cout:3d} k{k} s{s} x{cnt}: " +
+          " | ".join(" ".join(fmt(t) for t in v) for _, v in rows), flush=True)
 print("ResNet-18 step-weighted sum of conv GEMMs: " +
       ", ".join(f"{k} {v * 1e3:.3f} ms" for k, v in tot.items()), flush=True)

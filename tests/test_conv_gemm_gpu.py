@@ -83,6 +83,77 @@ def test_glds_conv_matches_reference_and_regstaged_kernel(H, monkeypatch, n, h, 
     assert torch.equal(dx, dx0)
 
 
+WGRAD_CASES = CASES + [
+    (2, 30, 8, 64, 7, 2, "same"),      # ResNet stem geometry (Wo = 15: 4 virtual rows per k-step)
+    (1, 140, 8, 16, 3, 1, "same"),     # Wo = 140 > 64: 3 segments of 47 per output row
+]
+
+
+@pytest.mark.parametrize("n,h,cin,cout,k,s,padding", WGRAD_CASES)
+@pytest.mark.parametrize("target_wg", [1, 512])
+def test_glds_wgrad(H, monkeypatch, n, h, cin, cout, k, s, padding, target_wg):
+    """Weight gradient over virtual rows (one split: atomic epilogue; many: slabs +
+    fixed-order reduce) against the fp32 reference and the register-staged kernel."""
+    monkeypatch.setattr(H, "WGRAD_TARGET_WG", target_wg)
+    monkeypatch.setenv("DAMD_WGRAD_KERNEL", "glds")  # also the N <= 64 layers the planner keeps off it
+    x = rb(rnd(n, h, h, cin, seed=11)).requires_grad_(True)
+    w = rb(rnd(k, k, cin, cout, scale=0.1, seed=12)).requires_grad_(True)
+    y = ref.conv2d(x, w, None, (s, s), padding)
+    dy = rb(rnd(*y.shape, seed=13))
+    gw, = torch.autograd.grad(y, (w,), dy)
+    plan = H.conv_wgrad_plan(x.shape, w.shape, (s, s), padding)
+    assert plan["amode"] == H.A_WGRAD64
+    assert plan["splits"] == 1 or target_wg > 1
+    dw = torch.zeros(w.shape, device=dev)
+    H.conv_wgrad(x.detach().bfloat16(), dy.bfloat16(), dw, (s, s), padding)
+    close(dw, gw, 1e-4, 2e-5)
+    monkeypatch.setenv("DAMD_WGRAD_KERNEL", "reg")
+    assert H.conv_wgrad_plan(x.shape, w.shape, (s, s), padding)["amode"] == H.A_WGRAD
+    dw0 = torch.zeros(w.shape, device=dev)
+    H.conv_wgrad(x.detach().bfloat16(), dy.bfloat16(), dw0, (s, s), padding)
+    close(dw, dw0, 1e-4, 2e-5)
+
+
+@pytest.mark.parametrize("kb", [32, 64])
+@pytest.mark.parametrize("n,h,cin,cout,k,s,padding", [CASES[0], CASES[1], CASES[4], WGRAD_CASES[-2]])
+def test_glds_kstep_variants_deterministic(H, monkeypatch, kb, n, h, cin, cout, k, s, padding):
+    """Both k-step depths of the LDS-DMA kernels (DAMD_CONV_KB) are exercised on every
+    operand path and each is run repeatedly: outputs must be bitwise identical run to run
+    (a staging race shows up as a mismatch) and match the reference."""
+    monkeypatch.setenv("DAMD_CONV_KB", str(kb))
+    monkeypatch.setenv("DAMD_WGRAD_KERNEL", "glds")
+    x = rb(rnd(n, h, h, cin, seed=21)).bfloat16()
+    w = rb(rnd(k, k, cin, cout, scale=0.1, seed=22)).bfloat16()
+    ho, _ = H.conv_out(h, k, s, padding)
+    dy = rb(rnd(n, ho, ho, cout, seed=23)).bfloat16()
+
+    def run():
+        outs = []
+        if cin % 64 == 0:
+            y = torch.empty(n, ho, ho, cout, device=dev, dtype=torch.bfloat16)
+            H.conv_fwd(x, w, y, (s, s), padding)
+            outs.append(y)
+        if s == 1 and cout % 64 == 0:
+            dx = torch.empty(n, h, h, cin, device=dev, dtype=torch.bfloat16)
+            H.conv_dgrad(dy, w, dx, (s, s), padding)
+            outs.append(dx)
+        dw = torch.zeros(k, k, cin, cout, device=dev)
+        H.conv_wgrad(x, dy, dw, (s, s), padding)
+        outs.append(dw)
+        return outs
+
+    ref2 = run()
+    for _ in range(3):
+        for a, b in zip(run(), ref2):
+            assert torch.equal(a, b)
+    xr, wr, dyr = x.float().requires_grad_(True), w.float().requires_grad_(True), dy.float()
+    y = ref.conv2d(xr, wr, None, (s, s), padding)
+    gx, gw = torch.autograd.grad(y, (xr, wr), dyr)
+    close(ref2[-1], gw, 1e-4, 2e-5)
+    if cin % kb == 0:
+        close(ref2[0], y.detach(), 1e-2, 4e-3)
+
+
 @pytest.mark.parametrize("split", [False, True])
 def test_glds_conv_epilogues(H, monkeypatch, split):
     """bias + ReLU, BN statistics, dgrad accumulation; fused epilogue and split-K slabs
@@ -91,7 +162,7 @@ def test_glds_conv_epilogues(H, monkeypatch, split):
     n, h, cin, cout = 2, 7, 128, 64
     plan = H.conv_fwd_plan((n, h, h, cin), (3, 3, cin, cout), (1, 1), "same")
     assert plan["amode"] == H.A_CONV64 and (plan["splits"] > 1) == split
-    assert plan["kps"] % 64 == 0
+    assert plan["kps"] % H.conv_kstep() == 0
     x = rb(rnd(n, h, h, cin, seed=40))
     w = rb(rnd(3, 3, cin, cout, scale=0.1, seed=41))
     b = rnd(cout, seed=42)
