@@ -35,6 +35,16 @@ hipError_t maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, in
                        int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s);
 hipError_t maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw, int sh,
                        int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s);
+// stem fusion (BatchNorm(st) -> ReLU -> MaxPool): the pool reads the conv output x
+hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H, int W, int C, int ph, int pw, int sh,
+                               int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s);
+// its backward: BN-backward partials / apply with the pool routing + ReLU mask recomputed
+hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
+                              int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
+                              float* part, int T, hipStream_t s);
+hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
+                             int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
+                             const float* co, uint16_t* dx, hipStream_t s);
 // global average pool over H*W: x [N][HW][C] bf16 -> y [N][C] (bf16 or fp32)
 hipError_t gap_fwd(const uint16_t* x, int N, int HW, int C, void* y, int y_f32, hipStream_t s);
 hipError_t gap_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* dx, hipStream_t s);

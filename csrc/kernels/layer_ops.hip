@@ -116,7 +116,7 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x,
     ld8f(st + 2 * C + c, sc);
     ld8f(st + 3 * C + c, sh);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) xv[e] = xv[e] * sc[e] + sh[e];
+    for (int e = 0; e < 8; ++e) xv[e] = fmaf(xv[e], sc[e], sh[e]);
     if (res_mode) {
       float rv[8];
       unpack8(reinterpret_cast<const uint4*>(r)[i], rv);
@@ -312,6 +312,175 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_k(const uint16_t* __restrict__
       }
     }
     reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+  }
+}
+
+// ---- stem fusion: BatchNorm -> ReLU -> MaxPool without the normalised tensor ----------
+// Forward: the pool reads the conv output x and normalises on the fly (the BN+ReLU output
+// is never stored); each candidate is rounded to bf16 exactly as bn_apply stores it, so
+// max / argmax equal the unfused pair's.  Backward: the pool's gradient routing and the
+// ReLU mask are recomputed from (dy_pool, argmax, x, BN scale/shift) in both BN-backward
+// passes, so neither the 4x larger un-pooled gradient nor the ReLU output is stored.
+__device__ __forceinline__ void bn_relu8(const float* x, const float* sc, const float* sh, float* y) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) y[e] = bf2f(f2bf(fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f)));
+}
+
+__global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_k(const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ st, PoolGeo g,
+                                                            uint16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int cg = g.C / 8;
+  const long total = (long)g.N * g.Ho * g.Wo * cg;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    long pix = i / cg;
+    const int ow = (int)(pix % g.Wo);
+    pix /= g.Wo;
+    const int oh = (int)(pix % g.Ho);
+    const int n = (int)(pix / g.Ho);
+    float sc[8], sh[8];
+    ld8f(st + 2 * g.C + c8 * 8, sc);
+    ld8f(st + 3 * g.C + c8 * 8, sh);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int kh = 0; kh < g.ph; ++kh) {
+      const int ih = oh * g.sh - g.pt + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.pw; ++kw) {
+        const int iw = ow * g.sw - g.pl + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float xv[8], v[8];
+        unpack8(reinterpret_cast<const uint4*>(x)[(((long)n * g.H + ih) * g.W + iw) * cg + c8], xv);
+        bn_relu8(xv, sc, sh, v);
+        const uint8_t idx = (uint8_t)(kh * g.pw + kw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; bi[e] = idx; }
+      }
+    }
+    reinterpret_cast<uint4*>(y)[i] = pack8(best);
+    uint2 a;
+    a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    reinterpret_cast<uint2*>(arg)[i] = a;
+  }
+}
+
+// gradient reaching input pixel (n, ih, iw), channels 8*c8.. through the max-pool windows
+// (fp32 sum, then rounded to bf16 as maxpool_bwd stores it)
+__device__ __forceinline__ void pool_grad8(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
+                                           const PoolGeo& g, int n, int ih, int iw, int c8, float* acc) {
+  const int cg = g.C / 8;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int ohlo = max(0, (ih + g.pt - g.ph + g.sh) / g.sh), ohhi = min(g.Ho - 1, (ih + g.pt) / g.sh);
+  const int owlo = max(0, (iw + g.pl - g.pw + g.sw) / g.sw), owhi = min(g.Wo - 1, (iw + g.pl) / g.sw);
+  for (int oh = ohlo; oh <= ohhi; ++oh) {
+    const int kh = ih - (oh * g.sh - g.pt);
+    if (kh < 0 || kh >= g.ph) continue;
+    for (int ow = owlo; ow <= owhi; ++ow) {
+      const int kw = iw - (ow * g.sw - g.pl);
+      if (kw < 0 || kw >= g.pw) continue;
+      const long o = (((long)n * g.Ho + oh) * g.Wo + ow) * cg + c8;
+      const uint2 a = reinterpret_cast<const uint2*>(arg)[o];
+      const uint8_t me = (uint8_t)(kh * g.pw + kw);
+      float d[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[o], d);
+      const uint32_t w[2] = {a.x, a.y};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (((w[e >> 2] >> (8 * (e & 3))) & 0xff) == me) acc[e] += d[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = bf2f(f2bf(acc[e]));
+}
+
+// masked upstream gradient of the BN output at input row `row` (flattened n, ih, iw)
+__device__ __forceinline__ void stem_dy8(const uint16_t* __restrict__ dpool, const uint8_t* __restrict__ arg,
+                                         const PoolGeo& g, long row, int c8, const float* xv, const float* sc,
+                                         const float* sh, float* d) {
+  const int iw = (int)(row % g.W);
+  const long t = row / g.W;
+  const int ih = (int)(t % g.H), n = (int)(t / g.H);
+  pool_grad8(dpool, arg, g, n, ih, iw, c8, d);
+  float yv[8];
+  bn_relu8(xv, sc, sh, yv);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+}
+
+__global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_k(const uint16_t* __restrict__ dpool,
+                                                           const uint8_t* __restrict__ arg, PoolGeo g,
+                                                           const uint16_t* __restrict__ x, const float* __restrict__ st,
+                                                           float* __restrict__ part, long M, long rows_per_block) {
+  __shared__ float red[2][NT * 8];
+  const int C = g.C, cg = C / 8, t = threadIdx.x;
+  const int rpi = NT / cg;
+  const int gq = t % cg, rr = t / cg;
+  const int c = gq * 8;
+  float s0[8], s1[8], mean[8], inv[8], sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
+  ld8f(st + c, mean);
+  ld8f(st + C + c, inv);
+  ld8f(st + 2 * C + c, sc);
+  ld8f(st + 3 * C + c, sh);
+  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rr < rpi) {
+    for (long row = r0 + rr; row < r1; row += rpi) {
+      float xv[8], d[8];
+      unpack8(reinterpret_cast<const uint4*>(x)[(row * C + c) / 8], xv);
+      stem_dy8(dpool, arg, g, row, gq, xv, sc, sh, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s0[e] += d[e];
+        s1[e] += d[e] * (xv[e] - mean[e]) * inv[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][t * 8 + e] = rr < rpi ? s0[e] : 0.f;
+    red[1][t * 8 + e] = rr < rpi ? s1[e] : 0.f;
+  }
+  __syncthreads();
+  for (int ch = t; ch < C; ch += NT) {
+    const int gg = ch / 8, e = ch % 8;
+    float a = 0.f, b = 0.f;
+    for (int q = 0; q < rpi; ++q) {
+      a += red[0][(q * cg + gg) * 8 + e];
+      b += red[1][(q * cg + gg) * 8 + e];
+    }
+    part[(size_t)blockIdx.x * 2 * C + ch] = a;
+    part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
+  }
+}
+
+__global__ __launch_bounds__(NT) void pool_bn_bwd_apply_k(const uint16_t* __restrict__ dpool,
+                                                          const uint8_t* __restrict__ arg, PoolGeo g,
+                                                          const uint16_t* __restrict__ x, const float* __restrict__ st,
+                                                          const float* __restrict__ co, uint16_t* __restrict__ dx,
+                                                          long n8) {
+  const int C = g.C, cg = C / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg), c = c8 * 8;
+    const long row = i / cg;
+    float xv[8], d[8], mean[8], inv[8], sc[8], sh[8], a[8], b[8], cc[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
+    ld8f(st + c, mean);
+    ld8f(st + C + c, inv);
+    ld8f(st + 2 * C + c, sc);
+    ld8f(st + 3 * C + c, sh);
+    stem_dy8(dpool, arg, g, row, c8, xv, sc, sh, d);
+    ld8f(co + c, a);
+    ld8f(co + C + c, b);
+    ld8f(co + 2 * C + c, cc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] = a[e] * d[e] + b[e] + cc[e] * (xv[e] - mean[e]) * inv[e];
+    reinterpret_cast<uint4*>(dx)[i] = pack8(d);
   }
 }
 
@@ -511,24 +680,30 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
                                                      const int32_t* __restrict__ labels, const Ctrl* __restrict__ ctrl,
                                                      int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
                                                      int32_t* __restrict__ yb) {
-  const long total = (long)per * HW * Cp;
+  // one thread per 8 (padded) channels of one pixel: one 16-byte store
+  const int cg = Cp / 8;
+  const long total = (long)per * HW * cg;
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
-    const int c = (int)(i % Cp);
-    const long pr = i / Cp;
+    const int c8 = (int)(i % cg);
+    const long pr = i / cg;
     const int p = (int)(pr % HW), r = (int)(pr / HW);
     // rows past the end of a short final batch: zero image, label -1 (masked downstream)
     const bool valid = wrap || base + r < n;
     const long row = valid ? (base + r) % n : 0;
-    float v = 0.f;
-    if (c < Cin && valid) {
-      const long si = (row * HW + p) * Cin + c;
-      v = x_u8 ? (float)((const uint8_t*)x)[si] / scale : ((const float*)x)[si];
+    const long si = (row * HW + p) * Cin;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c8 * 8 + e;
+      v[e] = 0.f;
+      if (c < Cin && valid)
+        v[e] = x_u8 ? (float)((const uint8_t*)x)[si + c] / scale : ((const float*)x)[si + c];
     }
-    xb[i] = f2bf(v);
-    if (p == 0 && c == 0) yb[r] = valid ? labels[row] : -1;
+    reinterpret_cast<uint4*>(xb)[i] = pack8(v);
+    if (p == 0 && c8 == 0) yb[r] = valid ? labels[row] : -1;
   }
 }
 
@@ -564,7 +739,8 @@ hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ct
 
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, const Ctrl* ctrl, int per,
                         int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s) {
-  hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp)), dim3(NT), 0, s, x, x_u8, scale, labels,
+  if (Cp % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp / 8)), dim3(NT), 0, s, x, x_u8, scale, labels,
                      ctrl, per, HW, Cin, Cp, xb, yb);
   return hipGetLastError();
 }
@@ -638,6 +814,35 @@ hipError_t maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int
   if (C % 8) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   hipLaunchKernelGGL(maxpool_bwd_k, dim3(grid_for((long)N * H * W * C / 8)), dim3(NT), 0, s, dy, arg, g, dx);
+  return hipGetLastError();
+}
+
+hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H, int W, int C, int ph, int pw, int sh,
+                               int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s) {
+  if (C % 8 || ph * pw > 255) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_k, dim3(grid_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0, s, x, st, g, y,
+                     arg);
+  return hipGetLastError();
+}
+
+hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
+                              int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
+                              float* part, int T, hipStream_t s) {
+  if (C % 8 || C / 8 > NT) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  const long M = (long)N * H * W, rows = (M + T - 1) / T;
+  hipLaunchKernelGGL(pool_bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, M, rows);
+  return hipGetLastError();
+}
+
+hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
+                             int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
+                             const float* co, uint16_t* dx, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  const long n8 = (long)N * H * W * C / 8;
+  hipLaunchKernelGGL(pool_bn_bwd_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, dpool, arg, g, x, st, co, dx, n8);
   return hipGetLastError();
 }
 

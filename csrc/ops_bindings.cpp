@@ -108,6 +108,26 @@ void register_kernel_ops(py::module_& m) {
                             g[7], g[8], g[9], g[10], g[11], P_<u16>(dx), P_<ihipStream_t>(s)),
           "maxpool_bwd");
   });
+  m.def("bn_relu_maxpool_fwd", [](U x, U st, std::vector<int> g, U y, U arg, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::bn_relu_maxpool_fwd(P_<const u16>(x), P_<const float>(st), g[0], g[1], g[2], g[3], g[4], g[5], g[6],
+                                    g[7], g[8], g[9], g[10], g[11], P_<u16>(y), P_<uint8_t>(arg), P_<ihipStream_t>(s)),
+          "bn_relu_maxpool_fwd");
+  });
+  m.def("pool_bn_bwd_reduce", [](U dpool, U arg, std::vector<int> g, U x, U st, U part, int T, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::pool_bn_bwd_reduce(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
+                                   g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st),
+                                   P_<float>(part), T, P_<ihipStream_t>(s)),
+          "pool_bn_bwd_reduce");
+  });
+  m.def("pool_bn_bwd_apply", [](U dpool, U arg, std::vector<int> g, U x, U st, U co, U dx, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::pool_bn_bwd_apply(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
+                                  g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st),
+                                  P_<const float>(co), P_<u16>(dx), P_<ihipStream_t>(s)),
+          "pool_bn_bwd_apply");
+  });
   m.def("gap_fwd", [](U x, int N, int HW, int C, U y, int y_f32, U s) {
     check(damd::gap_fwd(P_<const u16>(x), N, HW, C, P_<void>(y), y_f32, P_<ihipStream_t>(s)), "gap_fwd");
   });

@@ -337,6 +337,13 @@ class NativeGraphEngine(Engine):
                 nd.attrs["relu"] = True
                 r.attrs["dead"] = True
                 self._alias(r.out, y)
+                # BN -> ReLU -> MaxPool (the ResNet stem): the pool normalises on the fly and
+                # the BN+ReLU output is never stored (layer_ops.hip stem fusion)
+                outs = r.out.consumers
+                if (len(outs) == 1 and outs[0].kind == "MaxPooling2D"
+                        and env.get_bool("DAMD_STEM_FUSE", True)):
+                    nd.attrs["pool"] = outs[0]
+                    outs[0].attrs["bn"] = nd
 
     def _producer(self, t):
         for nd in self.nodes:
@@ -367,7 +374,7 @@ class NativeGraphEngine(Engine):
         self.labels = torch.zeros(self.B, dtype=torch.int32, device=dev)
         last = self.nodes[-1]
         for nd in self.nodes:
-            if nd is last:
+            if nd is last or nd.attrs.get("pool") is not None:  # stem-fused BN: no output tensor
                 continue
             alloc(nd.out)
         # logits: fp32, row pitch padded to 8
@@ -669,8 +676,8 @@ class NativeGraphEngine(Engine):
                                  M, C, H.stream_handle())
         H.bn_finalize(part, Tn, C, M, gamma, beta, l.epsilon, l.momentum, l.moving_mean.value,
                       l.moving_variance.value, st)
-        if nd.attrs.get("stats_only"):
-            return  # applied by the fused Add that consumes it
+        if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None:
+            return  # applied by the fused Add / MaxPool that consumes it
         H.bn_apply(x.buf, st, nd.out.root().buf, relu=nd.attrs.get("relu", False))
 
     def _fwd_Activation(self, nd):
@@ -696,6 +703,11 @@ class NativeGraphEngine(Engine):
 
     def _fwd_MaxPooling2D(self, nd):
         l = nd.layer
+        bn = nd.attrs.get("bn")
+        if bn is not None:  # stem fusion: pool(relu(BN(x))) straight from the conv output
+            H.bn_relu_maxpool_fwd(bn.inputs[0].root().buf, bn.attrs["st"], nd.out.root().buf, nd.attrs["arg"],
+                                  l.pool_size, l.strides, l.padding)
+            return
         H.maxpool_fwd(nd.inputs[0].root().buf, nd.out.root().buf, nd.attrs["arg"], l.pool_size, l.strides, l.padding)
 
     def _fwd_GlobalAveragePooling2D(self, nd):
@@ -773,8 +785,8 @@ class NativeGraphEngine(Engine):
                 fin()
 
     def _bwd_BatchNormalization(self, nd):
-        if nd.attrs.get("stats_only"):
-            return  # handled by the fused Add
+        if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None:
+            return  # handled by the fused Add / MaxPool
         y = nd.out.root()
         self._bn_backward(nd, y.grad, y.buf, bool(nd.attrs.get("relu")))
 
@@ -826,6 +838,18 @@ class NativeGraphEngine(Engine):
 
     def _bwd_MaxPooling2D(self, nd):
         l = nd.layer
+        bn = nd.attrs.get("bn")
+        if bn is not None:  # the whole BN(+ReLU) backward of the fused stem
+            x = bn.inputs[0].root()
+            bl = bn.layer
+            dx, fin = self._grad_target(x)
+            H.pool_bn_bwd(nd.out.root().grad, nd.attrs["arg"], x.buf, bn.attrs["st"], bn.attrs["part"],
+                          bn.attrs["co"], dx, l.pool_size, l.strides, l.padding,
+                          dgamma=self.gviews[id(bl.gamma)] if bl.gamma is not None else None,
+                          dbeta=self.gviews[id(bl.beta)] if bl.beta is not None else None)
+            if fin:
+                fin()
+            return
         x = nd.inputs[0].root()
         dx, fin = self._grad_target(x)
         if dx is not None:

@@ -423,6 +423,27 @@ def maxpool_bwd(dy, arg, dx, pool, strides, padding):
     _C().maxpool_bwd(_ptr(dy), _ptr(arg), g, _ptr(dx), stream_handle())
 
 
+def bn_relu_maxpool_fwd(x, st, y, arg, pool, strides, padding):
+    """y, arg = maxpool(relu(BN_st(x))) without materialising the BN output (stem fusion)."""
+    g = pool_geo(x.shape, pool, strides, padding)
+    _C().bn_relu_maxpool_fwd(_ptr(x), _ptr(st), g, _ptr(y), _ptr(arg), stream_handle())
+
+
+def pool_bn_bwd(dpool, arg, x, st, part, co, dx, pool, strides, padding, dgamma=None, dbeta=None):
+    """Backward of bn_relu_maxpool_fwd: BN batch-statistics backward with the pool routing
+    and ReLU mask recomputed (reduce -> finalize (dgamma/dbeta) -> apply into dx)."""
+    g = pool_geo(x.shape, pool, strides, padding)
+    C = x.shape[-1]
+    M = x.numel() // C
+    T = _C().bn_bwd_blocks(M, C)
+    assert part.numel() >= T * 2 * C
+    s = stream_handle()
+    _C().pool_bn_bwd_reduce(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(part), T, s)
+    _C().bn_bwd_finalize(_ptr(part), T, C, float(M), _ptr(st), 0, _ptr(dgamma), _ptr(dbeta), _ptr(co), s)
+    if dx is not None:
+        _C().pool_bn_bwd_apply(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(co), _ptr(dx), s)
+
+
 def gap_fwd(x, y):
     n, h, w, c = x.shape
     _C().gap_fwd(_ptr(x), n, h * w, c, _ptr(y), int(y.dtype == torch.float32), stream_handle())

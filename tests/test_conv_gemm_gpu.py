@@ -154,6 +154,45 @@ def test_glds_kstep_variants_deterministic(H, monkeypatch, kb, n, h, cin, cout, 
         close(ref2[0], y.detach(), 1e-2, 4e-3)
 
 
+@pytest.mark.parametrize("n,h,c", [(2, 16, 16), (3, 11, 64)])
+def test_stem_fused_kernels_match_unfused(H, n, h, c):
+    """bn_relu_maxpool_fwd / pool_bn_bwd == bn_apply(relu) + maxpool_fwd and maxpool_bwd +
+    BN backward (relu mask): bitwise on the pooled output, argmax and dx."""
+    C_ = H._C()
+    x = rb(rnd(n, h, h, c, scale=2.0, seed=31)).bfloat16()
+    M = n * h * h
+    g = (rnd(c, seed=32).abs() + 0.5).float()
+    b = rnd(c, seed=33).float()
+    st = torch.stack([rnd(c, seed=34) * 0.1, rnd(c, seed=35).abs() + 0.5, g, b])  # mean, inv, sc, sh
+    pool, strides, pad = (3, 3), (2, 2), "same"
+    geo = H.pool_geo(x.shape, pool, strides, pad)
+    ho, wo = geo[10], geo[11]
+    # forward
+    yb = torch.empty_like(x)
+    H.bn_apply(x, st, yb, relu=True)
+    p0 = torch.empty(n, ho, wo, c, device=dev, dtype=torch.bfloat16)
+    a0 = torch.empty(n, ho, wo, c, device=dev, dtype=torch.uint8)
+    H.maxpool_fwd(yb, p0, a0, pool, strides, pad)
+    p1, a1 = torch.empty_like(p0), torch.empty_like(a0)
+    H.bn_relu_maxpool_fwd(x, st, p1, a1, pool, strides, pad)
+    assert torch.equal(p0, p1) and torch.equal(a0, a1)
+    # backward
+    dp = rb(rnd(n, ho, wo, c, seed=36)).bfloat16()
+    T = C_.bn_bwd_blocks(M, c)
+    part0, part1 = torch.zeros(T, 2, c, device=dev), torch.zeros(T, 2, c, device=dev)
+    co0, co1 = torch.zeros(3, c, device=dev), torch.zeros(3, c, device=dev)
+    dg0, db0, dg1, db1 = (torch.zeros(c, device=dev) for _ in range(4))
+    dyb = torch.empty_like(x)
+    H.maxpool_bwd(dp, a0, dyb, pool, strides, pad)
+    dx0 = torch.empty_like(x)
+    H.bn_bwd(dyb, yb, True, x, st, part0, co0, dx0, dgamma=dg0, dbeta=db0)
+    dx1 = torch.empty_like(x)
+    H.pool_bn_bwd(dp, a1, x, st, part1, co1, dx1, pool, strides, pad, dgamma=dg1, dbeta=db1)
+    assert torch.equal(part0, part1)
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    assert torch.equal(dx0, dx1)
+
+
 @pytest.mark.parametrize("split", [False, True])
 def test_glds_conv_epilogues(H, monkeypatch, split):
     """bias + ReLU, BN statistics, dgrad accumulation; fused epilogue and split-K slabs
