@@ -42,41 +42,38 @@ inline int grid_for(long work, int per_block = NT, int cap = 8192) {
 }
 
 // ---- BatchNorm -------------------------------------------------------------------------
-// Sum the partials [T][2][C] over T in fp64 for the 8 channels c0..c0+7 of this block:
-// every thread strides over T with 32-byte loads, then a wave butterfly and a 4-wave LDS
-// combine (fixed order: deterministic).  On return sums[j] (j < 8) is the channel sum and
-// sums[8 + j] the sum of squares (or of the second statistic).  Grid = C / 8 blocks, so
-// even C = 64 keeps 8 x 256 threads on a reduction over ~1.5k partials.
+// Sum the partials [T][2][C] over T in fp64 for the 8 channels c0..c0+7 of this block.
+// Thread t owns value v = t % 16 of the 16-value record (8 sums, 8 second statistics)
+// and rows t / 16 + 16 k: up to 16 of its loads are in flight at once (the ResNet-18
+// partial counts, T <= 1024, take one or four such batches), then a two-level LDS tree
+// (16 x 16, fixed order: deterministic).  A per-value wave butterfly on doubles costs
+// ~200 dependent cross-lane permutes -- most of an 8 us kernel; this is ~2 latencies.
+// On return sums[j] (j < 8) is the channel sum, sums[8 + j] the second statistic.
 __device__ __forceinline__ void reduce_partials8(const float* __restrict__ part, int T, int C, int c0,
                                                  double* sums) {
-  __shared__ double red[NT / 64][16];
-  double a[16];
+  __shared__ double red[16][17];
+  const int t = threadIdx.x, v = t & 15, sl = t >> 4;
+  const float* p = part + (v < 8 ? c0 + v : C + c0 + (v - 8));
+  const size_t row = (size_t)2 * C;
+  double a = 0.0;
+  for (int i0 = sl; i0 < T; i0 += 16 * 16) {
+    float f[16];
 #pragma unroll
-  for (int j = 0; j < 16; ++j) a[j] = 0.0;
-  for (int i = threadIdx.x; i < T; i += NT) {
-    const float* p = part + (size_t)i * 2 * C + c0;
-    const float4 s0 = *reinterpret_cast<const float4*>(p), s1 = *reinterpret_cast<const float4*>(p + 4);
-    const float4 q0 = *reinterpret_cast<const float4*>(p + C), q1 = *reinterpret_cast<const float4*>(p + C + 4);
-    a[0] += s0.x; a[1] += s0.y; a[2] += s0.z; a[3] += s0.w;
-    a[4] += s1.x; a[5] += s1.y; a[6] += s1.z; a[7] += s1.w;
-    a[8] += q0.x; a[9] += q0.y; a[10] += q0.z; a[11] += q0.w;
-    a[12] += q1.x; a[13] += q1.y; a[14] += q1.z; a[15] += q1.w;
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + 16 * u;
+      f[u] = p[(size_t)min(i, T - 1) * row];
+      f[u] = i < T ? f[u] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) a += (double)f[u];
   }
-#pragma unroll
-  for (int j = 0; j < 16; ++j)
-#pragma unroll
-    for (int sft = 32; sft > 0; sft >>= 1) a[j] += __shfl_xor(a[j], sft);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) red[wave][j] = a[j];
-  }
+  red[sl][v] = a;
   __syncthreads();
-  if (threadIdx.x < 16) {
-    double v = 0.0;
+  if (t < 16) {
+    double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < NT / 64; ++w) v += red[w][threadIdx.x];
-    sums[threadIdx.x] = v;
+    for (int q = 0; q < 16; ++q) s += red[q][t];
+    sums[t] = s;
   }
   __syncthreads();
 }
