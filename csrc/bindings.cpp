@@ -47,6 +47,7 @@ class ConvNetTrainer : public StepExecutor {
     b_.hpart = P_<float>(g("hpart"));
     b_.W1alt = P_<float>(g("w1alt")); b_.V1alt = P_<float>(g("v1alt")); b_.w1bf = P_<uint16_t>(g("w1bf"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
+    b_.fuse_head = bufs.contains("fuse_head") ? (int)g("fuse_head") : 0;
     HIP_CHECK(convnet_set_lds_limits());
   }
   // X [n][784] (fp32, or uint8 holding k for inputs k/255) and labels [n] int32:

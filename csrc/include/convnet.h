@@ -13,6 +13,8 @@ struct ConvNetBuffers {
   float* W1alt; float* V1alt; uint16_t* w1bf;  // W1 double buffer (fp32, velocity) + bf16 copy
   uint16_t* pooled /* [5408][BP] */; uint8_t* code /* [B][5408] */; float* slabs; uint16_t* dhq; float* hpart;
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
+  // 1: the head (F2) runs inside F1 (hacc + counters in `slabs`, see convnet_fused.hip)
+  int fuse_head;
 };
 constexpr int kConvNetNParam = 347146;
 constexpr int kConvNetNGrad = 347152;

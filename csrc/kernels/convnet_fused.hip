@@ -215,14 +215,186 @@ __device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, in
 }
 
 // =================================================================================
+// Head fused into F1 (opt-in, DAMD_CONVNET_FUSE_HEAD=1; measured 37.5 vs 30.0 us/step for the
+// separate F2 launch at B=64, so F2 stays the default).
+// Dense-1 split-K: every F1 block adds its [IB rows][64] partial into hacc (fp32 atomics,
+// memory-side; 256 contiguous bytes per wave instruction) and draws a ticket from its
+// image group's counter.  The block whose ticket completes the group (the last arriver,
+// told by the returned count) runs F2's work for the group's rows: hacc + b1 + ReLU,
+// Dense(10), softmax-xent, accuracy, dz, dh (bf16 hi/lo, both layouts), the per-row
+// records, then re-zeroes hacc.  The block completing the whole grid writes back the
+// conv parameters' pending update and zeroes their gradient (F2's other duty).  Hand-off
+// per cdna_hip_programming.md §6 Guideline 16 (row 1 of the valid forms): every payload
+// access is memory-side or sc1 (atomics; hacc loads/stores via relaxed agent-scope
+// atomics), every storing wave drains vmcnt before the barrier that precedes the ticket.
+// Counters count forever (ticket mod blocks per group), so no per-step reset.  Saves
+// F2's launch and boundary (~9 us of a ~30 us step) for ~3 us of tail in F1.
+// hacc = slabs[0 .. B*64), counters = slabs[B*64 ..) (as unsigned): per group, then one
+// for the grid.
+// =================================================================================
+struct HeadIn {
+  float sp[2], sg[2], sv[2];  // b1/W2/b2 (714 values): this thread's i = tid, tid + 512
+  int y;                      // label of row (img0 + tid) for tid < IB
+  bool yvalid;
+};
+
+__device__ __forceinline__ void head_prefetch(HeadIn& h, const float* P, const float* G, const float* V,
+                                              const int* labels, const Ctrl& c, int img0, int B) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = min(tid + u * 512, NSMALL - 1);
+    h.sp[u] = P[OFF_B1 + i];
+    h.sg[u] = G[OFF_B1 + i];
+    h.sv[u] = V[OFF_B1 + i];
+  }
+  const long g = (long)c.cursor * c.global_batch + c.row0 + img0 + min(tid, 63);
+  h.yvalid = g < c.nsamples && img0 + tid < B;
+  h.y = labels[max(0L, min(g, (long)c.nsamples - 1))];
+}
+
+__device__ __forceinline__ float ld_agent(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void f1_head(const HeadIn& hin, float* xs, const float* cw, float* P, float* G, float* V,
+                                     Ctrl* ctrl, const Ctrl& c, float* slabs, uint16_t* dhq, float* rec, float cp,
+                                     float cg, float cv, int img0, int IB, int B, int tid, int wave, int lane) {
+  __shared__ int flag[2];
+  __shared__ float zsh[8][16];
+  __shared__ float ysh[64];
+  __shared__ unsigned char yok[64];
+  float* hacc = slabs;
+  unsigned* cnt = reinterpret_cast<unsigned*>(slabs + (long)B * HID);
+  const int ngroups = gridDim.y, per_group = gridDim.x;
+  // 1) this block's partial rows -> hacc (one wave instruction = one 256-B row)
+  for (int r = wave; r < IB; r += 8)
+    if (img0 + r < B) atomicAdd(hacc + (long)(img0 + r) * HID + lane, xs[r * HID + lane]);
+  if (tid < IB) {
+    ysh[tid] = __int_as_float(hin.y);
+    yok[tid] = hin.yvalid ? 1 : 0;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every adding wave: its atomics acknowledged
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned tg = __hip_atomic_fetch_add(cnt + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned ta = __hip_atomic_fetch_add(cnt + ngroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = (tg % per_group) == (unsigned)(per_group - 1);
+    flag[1] = (ta % (per_group * ngroups)) == (unsigned)(per_group * ngroups - 1);
+  }
+  __syncthreads();
+  // 2) the grid's last block: conv parameters' pending update written back, gradient zeroed
+  //    (every F1 block has read them by now -- it arrived)
+  if (flag[1] && tid < NCONV) {
+    float wn, vn;
+    sgd_update(cp, cg, cv, c.lr, c.momentum, c.nesterov, wn, vn);
+    P[tid] = wn;
+    if (c.momentum != 0.f) V[tid] = vn;
+    G[tid] = 0.f;
+  }
+  if (!flag[0]) return;
+  // 3) the group's last block: the head of rows img0 .. img0 + IB
+  float* sp = xs;                  // updated b1[64], W2[640], b2[10] (LDS, after the partial rows)
+  float* hs = xs + NSMALL + 2;     // [8 waves][64] h of the wave's current row
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * 512;
+    if (i < NSMALL) {
+      float wn, vn;
+      sgd_update(hin.sp[u], hin.sg[u], hin.sv[u], c.lr, c.momentum, c.nesterov, wn, vn);
+      sp[i] = wn;
+    }
+  }
+  __syncthreads();
+  const float* b1n = sp;
+  const float* w2n = sp + HID;
+  const float* b2n = sp + HID + HID * NCLS;
+  const long gstart = (long)c.cursor * c.global_batch;
+  const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
+  const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
+  const int BP = (B + CH - 1) / CH * CH;
+  const long Q = (long)BP * HID;
+  // one wave per row (rows are independent: no block barrier inside the loop)
+  for (int r = wave; r < IB; r += 8) {
+    const int b = img0 + r;
+    if (b >= B) break;
+    float* hacc_row = hacc + (long)b * HID;
+    const float hv = ld_agent(hacc_row + lane);
+    st_agent(hacc_row + lane, 0.f);  // consumed: zero for the next step
+    const float h = fmaxf(hv + b1n[lane], 0.f);
+    hs[wave * 64 + lane] = h;
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane < 16) {
+      float z = -INFINITY;
+      if (lane < NCLS) {
+        z = b2n[lane];
+#pragma unroll 8
+        for (int k = 0; k < HID; ++k) z = fmaf(hs[wave * 64 + k], w2n[k * NCLS + lane], z);
+      }
+      zsh[wave][lane] = z;
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const bool valid = yok[r] != 0;
+    const int y = valid ? __float_as_int(ysh[r]) : 0;
+    float z[NCLS];
+    float m = -INFINITY;
+    int am = 0;
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) {
+      z[k] = zsh[wave][k];
+      am = z[k] > m ? k : am;
+      m = fmaxf(m, z[k]);
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) se += __expf(z[k] - m);
+    const float lse = m + __logf(se);
+    float zy = z[0];
+#pragma unroll
+    for (int k = 1; k < NCLS; ++k) zy = (k == y) ? z[k] : zy;
+    float dz[NCLS];
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) dz[k] = valid ? (__expf(z[k] - lse) - (k == y ? 1.f : 0.f)) * inv : 0.f;
+    float dhl = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) dhl = fmaf(dz[k], w2n[lane * NCLS + k], dhl);
+    dhl = h > 0.f ? dhl : 0.f;
+    const uint16_t hi = f2bf(dhl), lo = bf16_lo(dhl, hi);
+    dhq[(long)b * HID + lane] = hi;
+    dhq[Q + (long)b * HID + lane] = lo;
+    dhq[2 * Q + (long)lane * BP + b] = hi;
+    dhq[3 * Q + (long)lane * BP + b] = lo;
+    rec[(long)(650 + lane) * B + b] = dhl;  // db1
+#pragma unroll
+    for (int k = 0; k < NCLS; ++k) rec[(long)(lane * NCLS + k) * B + b] = h * dz[k];  // dW2
+    if (lane < NCLS) {
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < NCLS; ++q) d = (q == lane) ? dz[q] : d;
+      rec[(long)(640 + lane) * B + b] = d;  // db2
+    }
+    if (lane == 0) {
+      rec[(long)714 * B + b] = valid ? (lse - zy) : 0.f;
+      rec[(long)715 * B + b] = (valid && am == y) ? 1.f : 0.f;
+    }
+  }
+}
+
+// =================================================================================
 // F1: grid (NS slices, ISPLIT image groups of IB = 2^lg images)
 // =================================================================================
-template <bool U8>
+template <bool U8, bool HEAD>
 __global__ __launch_bounds__(512) void f1_forward(
-    const void* __restrict__ X, const float* __restrict__ P, const float* __restrict__ G,
-    const float* __restrict__ V, float* __restrict__ W1alt, float* __restrict__ V1alt,
+    const void* __restrict__ X, float* __restrict__ P, float* __restrict__ G,
+    float* __restrict__ V, float* __restrict__ W1alt, float* __restrict__ V1alt,
     uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl, uint16_t* __restrict__ pooled,
-    uint8_t* __restrict__ code, float* __restrict__ slabs, int B, int PP, int lg, unsigned long long* st) {
+    uint8_t* __restrict__ code, float* __restrict__ slabs, const int* __restrict__ labels,
+    uint16_t* __restrict__ dhq, float* __restrict__ rec, int B, int PP, int lg, unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   Stamps sts;
@@ -236,7 +408,10 @@ __global__ __launch_bounds__(512) void f1_forward(
   uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
   const Ctrl c = *ctrl;
-  if (s == 0 && blockIdx.y == 0 && tid == 0) ctrl->cur2 = c.cursor;
+  if (s == 0 && blockIdx.y == 0 && tid == 0) {
+    ctrl->cur2 = c.cursor;
+    if (HEAD) ctrl->cur3 = c.cursor;  // no F2 in between: F3 reads the step index directly
+  }
   const long row_base = (long)c.cursor * c.global_batch + c.row0 + img0;
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
@@ -272,6 +447,8 @@ __global__ __launch_bounds__(512) void f1_forward(
   }
   const int tcl = min(tid, NCONV - 1);
   const float cp = P[tcl], cv = V[tcl], cg = G[tcl];
+  HeadIn hin;
+  if constexpr (HEAD) head_prefetch(hin, P, G, V, labels, c, img0, B);
 
   // ---- pending SGD update of the W1 slice (the owner block writes the next buffer and
   //      a bf16 copy for F3) and of the conv weights (registers; F2 writes them back) ----
@@ -334,10 +511,15 @@ __global__ __launch_bounds__(512) void f1_forward(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = 16 * mt + 4 * (lane >> 4) + j, lb = img0 + row;
-      if (lb < B) slabs[((long)s * B + lb) * HID + bn] = acc[j];
+      if constexpr (HEAD) xs[row * HID + bn] = acc[j];  // staged: one 256-B atomic row per wave op
+      else if (lb < B) slabs[((long)s * B + lb) * HID + bn] = acc[j];
     }
   }
   stamp(sts, st, 5);
+  if constexpr (HEAD) {
+    lds_barrier();
+    f1_head(hin, xs, cw, P, G, V, ctrl, c, slabs, dhq, rec, cp, cg, cv, img0, IB, B, tid, wave, lane);
+  }
   stamp_flush(sts, st, 6);
 }
 
@@ -809,11 +991,18 @@ static void launch_step_impl(const ConvNetBuffers& b, int B, int PP, hipStream_t
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
-  hipLaunchKernelGGL(f1_forward<U8>, dim3(NS, (B + (1 << lg) - 1) >> lg), dim3(512), convnet_f1_lds(PP, lg), st,
-                     b.X, b.P, b.G, b.V, b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, B, PP, lg,
-                     b.stamps);
-  hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dhq,
-                     b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
+  const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
+  if (b.fuse_head) {
+    hipLaunchKernelGGL((f1_forward<U8, true>), g1, dim3(512), convnet_f1_lds(PP, lg), st, b.X, b.P, b.G, b.V,
+                       b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, b.labels, b.dhq, b.hpart, B, PP,
+                       lg, b.stamps);
+  } else {
+    hipLaunchKernelGGL((f1_forward<U8, false>), g1, dim3(512), convnet_f1_lds(PP, lg), st, b.X, b.P, b.G, b.V,
+                       b.W1alt, b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.slabs, b.labels, b.dhq, b.hpart, B, PP,
+                       lg, b.stamps);
+    hipLaunchKernelGGL(f2_head, dim3(B), dim3(256), 0, st, b.labels, b.P, b.G, b.V, b.ctrl, b.slabs, b.dhq,
+                       b.hpart, B, NS, b.stamps ? b.stamps + 256 * 16 : nullptr);
+  }
   hipLaunchKernelGGL(f3_backward<U8>, dim3(NS), dim3(512), convnet_f3_lds(PP), st, b.X, b.P, b.G, b.V, b.w1bf,
                      b.ctrl, b.pooled, b.code, b.dhq, b.hpart, B, PP, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
 }
@@ -831,10 +1020,17 @@ hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st)
 }
 
 hipError_t convnet_set_lds_limits() {
-  const void* fns[4] = {(const void*)convnet::f3_backward<false>, (const void*)convnet::f3_backward<true>,
-                        (const void*)convnet::f1_forward<false>, (const void*)convnet::f1_forward<true>};
+  const void* fns[6] = {(const void*)convnet::f3_backward<false>, (const void*)convnet::f3_backward<true>,
+                        (const void*)convnet::f1_forward<false, false>, (const void*)convnet::f1_forward<true, false>,
+                        (const void*)convnet::f1_forward<false, true>, (const void*)convnet::f1_forward<true, true>};
   for (const void* f : fns) {
-    hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    // the head variants hold a little static LDS (labels, ticket flags): the dynamic
+    // limit is what is left of the CU's 160 KB
+    hipFuncAttributes at;
+    hipError_t e = hipFuncGetAttributes(&at, f);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024 - (int)at.sharedSizeBytes);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;

@@ -126,6 +126,11 @@ class FusedConvNetEngine(Engine):
                     slabs=self.slabs.data_ptr(), dhq=self.dhq.data_ptr(), hpart=self.hpart.data_ptr(),
                     pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
                     v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr())
+        # DAMD_CONVNET_FUSE_HEAD=1: the head (F2) folded into F1 by last-arriver tails with
+        # fp32 atomics (csrc/kernels/convnet_fused.hip). Measured slower on MI355X (37.5 vs
+        # 30.0 us/step at B=64: same-address atomic serialisation + a serial tail on the
+        # critical path) and not bitwise reproducible, so the separate F2 launch is default.
+        bufs["fuse_head"] = 1 if env.get_bool("DAMD_CONVNET_FUSE_HEAD", False) else 0
         self.stamps = None
         if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
             self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)
