@@ -9,7 +9,9 @@ enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4,
                  // channel count % 64 == 0; A_DGRAD64 stride 1 only
                  A_CONV64 = 5, A_DGRAD64 = 6,
                  // weight gradient over "virtual rows" (conv_gemm.hip): K = virtual rows
-                 A_WGRAD64 = 7 };
+                 A_WGRAD64 = 7,
+                 // conv_wgrad3.hip: direct 3x3/s1/p1 weight gradient (all taps per block)
+                 A_WGRAD3 = 8 };
 enum GemmBMode { B_NC = 0, B_KC = 1 };
 // E_SLAB: split-K partial of split z stored (plain fp32 stores) to C + z * M * ldc; a
 // deterministic splitk_reduce then adds the slabs into the destination in fixed order.
@@ -39,6 +41,9 @@ hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int spl
 // A_WGRAD64 (B_NC = dy; K = wgrad64_rows, k_per_split a multiple of wgrad64_rows_per_step)
 hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, int tile, hipStream_t s);
 int wgrad64_rows(int N, int Ho, int Wo, int kstep);
+// A_WGRAD3: K = wgrad3_rows (q space), k_per_split a multiple of 32, tiles 64x64 x 9 taps
+hipError_t wgrad3_launch(const GemmArgs& a, int epi, int splits, hipStream_t s);
+int wgrad3_rows(int N, int H, int W);
 int wgrad64_rows_per_step(int Wo, int kstep);
 // k-step depth of those kernels (32 or 64, env DAMD_CONV_KB): the gathered channel count
 // must be a multiple of it for A_CONV64 / A_DGRAD64

@@ -20,6 +20,34 @@ __device__ __forceinline__ s16x4 ds_tr16(const void* lds_byte_ptr) {
           (uintptr_t)lds_byte_ptr)));
 }
 
+// LDS-DMA (global_load_lds_dwordx4: 16 B per lane to lds_wave_base + 16 * lane) issued
+// from inline asm.  Through the builtin, hipcc treats the DMA as a pending LDS write of
+// unknown extent and emits s_waitcnt vmcnt(0) before the next ds_read -- i.e. every k-step
+// drains the stages just issued for later k-steps, and no load overlaps the MFMAs (seen in
+// the .s of every LDS-DMA kernel here).  From asm the DMA is invisible to hipcc's
+// bookkeeping: the kernel's own counted vmcnt + s_barrier order it (and it must be drained
+// before any compiler-counted global load).  M0 is saved and restored inside the statement
+// (cdna_hip_programming.md: the LDS-DMA recipe); the "memory" clobber keeps LDS reads from
+// being cached across it.
+__device__ __forceinline__ void glds16(const void* src, const void* lds_wave_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)lds_wave_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
+// Address of a device symbol held in SGPRs for the whole kernel: an opaque copy, so the
+// "memory" clobbers of the DMA statements do not make hipcc reload it from the GOT (an
+// s_load + lgkmcnt(0) in front of every DMA issue).
+template <class T>
+__device__ __forceinline__ const void* pinned_addr(const T* sym) {
+  uint64_t a = reinterpret_cast<uint64_t>(sym);
+  asm volatile("" : "+s"(a));
+  return reinterpret_cast<const void*>(a);
+}
+
 // MC image: [k rows][COLS] bf16 (mn-contiguous operand); the 16-byte chunk ch of row r is
 // stored at chunk ch ^ mc_swz(r).  The swizzle depends on r mod 32 only (k-steps of 32
 // rows are images of their own) and is an involution per row, so a lane-linear

@@ -45,12 +45,7 @@ constexpr int NT = 256;
 // 16-byte zero block: the DMA source of every padding / out-of-range row
 __device__ __attribute__((aligned(64))) uint4 g_zero16[4];
 
-typedef const void __attribute__((address_space(1)))* gptr_t;
-typedef void __attribute__((address_space(3)))* lptr_t;
-
-__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds_wave_base, 16, 0, 0);
-}
+using tile::glds16;  // inline-asm LDS-DMA (no compiler drain before the next ds_read)
 
 // k-contiguous image [rows][KB]: swizzle of row r (KB/8 chunks of 16 B per row)
 template <int KB>
@@ -128,6 +123,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
   const int RH = DGRAD ? a.H : a.Ho, RW = DGRAD ? a.W : a.Wo;
   const int SH = DGRAD ? a.Ho : a.H, SW = DGRAD ? a.Wo : a.W;
   const uint16_t* src = (const uint16_t*)a.A;
+  const void* zero = tile::pinned_addr(g_zero16);
   // A rows of this thread: r = RPQ * (wave + 4j) + lane / CPK; source chunk
   // (lane % CPK) ^ kc_swz(r), and kc_swz(r) depends on r mod 8 == (lane / CPK) mod 8
   const int rin = lane / CPK;
@@ -178,7 +174,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
       const bool ok = (unsigned)(ay[j] + dy) < (unsigned)SH && (unsigned)(ax[j] + dx) < (unsigned)SW;
-      glds16(ok ? (const void*)(arow[j] + toff) : (const void*)g_zero16, sa + (wave + 4 * j) * 1024);
+      glds16(ok ? (const void*)(arow[j] + toff) : zero, sa + (wave + 4 * j) * 1024);
     }
     char* sb = sa + A_ST;
 #pragma unroll
@@ -186,7 +182,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
       const void* p;
       if constexpr (DGRAD) p = brow[j] + ((long)tap * a.N) * a.kc + c0;
       else p = brow[j] + (long)kt * KB * a.ldb;
-      glds16(bval[j] ? p : (const void*)g_zero16, sb + (wave + 4 * j) * 1024);
+      glds16(bval[j] ? p : zero, sb + (wave + 4 * j) * 1024);
     }
     // advance to the next k-step
     c0 += KB;
@@ -280,6 +276,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
   const int wm = wave / WN, wn = wave % WN;
   const uint16_t* xs = (const uint16_t*)a.A;
   const uint16_t* dys = (const uint16_t*)a.B;
+  const void* zero = tile::pinned_addr(g_zero16);
   const int Cin = a.Cin, Cout = a.N;
 
   // Per lane and DMA instruction j everything but the virtual row is fixed: the k-row
@@ -339,7 +336,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
       if (v.nseg > 1)
         ok = ok && ow0 + a_slot[j] < a.Wo && (unsigned)(ow0 * a.stride + a_iwrel[j]) < (unsigned)a.W;
       const long off = (long)img * HW_C + (long)oh * sW_C + a_off[j] + (long)ow0 * a.stride * Cin;
-      glds16(ok ? (const void*)(xs + off) : (const void*)g_zero16, sa + (wave + 4 * j) * 1024);
+      glds16(ok ? (const void*)(xs + off) : zero, sa + (wave + 4 * j) * 1024);
     }
     char* sb = sa + A_ST;
 #pragma unroll
@@ -351,7 +348,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
       bool ok = b_ok[j] && R0 + b_g[j] < rend;
       if (v.nseg > 1) ok = ok && ow0 + b_slot[j] < a.Wo;
       const long off = (long)img * HoWo_C + ((long)oh * a.Wo + ow0) * Cout + b_off[j];
-      glds16(ok ? (const void*)(dys + off) : (const void*)g_zero16, sb + (wave + 4 * j) * 1024);
+      glds16(ok ? (const void*)(dys + off) : zero, sb + (wave + 4 * j) * 1024);
     }
     // advance the row state by G virtual rows (G == 1 whenever nseg > 1)
     if (v.nseg > 1) {

@@ -626,6 +626,10 @@ hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int spl
   if (splits < 1) return hipErrorInvalidValue;
   if ((epi & E_ATOMIC) && (epi & ~E_ATOMIC)) return hipErrorInvalidValue;
   if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
+  if (amode == A_WGRAD3) {
+    if (bmode != B_NC) return hipErrorInvalidValue;
+    return wgrad3_launch(a, epi, splits, s);
+  }
   if (amode == A_CONV64 || amode == A_DGRAD64 || amode == A_WGRAD64) {
     if (bmode != (amode == A_DGRAD64 ? B_KC : B_NC)) return hipErrorInvalidValue;
     return conv_gemm_launch(a, amode, epi, splits, tile, s);

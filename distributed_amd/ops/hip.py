@@ -21,7 +21,7 @@ import torch
 
 from ..native import require_C
 
-A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64, A_WGRAD64 = range(8)
+A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64, A_WGRAD64, A_WGRAD3 = range(9)
 B_NC, B_KC = 0, 1
 E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB = 1, 2, 4, 8, 16, 32, 64
 BK = 32
@@ -157,16 +157,36 @@ def wgrad64_geo(n: int, ho: int, wo: int, kb: int) -> Tuple[int, int]:
     return n * ho * nseg, kb // s
 
 
+def wgrad3_ok(n, h, w, cin, cout, k, s, pad) -> bool:
+    """Shapes the direct 3x3 weight-gradient kernel takes (mirror of wgrad3_launch)."""
+    return (k == 3 and s == 1 and pad == 1 and cin % 64 == 0 and cout % 64 == 0 and w + 1 <= 63
+            and n * (h + 1) * (w + 1) + 2048 < (1 << 21))
+
+
 def conv_wgrad_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
-    """Launch plan of conv_wgrad.  The LDS-DMA kernel over virtual rows (conv_gemm.hip)
-    for layers with N = Cout > 64, k-step 32 for images of <= 16 columns (4 blocks/CU:
+    """Launch plan of conv_wgrad.  3x3/stride-1/pad-1 layers with channels % 64 == 0: the
+    direct kernel (conv_wgrad3.hip, all nine taps per block).  Otherwise the LDS-DMA
+    kernel over virtual rows (conv_gemm.hip) for layers with N = Cout > 64, k-step 32 for images of <= 16 columns (4 blocks/CU:
     the small-image layers are bound by per-block overheads) else 64; the register-staged
     kernel over pixels for N <= 64 (measured faster there: scripts/bench_gemm.py)."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
     M, N = kh * kw * cin, cout
     kb = int(os.environ.get("DAMD_CONV_KB", "0")) or (32 if wo <= 16 else 64)
     vr, g = wgrad64_geo(n, ho, wo, kb)
-    pick = os.environ.get("DAMD_WGRAD_KERNEL", "auto")  # auto | glds | reg (tests, A/B runs)
+    pick = os.environ.get("DAMD_WGRAD_KERNEL", "auto")  # auto | direct | glds | reg (tests, A/B runs)
+    dma = os.environ.get("DAMD_CONV_GLDS", "1") != "0"
+    if dma and pick in ("auto", "direct") and wgrad3_ok(n, h, wd, cin, cout, kh, s, pad):
+        # direct 3x3 kernel (csrc/kernels/conv_wgrad3.hip): 64x64 (ci, co) tiles x all 9 taps
+        Q = n * (h + 1) * (wd + 1)
+        tiles = (cin // 64) * (cout // 64)
+        steps = -(-Q // 32)
+        cap = max(1, WGRAD_SLAB_MAX // (M * N * 4))
+        target = int(os.environ.get("DAMD_WGRAD3_WG", "256"))  # 8-9-wave blocks, 1 per CU
+        splits = max(1, min(-(-target // tiles), max(1, steps // 8), cap))
+        kps = -(-steps // splits) * 32
+        splits = -(-Q // kps)
+        return {"amode": A_WGRAD3, "M": M, "N": N, "K": Q, "tile": 0, "splits": splits, "kps": kps, "kstep": 0,
+                "ws": splits * M * N if splits > 1 else 0}
     glds = N > 64 if pick == "auto" else pick == "glds"
     if os.environ.get("DAMD_CONV_GLDS", "1") != "0" and glds and vr < (1 << 21):
         t = pick_tile(N)

@@ -226,3 +226,45 @@ def test_glds_conv_epilogues(H, monkeypatch, split):
     close(dx, gx, 1e-2, 4e-3)
     H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (1, 1), "same", accumulate=True)
     close(dx, 2 * gx, 1e-2, 8e-3)
+
+
+WGRAD3_CASES = [
+    # n, h, cin, cout: every ResNet-18 3x3/s1 width class plus ragged / small images
+    (2, 56, 64, 64),     # layer1 (pitch 57: two look-back blocks, 8-block x ring)
+    (3, 28, 128, 64),    # layer2-like, 2 ci tiles
+    (2, 14, 64, 256),    # layer3-like, 4 co tiles
+    (3, 7, 128, 128),    # layer4 geometry (pitch 8: 4 rows per k-step)
+    (1, 5, 64, 64),      # image smaller than one k-step
+    (2, 30, 64, 128),    # pitch 31 = exactly one look-back block
+]
+
+
+@pytest.mark.parametrize("n,h,cin,cout", WGRAD3_CASES)
+@pytest.mark.parametrize("target_wg", ["1", "4096"])
+def test_direct_wgrad3(H, monkeypatch, n, h, cin, cout, target_wg):
+    """Direct 3x3/s1/p1 weight gradient (csrc/kernels/conv_wgrad3.hip: sliding x window,
+    nine shifted taps) against the fp32 reference and the LDS-DMA GEMM kernel; one split
+    (atomic epilogue) and many (slabs, fixed-order reduce); repeat runs bitwise equal."""
+    monkeypatch.setenv("DAMD_WGRAD3_WG", target_wg)
+    x = rb(rnd(n, h, h, cin, seed=51)).requires_grad_(True)
+    w = rb(rnd(3, 3, cin, cout, scale=0.1, seed=52)).requires_grad_(True)
+    y = ref.conv2d(x, w, None, (1, 1), "same")
+    dy = rb(rnd(*y.shape, seed=53))
+    gw, = torch.autograd.grad(y, (w,), dy)
+    plan = H.conv_wgrad_plan(x.shape, w.shape, (1, 1), "same")
+    assert plan["amode"] == H.A_WGRAD3
+    assert plan["splits"] == 1 or target_wg != "1"
+    xb, dyb = x.detach().bfloat16(), dy.bfloat16()
+    dw = torch.zeros(w.shape, device=dev)
+    H.conv_wgrad(xb, dyb, dw, (1, 1), "same")
+    close(dw, gw, 1e-4, 2e-5)
+    if plan["splits"] > 1:
+        for _ in range(2):
+            dw2 = torch.zeros(w.shape, device=dev)
+            H.conv_wgrad(xb, dyb, dw2, (1, 1), "same")
+            assert torch.equal(dw, dw2)
+    monkeypatch.setenv("DAMD_WGRAD_KERNEL", "glds")
+    assert H.conv_wgrad_plan(x.shape, w.shape, (1, 1), "same")["amode"] == H.A_WGRAD64
+    dw0 = torch.zeros(w.shape, device=dev)
+    H.conv_wgrad(xb, dyb, dw0, (1, 1), "same")
+    close(dw, dw0, 1e-4, 2e-5)
