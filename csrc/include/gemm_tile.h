@@ -78,9 +78,14 @@ __device__ __forceinline__ bf16x8 frag_mc(const char* img, int c0, int lane) {
 // (m0, n0), M-tile index tm.  red: >= 2*4*64 floats of LDS, free to use (all staging reads
 // done).  Flags (gemm.h): +bias[n], +R[m][n] (bf16), BatchNorm statistics of the stored
 // pre-ReLU values per (M-tile, split), ReLU, and bf16 / fp32 / atomic / slab stores.
-template <int BM, int BN, int EPI>
+// GEMM row -> output row of C (and R): identity, or a scatter such as the parity classes
+// of the sub-pixel backprop-input (conv_gemm.hip).  Slabs (E_SLAB) keep GEMM rows.
+struct RowIdentity {
+  __device__ __forceinline__ size_t operator()(int m) const { return (size_t)m; }
+};
+template <int BM, int BN, int EPI, class RowOf = RowIdentity>
 __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], int m0, int n0, int tm, int wm,
-                                         int wn, int wave, int lane, float* red) {
+                                         int wn, int wave, int lane, float* red, RowOf row_of = RowOf{}) {
   constexpr int WN = BN / 64, WM = 4 / WN;
   float csum[4][4], csq[4][4];
 #pragma unroll
@@ -91,6 +96,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
     const bool mok = m < a.M;
+    const size_t orow = row_of(mok ? m : 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
@@ -104,7 +110,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       }
       if constexpr (EPI & E_ADD) {
         if (ok) {
-          const uint2 r = *reinterpret_cast<const uint2*>((const uint16_t*)a.R + (size_t)m * a.ldc + n);
+          const uint2 r = *reinterpret_cast<const uint2*>((const uint16_t*)a.R + orow * a.ldc + n);
           v[0] += __uint_as_float(r.x << 16);
           v[1] += __uint_as_float(r.x & 0xffff0000u);
           v[2] += __uint_as_float(r.y << 16);
@@ -129,16 +135,16 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
         float* c = (float*)a.C + ((size_t)blockIdx.z * a.M + m) * a.ldc + n;
         *reinterpret_cast<float4*>(c) = float4{v[0], v[1], v[2], v[3]};
       } else if constexpr (EPI & E_ATOMIC) {
-        float* c = (float*)a.C + (size_t)m * a.ldc + n;
+        float* c = (float*)a.C + orow * a.ldc + n;
 #pragma unroll
         for (int e = 0; e < 4; ++e) atomicAdd(c + e, v[e]);
       } else if constexpr (EPI & E_BF16) {
         uint2 pk;
         pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
         pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>((uint16_t*)a.C + (size_t)m * a.ldc + n) = pk;
+        *reinterpret_cast<uint2*>((uint16_t*)a.C + orow * a.ldc + n) = pk;
       } else {
-        *reinterpret_cast<float4*>((float*)a.C + (size_t)m * a.ldc + n) = float4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<float4*>((float*)a.C + orow * a.ldc + n) = float4{v[0], v[1], v[2], v[3]};
       }
     }
   }

@@ -110,9 +110,23 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
   const int lin = tile::xcd_tile(blockIdx.y * tiles_n + blockIdx.x, tiles);
   const int tn = lin % tiles_n, tm = lin / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.z * a.k_per_split;
-  const int kend = min(a.K, kbeg + a.k_per_split);
-  const int nk = (kend - kbeg) / KB;  // > 0 and exact: checked by the launcher
+  // Stride-2 backprop-input as four sub-pixel convolutions (blockIdx.z = parity class
+  // (ra, rb) of the input pixel; no K split): input row ih = 2 i2 + ra receives dy row
+  // oh = (ih + pad - kh) / 2 from the taps kh = kh0, kh0 + 2, .. (kh0 = (ra + pad) & 1)
+  // only, so each class is a stride-1 conv over the (H/2 x W/2) class grid with
+  // ceil((KH - kh0)/2) x ceil((KW - kw0)/2) taps -- 9 tap-products per 4 pixels instead
+  // of 36 with the zero taps of the dilated formulation.
+  const bool sp = DGRAD && a.stride == 2;
+  const int ra = sp ? (int)(blockIdx.z >> 1) : 0, rb = sp ? (int)(blockIdx.z & 1) : 0;
+  const int kh0 = sp ? (ra + a.pad) & 1 : 0, kw0 = sp ? (rb + a.pad) & 1 : 0;
+  const int tstep = sp ? 2 : 1;
+  const int nth = sp ? (a.KH - kh0 + 1) >> 1 : a.KH, ntw = sp ? (a.KW - kw0 + 1) >> 1 : a.KW;
+  const int kbeg = sp ? 0 : blockIdx.z * a.k_per_split;
+  const int kend = sp ? nth * ntw * a.Cin : min(a.K, kbeg + a.k_per_split);
+  const int nk = (kend - kbeg) / KB;  // exact: checked by the launcher (0 for an empty class)
+  if constexpr ((EPI & E_ADD) != 0) {
+    if (nk == 0) return;  // accumulating: a class without taps adds nothing
+  }
 
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
@@ -120,7 +134,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
 
   // ---- geometry: rows of the output grid (RH x RW), gathered tensor (SH x SW x SC) ----
   const int SC = a.Cin;
-  const int RH = DGRAD ? a.H : a.Ho, RW = DGRAD ? a.W : a.Wo;
+  const int RH = DGRAD ? (sp ? a.H >> 1 : a.H) : a.Ho, RW = DGRAD ? (sp ? a.W >> 1 : a.W) : a.Wo;
   const int SH = DGRAD ? a.Ho : a.H, SW = DGRAD ? a.Wo : a.W;
   const uint16_t* src = (const uint16_t*)a.A;
   const void* zero = tile::pinned_addr(g_zero16);
@@ -135,8 +149,8 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
     const int m = m0 + RPQ * (wave + 4 * j) + rin;
     const int mm = min(m, a.M - 1);
     const int ow = mm % RW, tmp = mm / RW, oh = tmp % RH, n = tmp / RH;
-    const int y0 = DGRAD ? oh + a.pad : oh * a.stride - a.pad;
-    const int x0 = DGRAD ? ow + a.pad : ow * a.stride - a.pad;
+    const int y0 = DGRAD ? (sp ? oh + ((ra + a.pad - kh0) >> 1) : oh + a.pad) : oh * a.stride - a.pad;
+    const int x0 = DGRAD ? (sp ? ow + ((rb + a.pad - kw0) >> 1) : ow + a.pad) : ow * a.stride - a.pad;
     ay[j] = m < a.M ? y0 : -(1 << 28);  // out-of-range rows: never in bounds
     ax[j] = x0;
     arow[j] = src + ((long)n * SH * SW + (long)y0 * SW + x0) * SC + 8 * ca;
@@ -163,13 +177,15 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
     }
   }
 
-  // k-step state (wave-uniform): tap (kh, kw) and channel offset c0 of k = kbeg + KB kt
+  // k-step state (wave-uniform): tap (kh, kw) of the iteration space (class taps when
+  // sp: weight tap (kh0 + 2 kh, kw0 + 2 kw)) and channel offset c0 of k = kbeg + KB kt
   int tap = kbeg / SC, c0 = kbeg - tap * SC;
-  int kh = tap / a.KW, kw = tap - kh * a.KW;
+  int kh = tap / ntw, kw = tap - kh * ntw;
 
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
     char* sa = smem + stage * ST;
     const int dy = DGRAD ? -kh : kh, dx = DGRAD ? -kw : kw;
+    const int wtap = sp ? (kh0 + tstep * kh) * a.KW + kw0 + tstep * kw : tap;
     const long toff = ((long)dy * SW + dx) * SC + c0;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
@@ -180,7 +196,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       const void* p;
-      if constexpr (DGRAD) p = brow[j] + ((long)tap * a.N) * a.kc + c0;
+      if constexpr (DGRAD) p = brow[j] + ((long)wtap * a.N) * a.kc + c0;
       else p = brow[j] + (long)kt * KB * a.ldb;
       glds16(bval[j] ? p : zero, sb + (wave + 4 * j) * 1024);
     }
@@ -189,7 +205,7 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
     if (c0 >= SC) {
       c0 = 0;
       ++tap;
-      if (++kw == a.KW) { kw = 0; ++kh; }
+      if (++kw == ntw) { kw = 0; ++kh; }
     }
   };
 
@@ -219,7 +235,17 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
   };
   kloop<STAGES, NQ>(nk, issue, compute);
   if constexpr ((EPI & E_STATS) != 0) __syncthreads();  // `red` aliases the staging stages
-  tile::epilogue<BM, BN, EPI>(a, acc, m0, n0, tm, wm, wn, wave, lane, reinterpret_cast<float*>(smem));
+  if (sp) {
+    // class-grid row (n, i2, j2) -> input pixel (n, 2 i2 + ra, 2 j2 + rb)
+    const int H = a.H, W = a.W;
+    auto row_of = [=](int m) -> size_t {
+      const int j2 = m % RW, tmp = m / RW, i2 = tmp % RH, n = tmp / RH;
+      return ((size_t)n * H + 2 * i2 + ra) * W + 2 * j2 + rb;
+    };
+    tile::epilogue<BM, BN, EPI>(a, acc, m0, n0, tm, wm, wn, wave, lane, reinterpret_cast<float*>(smem), row_of);
+  } else {
+    tile::epilogue<BM, BN, EPI>(a, acc, m0, n0, tm, wm, wn, wave, lane, reinterpret_cast<float*>(smem));
+  }
 }
 
 // =====================================================================================
@@ -396,9 +422,13 @@ inline int env_int(const char* name, int dflt) {
 }
 inline int conv_kb() { return env_int("DAMD_CONV_KB", 64) == 32 ? 32 : 64; }
 
+// DAMD_CONV_STAGES=3: a third LDS stage (A/B runs; 2 measured best, see the header)
+inline int conv_stages() { return env_int("DAMD_CONV_STAGES", kStages) == 3 ? 3 : 2; }
+
 template <int BM, int BN, int KB, bool DG, int EPI>
 void launch_stages(dim3 grid, const GemmArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, KB, DG, EPI, kStages>), grid, dim3(NT), 0, s, a);
+  if (conv_stages() == 3) hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, KB, DG, EPI, 3>), grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, KB, DG, EPI, 2>), grid, dim3(NT), 0, s, a);
 }
 
 template <int BM, int BN, bool DG, int EPI>
@@ -425,7 +455,8 @@ hipError_t launch_epi(const GemmArgs& a, int epi, int splits, int kb, hipStream_
 
 template <int BM, int BN, int KB, int EPI>
 void launch_wgrad_stages(dim3 grid, const GemmArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((wgrad_kernel<BM, BN, KB, EPI, kStages>), grid, dim3(NT), 0, s, a);
+  if (conv_stages() == 3) hipLaunchKernelGGL((wgrad_kernel<BM, BN, KB, EPI, 3>), grid, dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_kernel<BM, BN, KB, EPI, 2>), grid, dim3(NT), 0, s, a);
 }
 
 template <int BM, int BN>
@@ -477,7 +508,16 @@ hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, i
   if (splits < 1 || a.k_per_split % kb || a.k_per_split < kb || (long)splits * a.k_per_split < a.K ||
       (long)(splits - 1) * a.k_per_split >= a.K)
     return hipErrorInvalidValue;
-  if (dg && (a.stride != 1 || a.kc != a.Cin)) return hipErrorInvalidValue;
+  if (dg && a.kc != a.Cin) return hipErrorInvalidValue;
+  if (dg && a.stride == 2) {
+    // sub-pixel classes: even input extent, class-grid rows, no K split, no statistics
+    if (a.H % 2 || a.W % 2 || a.M % ((a.H / 2) * (a.W / 2)) || splits != 1 || (epi & (E_SLAB | E_STATS)) ||
+        a.pad < 0 || a.pad > 1)
+      return hipErrorInvalidValue;
+    splits = 4;  // grid z = the four parity classes
+  } else if (dg && a.stride != 1) {
+    return hipErrorInvalidValue;
+  }
   if (!dg && a.ldb % 8) return hipErrorInvalidValue;
   if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
   if (tile == 1)

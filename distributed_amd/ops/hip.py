@@ -338,6 +338,11 @@ def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx_shape, w_shape, strides, padding)
     M, N, K = n * h * wd, cin, kh * kw * cout
     t = pick_tile(N)
+    if (s == 2 and use_glds(cout) and h % 2 == 0 and wd % 2 == 0 and pad == 0
+            and os.environ.get("DAMD_DGRAD_SUBPIX", "1") != "0"):
+        # stride 2: four sub-pixel classes (conv_gemm.hip), rows = one class grid, no K split
+        return {"M": n * (h // 2) * (wd // 2), "N": N, "K": K, "tile": t, "splits": 1, "kps": K,
+                "amode": A_DGRAD64, "ws": 0}
     glds = s == 1 and use_glds(cout)
     splits, kps = split_plan(M, N, K, t, conv_kstep() if glds else BK)
     return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps,

@@ -67,7 +67,7 @@ def test_glds_conv_matches_reference_and_regstaged_kernel(H, monkeypatch, n, h, 
     H.conv_fwd(xb, wb, out, (s, s), padding)
     close(out, y.detach(), 1e-2, 4e-3)
     dplan = H.conv_dgrad_plan(x.shape, w.shape, (s, s), padding)
-    assert (dplan["amode"] == H.A_DGRAD64) == (s == 1 and cout % 64 == 0)
+    assert (dplan["amode"] == H.A_DGRAD64) == ((s == 1 or h % 2 == 0) and cout % 64 == 0)
     dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
     H.conv_dgrad(dyb, wb, dx, (s, s), padding)
     close(dx, gx, 1e-2, 4e-3)
@@ -80,7 +80,10 @@ def test_glds_conv_matches_reference_and_regstaged_kernel(H, monkeypatch, n, h, 
     assert torch.equal(out, out0)
     dx0 = torch.empty_like(dx)
     H.conv_dgrad(dyb, wb, dx0, (s, s), padding)
-    assert torch.equal(dx, dx0)
+    if s == 1:
+        assert torch.equal(dx, dx0)
+    else:  # sub-pixel classes sum the taps in another order than the dilated formulation
+        close(dx, dx0, 1e-2, 4e-3)
 
 
 WGRAD_CASES = CASES + [
@@ -268,3 +271,25 @@ def test_direct_wgrad3(H, monkeypatch, n, h, cin, cout, target_wg):
     dw0 = torch.zeros(w.shape, device=dev)
     H.conv_wgrad(xb, dyb, dw0, (1, 1), "same")
     close(dw, dw0, 1e-4, 2e-5)
+
+
+@pytest.mark.parametrize("n,h,cin,cout,k,padding", [
+    (2, 10, 64, 128, 3, "same"),    # ResNet downsample 3x3/s2 (TF "same": pad 0 top/left)
+    (3, 14, 128, 64, 3, "same"),    # 256x64 tiles, ragged class grid (7x7)
+    (2, 12, 64, 128, 1, "valid"),   # 1x1/s2 projection: one class has the tap, three are zero
+])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_subpixel_dgrad_stride2(H, n, h, cin, cout, k, padding, accumulate):
+    """Stride-2 backprop-input as four parity-class convolutions (conv_gemm.hip, grid z =
+    class, scattered epilogue rows) against the fp32 reference; accumulate adds onto dx."""
+    plan = H.conv_dgrad_plan((n, h, h, cin), (k, k, cin, cout), (2, 2), padding)
+    assert plan["amode"] == H.A_DGRAD64 and plan["splits"] == 1
+    x = rb(rnd(n, h, h, cin, seed=61)).requires_grad_(True)
+    w = rb(rnd(k, k, cin, cout, scale=0.1, seed=62))
+    y = ref.conv2d(x, w, None, (2, 2), padding)
+    dy = rb(rnd(*y.shape, seed=63))
+    gx, = torch.autograd.grad(y, (x,), dy)
+    base = rb(rnd(n, h, h, cin, seed=64)) if accumulate else torch.zeros(n, h, h, cin, device=dev)
+    dx = base.bfloat16().clone()
+    H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (2, 2), padding, accumulate=accumulate)
+    close(dx, base + gx, 1e-2, 4e-3)
