@@ -142,6 +142,12 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
   // (lane % CPK) ^ kc_swz(r), and kc_swz(r) depends on r mod 8 == (lane / CPK) mod 8
   const int rin = lane / CPK;
   const int ca = (lane % CPK) ^ kc_swz<KB>(rin);
+  // Packed-tap stem (forward, Cin == 4, KB == 32): a k-step is one filter row kh and its
+  // 32 elements are 8 consecutive input pixels x 4 channels (kw' = 0..7, the weights of
+  // kw' >= KW_true and channel 3 are zero), so chunk ca = input pixels x0 + 2ca, +1 --
+  // the 7x7x3 ResNet stem runs K = 224 instead of 7x7x8 = 392 with 8-padded channels.
+  const bool stem = !DGRAD && a.Cin == 4;
+  const int cpx = stem ? 2 * ca : 0;  // this lane's pixel offset within the row segment
   const uint16_t* arow[NA];
   int ay[NA], ax[NA];
 #pragma unroll
@@ -184,12 +190,12 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
 
   auto issue = [&](int stage, int kt) __attribute__((always_inline)) {
     char* sa = smem + stage * ST;
-    const int dy = DGRAD ? -kh : kh, dx = DGRAD ? -kw : kw;
+    const int dy = DGRAD ? -kh : (stem ? kbeg / KB + kt : kh), dx = DGRAD ? -kw : (stem ? 0 : kw);
     const int wtap = sp ? (kh0 + tstep * kh) * a.KW + kw0 + tstep * kw : tap;
-    const long toff = ((long)dy * SW + dx) * SC + c0;
+    const long toff = ((long)dy * SW + dx) * SC + (stem ? 0 : c0);
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-      const bool ok = (unsigned)(ay[j] + dy) < (unsigned)SH && (unsigned)(ax[j] + dx) < (unsigned)SW;
+      const bool ok = (unsigned)(ay[j] + dy) < (unsigned)SH && (unsigned)(ax[j] + dx + cpx) < (unsigned)SW;
       glds16(ok ? (const void*)(arow[j] + toff) : zero, sa + (wave + 4 * j) * 1024);
     }
     char* sb = sa + A_ST;
@@ -493,7 +499,11 @@ hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, i
   const int kb = a.kstep ? a.kstep : conv_kb();
   if (amode == A_WGRAD64) {
     const int nseg = (a.Wo + kb - 1) / kb;
-    if (a.Cin % 8 || a.N % 8 || a.M != a.KH * a.KW * a.Cin || a.Ho < 1 || a.Wo < 1 || a.K % (a.Ho * nseg))
+    // Cin == 4: the packed-tap stem (KW' = 8): each 8-element chunk is 2 input pixels whose
+    // bounds agree (even stride, pad and width)
+    const bool stem4 = a.Cin == 4 && a.KW % 2 == 0 && a.stride % 2 == 0 && a.pad % 2 == 0 && a.W % 2 == 0;
+    if ((a.Cin % 8 && !stem4) || a.N % 8 || a.M != a.KH * a.KW * a.Cin || a.Ho < 1 || a.Wo < 1 ||
+        a.K % (a.Ho * nseg))
       return hipErrorInvalidValue;
     if (a.K != wgrad64_rows(a.K / (a.Ho * nseg), a.Ho, a.Wo, kb) || a.K >= (1 << 21)) return hipErrorInvalidValue;
     const int G = wgrad64_rows_per_step(a.Wo, kb);
@@ -504,7 +514,12 @@ hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, i
     return tile == 1 ? launch_wgrad<256, 64>(a, epi, splits, kb, s) : launch_wgrad<128, 128>(a, epi, splits, kb, s);
   }
   const bool dg = amode == A_DGRAD64;
-  if (a.Cin % kb || a.N % 8 || a.M < 1 || a.K % kb || a.K != a.KH * a.KW * a.Cin) return hipErrorInvalidValue;
+  // packed-tap stem: 8 pixels x 4 channels per 32-deep k-step, pixel pairs never straddle
+  // the image edge (even stride, pad and width)
+  const bool stem = !dg && a.Cin == 4;
+  if (stem && (kb != 32 || a.KW != 8 || a.stride % 2 || a.pad % 2 || a.W % 2)) return hipErrorInvalidValue;
+  if ((!stem && a.Cin % kb) || a.N % 8 || a.M < 1 || a.K % kb || a.K != a.KH * a.KW * a.Cin)
+    return hipErrorInvalidValue;
   if (splits < 1 || a.k_per_split % kb || a.k_per_split < kb || (long)splits * a.k_per_split < a.K ||
       (long)(splits - 1) * a.k_per_split >= a.K)
     return hipErrorInvalidValue;

@@ -677,12 +677,36 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
                                                      const int32_t* __restrict__ labels, const Ctrl* __restrict__ ctrl,
                                                      int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
                                                      int32_t* __restrict__ yb) {
-  // one thread per 8 (padded) channels of one pixel: one 16-byte store
-  const int cg = Cp / 8;
-  const long total = (long)per * HW * cg;
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
+  if (Cp == 4) {
+    // packed-tap stem input (4 channels): one thread per 2 pixels, one 16-byte store
+    const long total = (long)per * HW / 2;
+    for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+      float v[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const long pr = 2 * i + h;
+        const int p = (int)(pr % HW), r = (int)(pr / HW);
+        const bool valid = wrap || base + r < n;
+        const long row = valid ? (base + r) % n : 0;
+        const long si = (row * HW + p) * Cin;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          v[4 * h + c] = 0.f;
+          if (c < Cin && valid)
+            v[4 * h + c] = x_u8 ? (float)((const uint8_t*)x)[si + c] / scale : ((const float*)x)[si + c];
+        }
+        if (p == 0) yb[r] = valid ? labels[row] : -1;
+      }
+      reinterpret_cast<uint4*>(xb)[i] = pack8(v);
+    }
+    return;
+  }
+  // one thread per 8 (padded) channels of one pixel: one 16-byte store
+  const int cg = Cp / 8;
+  const long total = (long)per * HW * cg;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
     const int c8 = (int)(i % cg);
     const long pr = i / cg;
@@ -736,7 +760,7 @@ hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ct
 
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, const Ctrl* ctrl, int per,
                         int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s) {
-  if (Cp % 8) return hipErrorInvalidValue;
+  if (Cp % 8 && !(Cp == 4 && Cin <= 4 && HW % 2 == 0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp / 8)), dim3(NT), 0, s, x, x_u8, scale, labels,
                      ctrl, per, HW, Cin, Cp, xb, yb);
   return hipGetLastError();

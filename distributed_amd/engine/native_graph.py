@@ -273,6 +273,15 @@ class NativeGraphEngine(Engine):
             nodes.append(nd)
         self.logits_t = tensors[out_key]
         self.nodes = nodes
+        # packed-tap stem: a <= 4-channel input read only by stride-2 convs of <= 8 columns
+        # is stored with 4 channels and those convs run K = KH x 32 (ops/hip.py stem4_ok)
+        if c <= 4 and x0.consumers and env.get_bool("DAMD_STEM4", True) and all(
+                nd.kind == "Conv2D" and H.stem4_ok((B, h, w, 4), (nd.layer.kernel.shape[0], nd.layer.kernel.shape[1],
+                                                                  4, nd.layer.kernel.shape[3]),
+                                                    nd.layer.strides, nd.layer.padding)
+                for nd in x0.consumers):
+            self.cin_pad = 4
+            x0.shape = (B, h, w, 4)
         self._fuse()
 
     def _out_shape(self, kind, l, xs):
@@ -406,7 +415,12 @@ class NativeGraphEngine(Engine):
                 ws = max(ws, H.conv_wgrad_workspace_elems(nd.inputs[0].root().shape, (kh, kw, cin, cout), l.strides,
                                                           l.padding))
                 nd.attrs["cin_pad"] = cin
-                if cin != cin0:
+                if cin == 4 and H.stem4_ok(nd.inputs[0].root().shape, (kh, kw, 4, cout), l.strides, l.padding):
+                    wsh = H.stem4_weight_shape((kh, kw, 4, cout))
+                    nd.attrs["stem4"] = True
+                    nd.attrs["w_pad"] = torch.zeros(wsh, dtype=torch.bfloat16, device=dev)
+                    nd.attrs["dw_pad"] = torch.zeros(wsh, dtype=torch.float32, device=dev)
+                elif cin != cin0:
                     nd.attrs["w_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.bfloat16, device=dev)
                     nd.attrs["dw_pad"] = torch.zeros(kh, kw, cin, cout, dtype=torch.float32, device=dev)
                 xshape, wshape = nd.inputs[0].root().shape, (kh, kw, cin, cout)
@@ -660,12 +674,19 @@ class NativeGraphEngine(Engine):
         l = nd.layer
         x = nd.inputs[0].root().buf
         wb = self._w(nd, l.kernel)
+        bias = self.views[id(l.bias)] if l.use_bias else None
+        relu = getattr(l.activation, "__name__", "linear") == "relu"
+        if nd.attrs.get("stem4"):
+            kh, kw, cin, cout = l.kernel.shape
+            wp = nd.attrs["w_pad"]
+            wp[:, :kw, :cin].copy_(self.views[id(l.kernel)])  # zeros elsewhere stay zero
+            H.conv_fwd_stem4(x, wp, nd.out.root().buf, kh, l.strides, l.padding, bias=bias, relu=relu,
+                             stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
+            return
         if "w_pad" in nd.attrs:
             kh, kw, cin, cout = l.kernel.shape
             H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
             wb = nd.attrs["w_pad"]
-        bias = self.views[id(l.bias)] if l.use_bias else None
-        relu = getattr(l.activation, "__name__", "linear") == "relu"
         H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
                    stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
 
@@ -765,7 +786,13 @@ class NativeGraphEngine(Engine):
             wsp = self.gemm_ws_w if ws_s is not None else self.gemm_ws
             if l.use_bias:
                 H.colsum(dy, self.gviews[id(l.bias)])
-            if "dw_pad" in nd.attrs:
+            if nd.attrs.get("stem4"):
+                kh, kw, cin, cout = l.kernel.shape
+                dwp = nd.attrs["dw_pad"]
+                dwp.zero_()
+                H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=wsp)
+                self.gviews[id(l.kernel)].add_(dwp[:, :kw, :cin])
+            elif "dw_pad" in nd.attrs:
                 dwp = nd.attrs["dw_pad"]
                 dwp.zero_()
                 H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=wsp)

@@ -173,6 +173,19 @@ def conv_wgrad_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     M, N = kh * kw * cin, cout
     kb = int(os.environ.get("DAMD_CONV_KB", "0")) or (32 if wo <= 16 else 64)
     vr, g = wgrad64_geo(n, ho, wo, kb)
+    if stem4_ok(x_shape, w_shape, strides, padding):
+        # packed-tap stem: M = KH x 8 x 4 rows of the stem4_weight_shape layout
+        M = kh * 32
+        t = pick_tile(N)
+        bm, bn = (256, 64) if t == 1 else (128, 128)
+        tiles = -(-M // bm) * -(-N // bn)
+        steps = -(-vr // g)
+        cap = max(1, WGRAD_SLAB_MAX // (M * N * 4))
+        splits = max(1, min(-(-WGRAD_TARGET_WG // tiles), max(1, steps // 4), cap))
+        kps = -(-steps // splits) * g
+        splits = -(-vr // kps)
+        return {"amode": A_WGRAD64, "M": M, "N": N, "K": vr, "tile": t, "splits": splits, "kps": kps, "kstep": kb,
+                "ws": splits * M * N if splits > 1 else 0}
     pick = os.environ.get("DAMD_WGRAD_KERNEL", "auto")  # auto | direct | glds | reg (tests, A/B runs)
     dma = os.environ.get("DAMD_CONV_GLDS", "1") != "0"
     if dma and pick in ("auto", "direct") and wgrad3_ok(n, h, wd, cin, cout, kh, s, pad):
@@ -282,10 +295,90 @@ def conv_geo(x_shape, w_shape, strides, padding):
     return n, h, w_, cin, ho, wo, kh, kw, strides[0], pad, cout
 
 
+def stem4_ok(x_shape, w_shape, strides, padding) -> bool:
+    """A conv the packed-tap stem kernels take (conv_gemm.hip): a 4-channel input (e.g.
+    RGB + one zero channel), a square kernel of <= 8 columns, even stride, even top/left
+    padding and an even image width.  Its weights are laid out [KH][8][4][Cout] (zero
+    beyond the true KW columns / Cin channels): stem4_weight_layout."""
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
+    return (cin == 4 and kw <= 8 and s % 2 == 0 and pad % 2 == 0 and wd % 2 == 0 and cout % 8 == 0
+            and os.environ.get("DAMD_CONV_GLDS", "1") != "0")
+
+
+def stem4_weight_shape(w_shape):
+    kh, kw, cin, cout = w_shape
+    return (kh, 8, 4, cout)
+
+
+def conv_fwd_stem4(x, w8, out, kernel_size, strides=(2, 2), padding="same", bias=None, relu=False, stats=None,
+                   workspace: Optional[torch.Tensor] = None):
+    """Packed-tap stem forward: out = conv(x [N,H,W,4], true kernel kernel_size x
+    kernel_size) with w8 = the weights in stem4_weight_shape layout (bf16)."""
+    k = kernel_size
+    cout = w8.shape[-1]
+    wshape = (k, k, 4, cout)
+    if not stem4_ok(x.shape, wshape, strides, padding) or tuple(w8.shape) != stem4_weight_shape(wshape):
+        raise ValueError("conv_fwd_stem4: not a packed-tap stem conv")
+    _chk(x, torch.bfloat16, "x")
+    _chk(w8, torch.bfloat16, "w8")
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, wshape, strides, padding)
+    assert tuple(out.shape) == (n, ho, wo, cout)
+    plan = conv_fwd_plan(x.shape, wshape, strides, padding)
+    if stats is not None and stats.shape[0] != plan["stats_T"]:
+        raise ValueError(f"conv_fwd_stem4: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
+    M, K = plan["M"], plan["K"]
+    geo = (h, wd, 4, ho, wo, kh, 8, s, pad)
+    if plan["splits"] == 1:
+        epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | \
+            (E_STATS if stats is not None else 0)
+        gemm(x, w8, out, amode=A_CONV64, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=epi, bias=bias,
+             stats=stats, geo=geo, tile=plan["tile"], kstep=32)
+        return
+    ws = _workspace(workspace, plan["ws"], x.device)
+    gemm(x, w8, ws, amode=A_CONV64, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
+         splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=32)
+    _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), _ptr(stats), FINISH_RB,
+                       _ptr(out), cout, stream_handle())
+
+
+def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
+                     workspace: Optional[torch.Tensor] = None):
+    """Packed-tap stem weight gradient: dw8 [KH][8][4][Cout] (fp32) += the gradient in the
+    stem4_weight_shape layout (entries beyond the true kernel are junk to drop)."""
+    k = kernel_size
+    cout = dw8.shape[-1]
+    wshape = (k, k, 4, cout)
+    if not stem4_ok(x.shape, wshape, strides, padding) or tuple(dw8.shape) != stem4_weight_shape(wshape):
+        raise ValueError("conv_wgrad_stem4: not a packed-tap stem conv")
+    _chk(x, torch.bfloat16, "x")
+    _chk(dy, torch.bfloat16, "dy")
+    _chk(dw8, torch.float32, "dw8")
+    plan = conv_wgrad_plan(x.shape, wshape, strides, padding)
+    n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, wshape, strides, padding)
+    geo = (h, wd, 4, ho, wo, kh, 8, s, pad)
+    M, N, K, splits = plan["M"], plan["N"], plan["K"], plan["splits"]
+    if splits == 1:
+        gemm(x, dy, dw8, amode=A_WGRAD64, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_ATOMIC, geo=geo,
+             k_per_split=plan["kps"], tile=plan["tile"], kstep=plan["kstep"])
+        return
+    workspace = _workspace(workspace, plan["ws"], x.device)
+    gemm(x, dy, workspace, amode=A_WGRAD64, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_SLAB,
+         splits=splits, k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=plan["kstep"])
+    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw8), stream_handle())
+
+
 def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     """Launch plan of conv_fwd: tile, split-K, number of BN-statistics partials and the
     fp32 workspace it needs (0 when not split)."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x_shape, w_shape, strides, padding)
+    if stem4_ok(x_shape, w_shape, strides, padding):
+        # packed-tap stem: K = KH x (8 pixels x 4 channels), k-step 32 (conv_gemm.hip)
+        M, N, K = n * ho * wo, cout, kh * 32
+        t = pick_tile(N)
+        splits, kps = split_plan(M, N, K, t, 32)
+        return {"M": M, "N": N, "K": K, "tile": t, "splits": splits, "kps": kps, "amode": A_CONV64,
+                "kstep": 32, "stats_T": -(-M // (FINISH_RB if splits > 1 else tile_rows(t))),
+                "ws": splits * M * N if splits > 1 else 0}
     M, N, K = n * ho * wo, cout, kh * kw * cin
     t = pick_tile(N)
     glds = use_glds(cin)

@@ -293,3 +293,34 @@ def test_subpixel_dgrad_stride2(H, n, h, cin, cout, k, padding, accumulate):
     dx = base.bfloat16().clone()
     H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (2, 2), padding, accumulate=accumulate)
     close(dx, base + gx, 1e-2, 4e-3)
+
+
+@pytest.mark.parametrize("n,h,cin,cout,k,padding", [(2, 32, 3, 64, 7, "same"), (3, 18, 4, 32, 5, "valid"),
+                                                     (1, 24, 1, 64, 3, "same")])
+def test_packed_tap_stem(H, n, h, cin, cout, k, padding):
+    """Packed-tap stem (conv_gemm.hip, 4-channel input, K = KH x 8 pixels x 4 channels):
+    forward (+BN statistics) and weight gradient against the fp32 reference of the true
+    KxK x cin conv; the layout's padding taps/channels come back as zero-input junk only."""
+    x = rb(rnd(n, h, h, cin, seed=71))
+    w = rb(rnd(k, k, cin, cout, scale=0.1, seed=72))
+    x4 = torch.zeros(n, h, h, 4, device=dev)
+    x4[..., :cin] = x
+    wshape = (k, k, 4, cout)
+    assert H.stem4_ok(x4.shape, wshape, (2, 2), padding)
+    w8 = torch.zeros(H.stem4_weight_shape(wshape), device=dev, dtype=torch.bfloat16)
+    w8[:, :k, :cin] = w.bfloat16()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    y = ref.conv2d(xr, wr, None, (2, 2), padding)
+    plan = H.conv_fwd_plan(x4.shape, wshape, (2, 2), padding)
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    st = torch.zeros(plan["stats_T"], 2, cout, device=dev)
+    H.conv_fwd_stem4(x4.bfloat16(), w8, out, k, (2, 2), padding, stats=st)
+    close(out, y.detach(), 1e-2, 4e-3)
+    yb = out.float().reshape(-1, cout)
+    close(st[:, 0].sum(0), yb.sum(0), 1e-4, 1e-5)
+    dy = rb(rnd(*y.shape, seed=73))
+    gw, = torch.autograd.grad(y, (wr,), dy)
+    dw8 = torch.zeros(H.stem4_weight_shape(wshape), device=dev)
+    H.conv_wgrad_stem4(x4.bfloat16(), dy.bfloat16(), dw8, k, (2, 2), padding)
+    close(dw8[:, :k, :cin], gw, 1e-4, 2e-5)

@@ -29,7 +29,10 @@ def test_resnet18_shapes_and_eligibility_reasons():
     assert out["conv5_block2_out"] == (8, 7, 7, 512)
     assert out["avg_pool"] == (8, 512)
     assert out["predictions"] == (8, 1000)
-    assert pl.cin_pad == 8  # RGB padded to 8 channels for 16-byte im2col chunks
+    # RGB stored with 4 channels: the 7x7/2 stem takes the packed-tap kernel (2 pixels x 4
+    # channels per 16-byte chunk); without it RGB pads to 8 channels
+    assert pl.cin_pad == 4
+    assert pl.x0.shape == (8, 224, 224, 4)
 
 
 def test_mnist_plan():
