@@ -55,7 +55,8 @@ struct Ctrl {
   int   cur2;               // 14 step index as seen by the 2nd kernel of a step (set by the 1st)
   int   cur3;               // 15 step index as seen by the 3rd kernel (set by the 2nd)
   int   wpar;               // 16 which W1 buffer is current (0: inside P, 1: the alternate)
-  int   pad[15];
+  int   flush_ticket;       // 17 arrival counter of flush_pending (its last block resets wpar)
+  int   pad[14];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

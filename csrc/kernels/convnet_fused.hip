@@ -959,9 +959,17 @@ __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, floa
     ctrl->acc_count = c.acc_count + G[OFF_CNT];
     for (int i = NPARAM; i < NGRAD; ++i) G[i] = 0.f;
   }
+  // W1 is back inside P: the last block to arrive clears wpar (every block has read it by
+  // then), so the flush is one launch instead of a follow-up fix-up kernel
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(&ctrl->flush_ticket, 1) == (int)gridDim.x - 1) {
+      ctrl->wpar = 0;
+      ctrl->flush_ticket = 0;
+    }
+  }
 }
-// after flush_pending (separate launch: its blocks read wpar): W1 is back inside P
-__global__ void flush_fixup(Ctrl* __restrict__ ctrl) { ctrl->wpar = 0; }
 
 }  // namespace convnet
 
@@ -1015,7 +1023,6 @@ hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream
 
 hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st) {
   hipLaunchKernelGGL(convnet::flush_pending, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.ctrl);
-  hipLaunchKernelGGL(convnet::flush_fixup, dim3(1), dim3(1), 0, st, b.ctrl);
   return hipGetLastError();
 }
 

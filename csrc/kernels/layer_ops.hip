@@ -481,6 +481,181 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_k(const uint16_t* __rest
   }
 }
 
+// ---- stem backward, 3x3/s2 pool with H = 2 Ho, W = 2 Wo: one thread per 2x2 input quad --
+// Pixel-centric gathers (above) load every covering pool window per input pixel: 2.25
+// windows x (16 B gradient + 8 B argmax code) per pixel on average, each a dependent
+// chain.  The 2x2 quad (2a..2a+1, 2b..2b+1) is covered by exactly the windows
+// {a-1+PT, a+PT} x {b-1+PL, b+PL}: one thread loads those 4 windows once (8 independent
+// loads) and routes them to its 4 pixels.  Window (wr, wc) reaches pixel (py, px) at tap
+// kh = py + 2 - PT - 2 wr, kw = px + 2 - PL - 2 wc (valid when in [0, 2]); taps are
+// accumulated in ascending (oh, ow) order exactly as pool_grad8 does, so the routed
+// gradient and dx are bitwise those of the pixel-centric kernels for the same BN
+// coefficients.
+struct Quad8 {
+  float d[4][8];  // routed (bf16-rounded) pool gradient of pixels (py, px) = (q >> 1, q & 1)
+};
+
+template <int PT, int PL>
+__device__ __forceinline__ void quad_route8(const uint16_t* __restrict__ dpool, const uint8_t* __restrict__ arg,
+                                            const PoolGeo& g, int n, int a, int b, int c8, Quad8& o) {
+  const int cg = g.C / 8;
+  float dw[2][2][8];
+  uint32_t aw[2][2][2];
+#pragma unroll
+  for (int wr = 0; wr < 2; ++wr) {
+#pragma unroll
+    for (int wc = 0; wc < 2; ++wc) {
+      const int oh = a - 1 + PT + wr, ow = b - 1 + PL + wc;
+      if ((unsigned)oh < (unsigned)g.Ho && (unsigned)ow < (unsigned)g.Wo) {
+        const long w = (((long)n * g.Ho + oh) * g.Wo + ow) * cg + c8;
+        unpack8(reinterpret_cast<const uint4*>(dpool)[w], dw[wr][wc]);
+        const uint2 av = reinterpret_cast<const uint2*>(arg)[w];
+        aw[wr][wc][0] = av.x;
+        aw[wr][wc][1] = av.y;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dw[wr][wc][e] = 0.f;
+        aw[wr][wc][0] = aw[wr][wc][1] = 0xffffffffu;  // code 255 never matches a tap
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int py = q >> 1, px = q & 1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.d[q][e] = 0.f;
+#pragma unroll
+    for (int wr = 0; wr < 2; ++wr) {
+      const int kh = py + 2 - PT - 2 * wr;
+      if (kh < 0 || kh > 2) continue;
+#pragma unroll
+      for (int wc = 0; wc < 2; ++wc) {
+        const int kw = px + 2 - PL - 2 * wc;
+        if (kw < 0 || kw > 2) continue;
+        const uint32_t me = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (((aw[wr][wc][e >> 2] >> (8 * (e & 3))) & 0xffu) == me) o.d[q][e] += dw[wr][wc][e];
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o.d[q][e] = bf2f(f2bf(o.d[q][e]));
+  }
+}
+
+template <int PT, int PL>
+__global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_q_k(const uint16_t* __restrict__ dpool,
+                                                             const uint8_t* __restrict__ arg, PoolGeo g,
+                                                             const uint16_t* __restrict__ x,
+                                                             const float* __restrict__ st, float* __restrict__ part,
+                                                             long nquad, long quads_per_block) {
+  __shared__ float red[2][NT * 8];
+  const int C = g.C, cg = C / 8, t = threadIdx.x;
+  const int rpi = NT / cg;
+  const int gq = t % cg, rr = t / cg;
+  const int c = gq * 8;
+  float s0[8], s1[8], mean[8], inv[8], sc[8], sh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
+  ld8f(st + c, mean);
+  ld8f(st + C + c, inv);
+  ld8f(st + 2 * C + c, sc);
+  ld8f(st + 3 * C + c, sh);
+  const long q0 = blockIdx.x * quads_per_block, q1 = min(nquad, q0 + quads_per_block);
+  if (rr < rpi) {
+    for (long qd = q0 + rr; qd < q1; qd += rpi) {
+      const int b = (int)(qd % g.Wo);
+      const long tq = qd / g.Wo;
+      const int a = (int)(tq % g.Ho), n = (int)(tq / g.Ho);
+      float xv[4][8];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const long pix = ((long)n * g.H + 2 * a + (q >> 1)) * g.W + 2 * b + (q & 1);
+        unpack8(reinterpret_cast<const uint4*>(x)[pix * cg + gq], xv[q]);
+      }
+      Quad8 r;
+      quad_route8<PT, PL>(dpool, arg, g, n, a, b, gq, r);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float yv[8];
+        bn_relu8(xv[q], sc, sh, yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = yv[e] > 0.f ? r.d[q][e] : 0.f;
+          s0[e] += d;
+          s1[e] += d * (xv[q][e] - mean[e]) * inv[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][t * 8 + e] = rr < rpi ? s0[e] : 0.f;
+    red[1][t * 8 + e] = rr < rpi ? s1[e] : 0.f;
+  }
+  __syncthreads();
+  for (int ch = t; ch < C; ch += NT) {
+    const int gg = ch / 8, e = ch % 8;
+    float sa = 0.f, sb = 0.f;
+    for (int q = 0; q < rpi; ++q) {
+      sa += red[0][(q * cg + gg) * 8 + e];
+      sb += red[1][(q * cg + gg) * 8 + e];
+    }
+    part[(size_t)blockIdx.x * 2 * C + ch] = sa;
+    part[(size_t)blockIdx.x * 2 * C + C + ch] = sb;
+  }
+}
+
+template <int PT, int PL>
+__global__ __launch_bounds__(NT) void pool_bn_bwd_apply_q_k(const uint16_t* __restrict__ dpool,
+                                                            const uint8_t* __restrict__ arg, PoolGeo g,
+                                                            const uint16_t* __restrict__ x,
+                                                            const float* __restrict__ st,
+                                                            const float* __restrict__ co, uint16_t* __restrict__ dx,
+                                                            long nq8) {
+  const int C = g.C, cg = C / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nq8; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg), c = c8 * 8;
+    const long qd = i / cg;
+    const int b = (int)(qd % g.Wo);
+    const long tq = qd / g.Wo;
+    const int a = (int)(tq % g.Ho), n = (int)(tq / g.Ho);
+    long pix[4];
+    float xv[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      pix[q] = ((long)n * g.H + 2 * a + (q >> 1)) * g.W + 2 * b + (q & 1);
+      unpack8(reinterpret_cast<const uint4*>(x)[pix[q] * cg + c8], xv[q]);
+    }
+    Quad8 r;
+    quad_route8<PT, PL>(dpool, arg, g, n, a, b, c8, r);
+    float mean[8], inv[8], sc[8], sh[8], ca[8], cb[8], cc[8];
+    ld8f(st + c, mean);
+    ld8f(st + C + c, inv);
+    ld8f(st + 2 * C + c, sc);
+    ld8f(st + 3 * C + c, sh);
+    ld8f(co + c, ca);
+    ld8f(co + C + c, cb);
+    ld8f(co + 2 * C + c, cc);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float yv[8], d[8];
+      bn_relu8(xv[q], sc, sh, yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float dm = yv[e] > 0.f ? r.d[q][e] : 0.f;
+        d[e] = ca[e] * dm + cb[e] + cc[e] * (xv[q][e] - mean[e]) * inv[e];
+      }
+      reinterpret_cast<uint4*>(dx)[pix[q] * cg + c8] = pack8(d);
+    }
+  }
+}
+
+__host__ __forceinline__ bool quad_pool_geo(const PoolGeo& g) {
+  return g.ph == 3 && g.pw == 3 && g.sh == 2 && g.sw == 2 && (g.pt == 0 || g.pt == 1) && (g.pl == 0 || g.pl == 1) &&
+         g.H == 2 * g.Ho && g.W == 2 * g.Wo;
+}
+
 __global__ __launch_bounds__(NT) void gap_fwd_k(const uint16_t* __restrict__ x, int N, int HW, int C, void* y,
                                                 int y_f32) {
   const int cg = C / 8;
@@ -853,6 +1028,13 @@ hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, 
   if (C % 8 || C / 8 > NT) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   const long M = (long)N * H * W, rows = (M + T - 1) / T;
+  if (quad_pool_geo(g)) {
+    const long nq = (long)N * Ho * Wo, qpb = (nq + T - 1) / T;
+    auto k = g.pt ? (g.pl ? pool_bn_bwd_reduce_q_k<1, 1> : pool_bn_bwd_reduce_q_k<1, 0>)
+                  : (g.pl ? pool_bn_bwd_reduce_q_k<0, 1> : pool_bn_bwd_reduce_q_k<0, 0>);
+    hipLaunchKernelGGL(k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, nq, qpb);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pool_bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, M, rows);
   return hipGetLastError();
 }
@@ -863,6 +1045,13 @@ hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, i
   if (C % 8) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   const long n8 = (long)N * H * W * C / 8;
+  if (quad_pool_geo(g)) {
+    const long nq8 = (long)N * Ho * Wo * C / 8;
+    auto k = g.pt ? (g.pl ? pool_bn_bwd_apply_q_k<1, 1> : pool_bn_bwd_apply_q_k<1, 0>)
+                  : (g.pl ? pool_bn_bwd_apply_q_k<0, 1> : pool_bn_bwd_apply_q_k<0, 0>);
+    hipLaunchKernelGGL(k, dim3(grid_for(nq8)), dim3(NT), 0, s, dpool, arg, g, x, st, co, dx, nq8);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pool_bn_bwd_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, dpool, arg, g, x, st, co, dx, n8);
   return hipGetLastError();
 }

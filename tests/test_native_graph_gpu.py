@@ -377,7 +377,9 @@ def test_rccl_allreduce_captured_in_step_graph(which):
                         extra_env={"DAMD_FORCE_ALLREDUCE": "1", "DAMD_BUCKET_MB": "0.02"}, **kw)
     wb, hb, eb = _train(build, x, y, init, batch, steps, **kw)
     assert ea == eb == which
-    tol = dict(rtol=1e-4, atol=1e-5) if which == "native_graph" else dict(rtol=1e-3, atol=1e-4)
+    # fused engine: F3 adds the conv weight/bias gradient partials with fp32 atomics (order
+    # not fixed), and 45 momentum steps amplify that rounding noise on the small conv bias
+    tol = dict(rtol=1e-4, atol=1e-5) if which == "native_graph" else dict(rtol=1e-3, atol=5e-4)
     for a, b in zip(wa, wb):
         np.testing.assert_allclose(a, b, **tol)
     np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-4)
