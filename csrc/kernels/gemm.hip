@@ -600,11 +600,39 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
   }
 }
 
+// Few splits over a large gradient (the ResNet weight gradients: 2-16 slabs of 0.15-2.4 M
+// floats): one float4 per thread, all slab loads issued before the first add (up to 16
+// independent 16-byte loads in flight), summed in split order after dst -- the same order
+// (and so the same bits) as splitk_reduce_k, whose 16 split groups each hold <= 1 slab here.
+// splitk_reduce_k would leave 16 - S of every 16 threads idle and run ~n4/16 tiny blocks.
+constexpr int FLAT_MAX_SPLITS = 16;
+__global__ __launch_bounds__(NT) void splitk_reduce_flat_k(const float4* __restrict__ slab, int splits, long n4,
+                                                          float4* __restrict__ dst) {
+  const long i = blockIdx.x * (long)NT + threadIdx.x;
+  if (i >= n4) return;
+  float4 v[FLAT_MAX_SPLITS];
+#pragma unroll
+  for (int sp = 0; sp < FLAT_MAX_SPLITS; ++sp)
+    if (sp < splits) v[sp] = slab[(size_t)sp * n4 + i];
+  float4 d = dst[i];
+#pragma unroll
+  for (int sp = 0; sp < FLAT_MAX_SPLITS; ++sp)
+    if (sp < splits) {
+      d.x += v[sp].x; d.y += v[sp].y; d.z += v[sp].z; d.w += v[sp].w;
+    }
+  dst[i] = d;
+}
+
 }  // namespace
 
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s) {
   if (n % 4 || splits < 1) return hipErrorInvalidValue;
   const long n4 = n / 4;
+  if (splits <= FLAT_MAX_SPLITS && n4 >= 32 * NT) {
+    hipLaunchKernelGGL(splitk_reduce_flat_k, dim3((unsigned)((n4 + NT - 1) / NT)), dim3(NT), 0, s,
+                       reinterpret_cast<const float4*>(slab), splits, n4, reinterpret_cast<float4*>(dst));
+    return hipGetLastError();
+  }
   const long g = (n4 + RED_E - 1) / RED_E;
   hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab),
                      splits, n4, reinterpret_cast<float4*>(dst));

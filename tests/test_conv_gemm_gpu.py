@@ -339,3 +339,20 @@ def test_packed_tap_stem(H, n, h, cin, cout, k, padding):
     dw8 = torch.zeros(H.stem4_weight_shape(wshape), device=dev)
     H.conv_wgrad_stem4(x4.bfloat16(), dy.bfloat16(), dw8, k, (2, 2), padding)
     close(dw8[:, :k, :cin], gw, 1e-4, 2e-5)
+
+
+@pytest.mark.parametrize("splits,n", [(3, 1 << 16), (16, 3 << 14), (3, 4096), (40, 1 << 15)])
+def test_splitk_reduce_paths(H, splits, n):
+    """dst += sum of the split slabs in split order: the flat kernel (<= 16 splits, large n)
+    and the split-group kernel (small n, or many splits) against a sequential torch sum."""
+    slab = torch.randn(splits, n, device=dev)
+    dst = torch.randn(n, device=dev)
+    want = dst.clone()
+    for sp in range(splits):
+        want = want + slab[sp]
+    H._C().splitk_reduce(H._ptr(slab), splits, n, H._ptr(dst), H.stream_handle())
+    torch.cuda.synchronize()
+    if splits <= 16:
+        assert torch.equal(dst, want)  # same order: bitwise
+    else:
+        close(dst, want, 1e-5, 1e-6)
