@@ -17,7 +17,8 @@ hipError_t bn_finalize(const float* part, int T, int C, float count, const float
 hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const float* st2, int res_mode,
                     int relu, uint16_t* y, long M, int C, hipStream_t s);
 // inference: y = act(x*scale + shift) with scale/shift from the moving statistics
-// backward, pass 1: dz = dy * [y > 0] (relu_mask) ; per-block partial sums of dz and
+// backward, pass 1: dz = dy * [y > 0] (relu_mask 1; relu_mask 2: y recomputed as
+// bf16(relu(x * sc + sh)) from x and st, bitwise the stored bn_apply output, y unread) ; per-block partial sums of dz and
 // dz * xhat -> part [T][2][C]; optionally writes dz (bf16).  Returns T via *T_out.
 hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
                          const float* st, uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s);

@@ -42,6 +42,12 @@ inline int grid_for(long work, int per_block = NT, int cap = 8192) {
 }
 
 // ---- BatchNorm -------------------------------------------------------------------------
+// relu(BN(x)) rounded to bf16 exactly as bn_apply stores it: ReLU masks recomputed from
+// the BN input (relu_mask == 2 below, the stem kernels) equal those of the stored output.
+__device__ __forceinline__ void bn_relu8(const float* x, const float* sc, const float* sh, float* y) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) y[e] = bf2f(f2bf(fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f)));
+}
 // Sum the partials [T][2][C] over T in fp64 for the 8 channels c0..c0+7 of this block.
 // Thread t owns value v = t % 16 of the 16-value record (8 sums, 8 second statistics)
 // and rows t / 16 + 16 k: up to 16 of its loads are in flight at once (the ResNet-18
@@ -145,25 +151,32 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
   const int rpi = NT / cg;  // rows per iteration
   const int g = t % cg, rr = t / cg;
   const int c = g * 8;
-  float s0[8], s1[8], mean[8], inv[8];
+  float s0[8], s1[8], mean[8], inv[8], sc[8], sh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
   ld8f(st + c, mean);
   ld8f(st + C + c, inv);
+  if (relu_mask == 2) {
+    ld8f(st + 2 * C + c, sc);
+    ld8f(st + 3 * C + c, sh);
+  }
   const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   if (rr < rpi) {
     for (long row = r0 + rr; row < r1; row += rpi) {
       const long off = (row * C + c) / 8;
       float d[8], xv[8];
       unpack8(reinterpret_cast<const uint4*>(dy)[off], d);
+      unpack8(reinterpret_cast<const uint4*>(x)[off], xv);
       if (relu_mask) {
         float yv[8];
-        unpack8(reinterpret_cast<const uint4*>(y)[off], yv);
+        if (relu_mask == 2)
+          bn_relu8(xv, sc, sh, yv);
+        else
+          unpack8(reinterpret_cast<const uint4*>(y)[off], yv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
         if (dz_out) reinterpret_cast<uint4*>(dz_out)[off] = pack8(d);
       }
-      unpack8(reinterpret_cast<const uint4*>(x)[off], xv);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         s0[e] += d[e];
@@ -214,13 +227,20 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_k(const uint16_t* __restrict_
     const int c = (int)((i * 8) % C);
     float d[8], xv[8], mean[8], inv[8], a[8], b[8], cc[8];
     unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
     if (relu_mask) {
       float yv[8];
-      unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+      if (relu_mask == 2) {
+        float sc[8], sh[8];
+        ld8f(st + 2 * C + c, sc);
+        ld8f(st + 3 * C + c, sh);
+        bn_relu8(xv, sc, sh, yv);
+      } else {
+        unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
     }
-    unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
     ld8f(st + c, mean);
     ld8f(st + C + c, inv);
     ld8f(co + c, a);
@@ -318,10 +338,6 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_k(const uint16_t* __restrict__
 // max / argmax equal the unfused pair's.  Backward: the pool's gradient routing and the
 // ReLU mask are recomputed from (dy_pool, argmax, x, BN scale/shift) in both BN-backward
 // passes, so neither the 4x larger un-pooled gradient nor the ReLU output is stored.
-__device__ __forceinline__ void bn_relu8(const float* x, const float* sc, const float* sh, float* y) {
-#pragma unroll
-  for (int e = 0; e < 8; ++e) y[e] = bf2f(f2bf(fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f)));
-}
 
 __global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_k(const uint16_t* __restrict__ x,
                                                             const float* __restrict__ st, PoolGeo g,

@@ -806,10 +806,12 @@ class NativeGraphEngine(Engine):
             xt.written = True
             H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
 
-    def _bn_backward(self, bn, dy, ymask, relu, dz_out=None):
+    def _bn_backward(self, bn, dy, ymask, relu, dz_out=None, mask_from_x=False):
         """BatchNorm backward of node ``bn`` for upstream gradient dy (masked by
         [ymask > 0] when relu); dgamma/dbeta into the gradient sinks, dx into the input's
-        gradient; optionally also writes the masked dy to dz_out."""
+        gradient; optionally also writes the masked dy to dz_out.  ``mask_from_x``: the
+        output is bn_apply(x, relu) with no residual, so the kernels recompute the ReLU
+        mask from x (already read) instead of reading the stored output."""
         l = bn.layer
         C_ = self.C
         s = H.stream_handle()
@@ -818,14 +820,15 @@ class NativeGraphEngine(Engine):
         M = int(np.prod(x.shape[:-1]))
         st, part, co, Tn = bn.attrs["st"], bn.attrs["part"], bn.attrs["co"], bn.attrs["T"]
         ym = ymask.data_ptr() if relu else 0
-        C_.bn_bwd_reduce(dy.data_ptr(), ym, int(relu), x.buf.data_ptr(), st.data_ptr(),
+        mode = (2 if mask_from_x else 1) if relu else 0
+        C_.bn_bwd_reduce(dy.data_ptr(), ym, mode, x.buf.data_ptr(), st.data_ptr(),
                          dz_out.data_ptr() if (dz_out is not None and relu) else 0, part.data_ptr(), Tn, M, C, s)
         C_.bn_bwd_finalize(part.data_ptr(), Tn, C, float(M), st.data_ptr(), 0,
                            self.gviews[id(l.gamma)].data_ptr() if l.gamma is not None else 0,
                            self.gviews[id(l.beta)].data_ptr() if l.beta is not None else 0, co.data_ptr(), s)
         dx, fin = self._grad_target(x)
         if dx is not None:
-            C_.bn_bwd_apply(dy.data_ptr(), ym, int(relu), x.buf.data_ptr(), st.data_ptr(), co.data_ptr(),
+            C_.bn_bwd_apply(dy.data_ptr(), ym, mode, x.buf.data_ptr(), st.data_ptr(), co.data_ptr(),
                             dx.data_ptr(), M, C, s)
             if fin:
                 fin()
@@ -834,7 +837,8 @@ class NativeGraphEngine(Engine):
         if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None:
             return  # handled by the fused Add / MaxPool
         y = nd.out.root()
-        self._bn_backward(nd, y.grad, y.buf, bool(nd.attrs.get("relu")))
+        self._bn_backward(nd, y.grad, y.buf, bool(nd.attrs.get("relu")),
+                          mask_from_x=env.get_bool("DAMD_BN_MASK_FROM_X", True))
 
     def _bwd_Activation(self, nd):
         x = nd.inputs[0].root()

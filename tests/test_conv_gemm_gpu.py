@@ -356,3 +356,25 @@ def test_splitk_reduce_paths(H, splits, n):
         assert torch.equal(dst, want)  # same order: bitwise
     else:
         close(dst, want, 1e-5, 1e-6)
+
+
+@pytest.mark.parametrize("M,c", [(3000, 64), (1000, 256)])
+def test_bn_bwd_relu_mask_from_x(H, M, c):
+    """relu_mask 2 (mask recomputed from x and the BN scale/shift) == relu_mask 1 reading
+    y = bn_apply(x, relu): bitwise partials, dgamma/dbeta and dx."""
+    C_ = H._C()
+    x = rb(rnd(M, c, scale=2.0, seed=51)).bfloat16()
+    st = torch.stack([rnd(c, seed=52) * 0.1, rnd(c, seed=53).abs() + 0.5,
+                      rnd(c, seed=54).abs() + 0.5, rnd(c, seed=55)]).float()
+    y = torch.empty_like(x)
+    H.bn_apply(x, st, y, relu=True)
+    dy = rb(rnd(M, c, seed=56)).bfloat16()
+    T = C_.bn_bwd_blocks(M, c)
+    out = []
+    for mode in (1, 2):
+        part, co = torch.zeros(T, 2, c, device=dev), torch.zeros(3, c, device=dev)
+        dg, db, dx = torch.zeros(c, device=dev), torch.zeros(c, device=dev), torch.empty_like(x)
+        H.bn_bwd(dy, y if mode == 1 else None, mode, x, st, part, co, dx, dgamma=dg, dbeta=db)
+        out.append((part, dg, db, dx))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
