@@ -871,6 +871,39 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
+  if (Cp == 4 && Cin == 3 && x_u8 && HW % 4 == 0) {
+    // RGB uint8 rows -> packed 4-channel bf16: one thread per 4 pixels of one row, the 12
+    // source bytes as three aligned dword loads (byte loads moved 64 B per wave
+    // instruction), two 16-byte stores
+    const long total = (long)per * HW / 4;
+    for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+      const long pr = 4 * i;
+      const int p = (int)(pr % HW), r = (int)(pr / HW);
+      const bool valid = wrap || base + r < n;
+      const long row = valid ? (base + r) % n : 0;
+      uint32_t w[3] = {0u, 0u, 0u};
+      if (valid) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>((const uint8_t*)x + (row * HW + p) * 3);
+        w[0] = src[0];
+        w[1] = src[1];
+        w[2] = src[2];
+      }
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const int b = 3 * k + c;
+          v[4 * k + c] = (float)((w[b >> 2] >> (8 * (b & 3))) & 0xffu) / scale;
+        }
+        v[4 * k + 3] = 0.f;
+      }
+      if (p == 0) yb[r] = valid ? labels[row] : -1;
+      reinterpret_cast<uint4*>(xb)[2 * i] = pack8(v);
+      reinterpret_cast<uint4*>(xb)[2 * i + 1] = pack8(v + 8);
+    }
+    return;
+  }
   if (Cp == 4) {
     // packed-tap stem input (4 channels): one thread per 2 pixels, one 16-byte store
     const long total = (long)per * HW / 2;

@@ -383,3 +383,18 @@ def test_rccl_allreduce_captured_in_step_graph(which):
     for a, b in zip(wa, wb):
         np.testing.assert_allclose(a, b, **tol)
     np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-4)
+
+
+def test_u8_batch_gather_matches_float_feed():
+    """k/255 inputs kept on the device as uint8 (4-pixel dword gather into the packed
+    4-channel stem layout) == the fp32 device copy: one step, same weights and loss."""
+    x, y = _data(64, (32, 32, 3), 10, seed=8)
+    tf.keras.backend.clear_session()
+    init = _small_resnet().get_weights()
+    wa, ha, ea = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9)
+    wb, hb, eb = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9,
+                        extra_env={"DAMD_X_U8": "0"})
+    assert ea == eb == "native_graph"
+    for a, b in zip(wa, wb):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-6)
