@@ -56,5 +56,9 @@ hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipS
 // of rows_per_block rows: [ceil(M / rows_per_block)][2][N]
 hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
                          float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s);
+// fp32 split-K epilogue (dense logits): out[m][n] = relu?(sum_s slab[s][m][n] + bias[n]),
+// slab [splits][M][N], out pitch ldc, fixed summation order
+hipError_t splitk_finish_f32(const float* slab, int splits, int M, int N, const float* bias, int relu, float* out,
+                             int ldc, hipStream_t s);
 
 }  // namespace damd

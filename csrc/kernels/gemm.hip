@@ -623,7 +623,40 @@ __global__ __launch_bounds__(NT) void splitk_reduce_flat_k(const float4* __restr
   dst[i] = d;
 }
 
+// fp32-output split-K epilogue: one thread per 4 columns of one row, splits summed in
+// order, then bias / ReLU (the small-M dense GEMMs: logits of a 64-row batch)
+__global__ __launch_bounds__(NT) void splitk_finish_f32_k(const float* __restrict__ slab, int S, int M, int N,
+                                                         const float* __restrict__ bias, int relu,
+                                                         float* __restrict__ out, int ldc) {
+  const int n4 = N / 4;
+  const long i = blockIdx.x * (long)NT + threadIdx.x;
+  if (i >= (long)M * n4) return;
+  const int m = (int)(i / n4), n = 4 * (int)(i % n4);
+  const size_t plane = (size_t)M * N;
+  float4 v = *reinterpret_cast<const float4*>(slab + (size_t)m * N + n);
+  for (int sp = 1; sp < S; ++sp) {
+    const float4 q = *reinterpret_cast<const float4*>(slab + sp * plane + (size_t)m * N + n);
+    v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+  }
+  if (bias) {
+    v.x += bias[n]; v.y += bias[n + 1]; v.z += bias[n + 2]; v.w += bias[n + 3];
+  }
+  if (relu) {
+    v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+  }
+  *reinterpret_cast<float4*>(out + (size_t)m * ldc + n) = v;
+}
+
 }  // namespace
+
+hipError_t splitk_finish_f32(const float* slab, int splits, int M, int N, const float* bias, int relu, float* out,
+                             int ldc, hipStream_t s) {
+  if (splits < 1 || N % 4 || ldc % 4) return hipErrorInvalidValue;
+  const long n = (long)M * (N / 4);
+  hipLaunchKernelGGL(splitk_finish_f32_k, dim3((unsigned)((n + NT - 1) / NT)), dim3(NT), 0, s, slab, splits, M, N,
+                     bias, relu, out, ldc);
+  return hipGetLastError();
+}
 
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s) {
   if (n % 4 || splits < 1) return hipErrorInvalidValue;

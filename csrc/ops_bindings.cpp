@@ -62,6 +62,12 @@ void register_kernel_ops(py::module_& m) {
                               P_<float>(stats), rb, P_<uint16_t>(out), ldc, P_<ihipStream_t>(stream)),
           "splitk_finish");
   });
+  m.def("splitk_finish_f32", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, int relu, uintptr_t out,
+                                int ldc, uintptr_t stream) {
+    check(damd::splitk_finish_f32(P_<const float>(slab), splits, M, N, P_<const float>(bias), relu, P_<float>(out),
+                                  ldc, P_<ihipStream_t>(stream)),
+          "splitk_finish_f32");
+  });
   m.def("splitk_reduce", [](uintptr_t slab, int splits, long n, uintptr_t dst, uintptr_t stream) {
     check(damd::splitk_reduce(P_<const float>(slab), splits, n, P_<float>(dst), P_<ihipStream_t>(stream)),
           "splitk_reduce");

@@ -444,7 +444,8 @@ class NativeGraphEngine(Engine):
             elif k == "Dense":
                 l = nd.layer
                 kin, units = l.kernel.shape
-                ws = max(ws, H.wgrad_workspace_elems(kin, _pad8(units), self.B))
+                ws = max(ws, H.wgrad_workspace_elems(kin, _pad8(units), self.B),
+                         H.dense_workspace_elems(self.B, _pad8(units), kin))
                 if nd.attrs.get("logits") and units % 8:
                     up = _pad8(units)
                     nd.attrs["w_pad"] = torch.zeros(kin, up, dtype=torch.bfloat16, device=dev)
@@ -760,7 +761,7 @@ class NativeGraphEngine(Engine):
                 bias = nd.attrs["b_pad"]
         relu = getattr(l.activation, "__name__", "linear") == "relu"
         out = self.logits if nd.attrs.get("logits") else nd.out.root().buf
-        H.dense_fwd(x2, wb, out, bias=bias, relu=relu)
+        H.dense_fwd(x2, wb, out, bias=bias, relu=relu, workspace=self.gemm_ws)
 
     # backward ops
     def _dy(self, nd):
@@ -943,7 +944,7 @@ class NativeGraphEngine(Engine):
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written
             xt.written = True
-            H.dense_dgrad(dy, wb, xt.grad.view(xt.grad.shape[0], -1), accumulate=acc)
+            H.dense_dgrad(dy, wb, xt.grad.view(xt.grad.shape[0], -1), accumulate=acc, workspace=self.gemm_ws)
 
     # --- driver ---------------------------------------------------------------------------------
     def _capture(self):

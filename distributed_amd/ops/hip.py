@@ -241,8 +241,38 @@ def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=Non
 
 
 # ---- dense -------------------------------------------------------------------------------
-def dense_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, relu=False, stats=None):
-    """out[M,N] = x[M,K] @ w[K,N] (+bias)(relu); x, w bf16; out bf16 or fp32."""
+# Small-M dense GEMMs (a 64-row batch against a 512 x 1000 classifier) give 4-8 output
+# tiles: 4-8 busy CUs walking 8-16 serial k-steps (23-32 us on MI355X for <= 66 MFLOP).
+# They are split over K into fp32 slabs (one k-step or two per workgroup) and finished by
+# a fixed-order reduction kernel with the bias / ReLU / accumulate epilogue.
+DENSE_SPLIT_MAX_TILES = 32
+DENSE_SPLIT_TARGET_WG = 128
+
+
+def dense_split_plan(M: int, N: int, K: int) -> Tuple[int, int]:
+    """(splits, k_per_split) of a dense forward / backprop-input GEMM [M,N] over K."""
+    t = pick_tile(N)
+    bm, bn = (256, 64) if t == 1 else (128, 128)
+    tiles = -(-M // bm) * -(-N // bn)
+    kfull = -(-K // BK) * BK
+    if tiles > DENSE_SPLIT_MAX_TILES or K < 2 * BK:
+        return 1, kfull
+    splits = max(1, min(-(-DENSE_SPLIT_TARGET_WG // tiles), K // BK))
+    kps = -(-(-(-K // splits)) // BK) * BK
+    return -(-K // kps), kps
+
+
+def dense_workspace_elems(M: int, N: int, K: int) -> int:
+    """fp32 workspace of the split forward (x[M,K] @ w[K,N]) and backprop-input GEMMs."""
+    s1, _ = dense_split_plan(M, N, K)
+    s2, _ = dense_split_plan(M, K, N)
+    return max(s1 * M * N if s1 > 1 else 0, s2 * M * K if s2 > 1 else 0)
+
+
+def dense_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, relu=False, stats=None,
+              workspace: Optional[torch.Tensor] = None):
+    """out[M,N] = x[M,K] @ w[K,N] (+bias)(relu); x, w bf16; out bf16 or fp32.  With a
+    workspace, under-filled shapes run split-K (dense_split_plan)."""
     M, K = x.shape
     K2, N = w.shape
     assert K == K2 and tuple(out.shape) == (M, N)
@@ -250,6 +280,17 @@ def dense_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, re
     _chk(w, torch.bfloat16, "w")
     if K % 8 or N % 8:
         raise ValueError("dense_fwd: K and N must be multiples of 8 (pad the layer)")
+    splits, kps = dense_split_plan(M, N, K)
+    if splits > 1 and stats is None and workspace is not None and workspace.numel() >= splits * M * N:
+        gemm(x, w, workspace, amode=A_KC, bmode=B_NC, M=M, N=N, K=K, lda=K, ldb=N, ldc=N, epi=E_SLAB,
+             splits=splits, k_per_split=kps)
+        if out.dtype == torch.float32:
+            _C().splitk_finish_f32(_ptr(workspace), splits, M, N, _ptr(bias), int(relu), _ptr(out), N,
+                                   stream_handle())
+        else:
+            _C().splitk_finish(_ptr(workspace), splits, M, N, _ptr(bias), 0, int(relu), 0, FINISH_RB, _ptr(out), N,
+                               stream_handle())
+        return
     epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0)
     epi |= E_BF16 if out.dtype == torch.bfloat16 else 0
     if stats is not None:
@@ -257,14 +298,22 @@ def dense_fwd(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, bias=None, re
     gemm(x, w, out, amode=A_KC, bmode=B_NC, M=M, N=N, K=K, lda=K, ldb=N, ldc=N, epi=epi, bias=bias, stats=stats)
 
 
-def dense_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, accumulate=False):
-    """dx[M,K] (+)= dy[M,N] @ w[K,N]^T (bf16 out)."""
+def dense_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, accumulate=False,
+                workspace: Optional[torch.Tensor] = None):
+    """dx[M,K] (+)= dy[M,N] @ w[K,N]^T (bf16 out); split-K with a workspace like dense_fwd."""
     M, N = dy.shape
     K, N2 = w.shape
     assert N == N2 and tuple(dx.shape) == (M, K)
     _chk(dy, torch.bfloat16, "dy")
     _chk(w, torch.bfloat16, "w")
     _chk(dx, torch.bfloat16, "dx")
+    splits, kps = dense_split_plan(M, K, N)
+    if splits > 1 and workspace is not None and workspace.numel() >= splits * M * K and K // 8 <= 256:
+        gemm(dy, w, workspace, amode=A_KC, bmode=B_KC, M=M, N=K, K=N, lda=N, ldc=K, epi=E_SLAB, kc=N,
+             splits=splits, k_per_split=kps)
+        _C().splitk_finish(_ptr(workspace), splits, M, K, 0, _ptr(dx) if accumulate else 0, 0, 0, FINISH_RB,
+                           _ptr(dx), K, stream_handle())
+        return
     epi = E_BF16 | (E_ADD if accumulate else 0)
     gemm(dy, w, dx, amode=A_KC, bmode=B_KC, M=M, N=K, K=N, lda=N, ldc=K, epi=epi, kc=N,
          R=dx if accumulate else None)

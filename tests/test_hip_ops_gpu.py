@@ -279,3 +279,25 @@ def test_gap_xent_colsum_sgd(H):
     close(V, vn, 1e-6, 1e-7)
     close(P, p0 + 0.9 * vn - 0.1 * G, 1e-6, 1e-7)
     assert torch.equal(Pb, P.bfloat16())
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 512, 1008), (64, 5408, 64), (64, 64, 16)])
+@pytest.mark.parametrize("out_bf16", [False, True])
+def test_dense_split_k(H, M, K, N, out_bf16):
+    """Split-K dense forward / backprop-input (workspace given, small-M shapes) against the
+    fp32 reference, including the bias/ReLU and accumulate epilogues of the finish kernels."""
+    splits, _ = H.dense_split_plan(M, N, K)
+    assert splits > 1
+    ws = torch.empty(H.dense_workspace_elems(M, N, K), device=dev)
+    x = rb(rnd(M, K, seed=11))
+    w = rb(rnd(K, N, scale=0.1, seed=12))
+    b = rnd(N, seed=13)
+    out = torch.empty(M, N, device=dev, dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    H.dense_fwd(x.bfloat16(), w.bfloat16(), out, bias=b, relu=True, workspace=ws)
+    close(out, (x @ w + b).relu(), 1e-2 if out_bf16 else 1e-4, 4e-3 if out_bf16 else 1e-5)
+    dy = rb(rnd(M, N, seed=14))
+    dx = torch.empty(M, K, device=dev, dtype=torch.bfloat16)
+    H.dense_dgrad(dy.bfloat16(), w.bfloat16(), dx, workspace=ws)
+    close(dx, dy @ w.t(), 1e-2, 4e-3)
+    H.dense_dgrad(dy.bfloat16(), w.bfloat16(), dx, accumulate=True, workspace=ws)
+    close(dx, 2 * (dy @ w.t()), 1e-2, 8e-3)
