@@ -959,12 +959,15 @@ __global__ __launch_bounds__(256) void flush_pending(float* __restrict__ P, floa
     ctrl->acc_count = c.acc_count + G[OFF_CNT];
     for (int i = NPARAM; i < NGRAD; ++i) G[i] = 0.f;
   }
-  // W1 is back inside P: the last block to arrive clears wpar (every block has read it by
-  // then), so the flush is one launch instead of a follow-up fix-up kernel
+  // W1 is back inside P: the last block to arrive clears wpar, so the flush is one launch
+  // instead of a follow-up fix-up kernel.  Every block's threads consumed their load of
+  // ctrl (the loop above used c.wpar) before the barrier, so the ticket needs no fence --
+  // an agent-scope fence per block (an L2 write-back on the multi-XCD part) made this
+  // launch 13.8 us instead of ~5.
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(&ctrl->flush_ticket, 1) == (int)gridDim.x - 1) {
+    if (__hip_atomic_fetch_add(&ctrl->flush_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        (int)gridDim.x - 1) {
       ctrl->wpar = 0;
       ctrl->flush_ticket = 0;
     }

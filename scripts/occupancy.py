@@ -6,7 +6,9 @@ SIMD and workgroups per CU those allow on gfx950 (MI355X: 4 SIMDs per CU, a 512-
 unified VGPR+AGPR file per SIMD lane allocated in 8-register granules, at most 8 waves per
 SIMD; 160 KiB LDS per CU), which resource binds, and the launch's workgroup count against
 the 256 CUs (one full wave of workgroups = 256 x workgroups-per-CU).  Mean duration per
-launch is from the same trace.
+launch is from the same trace.  Caveat: the trace's LDS_Block_Size can read 0 for kernels
+whose LDS is all dynamic (the fused MNIST kernels size theirs at launch), so their LDS
+limit is not applied here.
 
 usage: python scripts/occupancy.py <kernel_trace.csv> [out.txt]
 """
