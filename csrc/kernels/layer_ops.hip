@@ -48,25 +48,27 @@ __device__ __forceinline__ void bn_relu8(const float* x, const float* sc, const 
 #pragma unroll
   for (int e = 0; e < 8; ++e) y[e] = bf2f(f2bf(fmaxf(fmaf(x[e], sc[e], sh[e]), 0.f)));
 }
-// Sum the partials [T][2][C] over T in fp64 for the 8 channels c0..c0+7 of this block.
-// Thread t owns value v = t % 16 of the 16-value record (8 sums, 8 second statistics)
-// and rows t / 16 + 16 k: up to 16 of its loads are in flight at once (the ResNet-18
-// partial counts, T <= 1024, take one or four such batches), then a two-level LDS tree
-// (16 x 16, fixed order: deterministic).  A per-value wave butterfly on doubles costs
-// ~200 dependent cross-lane permutes -- most of an 8 us kernel; this is ~2 latencies.
+// Sum the partials [T][2][C] over T in fp64 for the 8 channels c0..c0+7 of this block
+// (FT = 1024 threads).  Thread t owns value v = t % 16 of the 16-value record (8 sums, 8
+// second statistics) and rows t / 16 + 64 k: 64 row slices with up to 16 loads each in
+// flight, so the ResNet-18 partial counts (T = 784..1024; 3136 at the stem) take one
+// batch of loads (four with the 256-thread version: ~1 us of latency each), then a
+// three-level LDS tree (64 -> 16 -> 1 slices, fixed order: deterministic).
 // On return sums[j] (j < 8) is the channel sum, sums[8 + j] the second statistic.
+constexpr int FT = 1024, FSL = FT / 16;
 __device__ __forceinline__ void reduce_partials8(const float* __restrict__ part, int T, int C, int c0,
                                                  double* sums) {
-  __shared__ double red[16][17];
+  __shared__ double red[FSL][17];
+  __shared__ double red2[16][17];
   const int t = threadIdx.x, v = t & 15, sl = t >> 4;
   const float* p = part + (v < 8 ? c0 + v : C + c0 + (v - 8));
   const size_t row = (size_t)2 * C;
   double a = 0.0;
-  for (int i0 = sl; i0 < T; i0 += 16 * 16) {
+  for (int i0 = sl; i0 < T; i0 += FSL * 16) {
     float f[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int i = i0 + 16 * u;
+      const int i = i0 + FSL * u;
       f[u] = p[(size_t)min(i, T - 1) * row];
       f[u] = i < T ? f[u] : 0.f;
     }
@@ -75,16 +77,24 @@ __device__ __forceinline__ void reduce_partials8(const float* __restrict__ part,
   }
   red[sl][v] = a;
   __syncthreads();
-  if (t < 16) {
-    double s = 0.0;
+  if (t < 256) {
+    const int g = t >> 4;
+    double b = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) s += red[q][t];
-    sums[t] = s;
+    for (int q = 0; q < FSL / 16; ++q) b += red[g * (FSL / 16) + q][v];
+    red2[g][v] = b;
+  }
+  __syncthreads();
+  if (t < 16) {
+    double s2 = 0.0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s2 += red2[q][t];
+    sums[t] = s2;
   }
   __syncthreads();
 }
 
-__global__ __launch_bounds__(NT) void bn_finalize_k(const float* part, int T, int C, float count,
+__global__ __launch_bounds__(FT) void bn_finalize_k(const float* part, int T, int C, float count,
                                                     const float* gamma, const float* beta, float eps, float mom,
                                                     float* rmean, float* rvar, float* st) {
   __shared__ double sums[16];
@@ -203,7 +213,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
   }
 }
 
-__global__ __launch_bounds__(NT) void bn_bwd_finalize_k(const float* part, int T, int C, float count,
+__global__ __launch_bounds__(FT) void bn_bwd_finalize_k(const float* part, int T, int C, float count,
                                                         const float* st, float* dgamma, float* dbeta, float* co) {
   __shared__ double sums[16];
   const int c0 = blockIdx.x * 8;
@@ -1003,7 +1013,7 @@ hipError_t unpad_add(const float* src, int R, int C1, int C2, int C1p, int C2p, 
 hipError_t bn_finalize(const float* part, int T, int C, float count, const float* gamma, const float* beta, float eps,
                        float momentum, float* rmean, float* rvar, float* st, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_finalize_k, dim3(C / 8), dim3(NT), 0, s, part, T, C, count, gamma, beta, eps,
+  hipLaunchKernelGGL(bn_finalize_k, dim3(C / 8), dim3(FT), 0, s, part, T, C, count, gamma, beta, eps,
                      momentum, rmean, rvar, st);
   return hipGetLastError();
 }
@@ -1034,7 +1044,7 @@ hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const f
                            float* dgamma, float* dbeta, float* co, hipStream_t s) {
   (void)gamma;
   if (C % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3(C / 8), dim3(NT), 0, s, part, T, C, count, st, dgamma, dbeta,
+  hipLaunchKernelGGL(bn_bwd_finalize_k, dim3(C / 8), dim3(FT), 0, s, part, T, C, count, st, dgamma, dbeta,
                      co);
   return hipGetLastError();
 }
