@@ -100,7 +100,7 @@ def pick_splits(M: int, N: int, K: int, tile: int, target_wg: int = 1024) -> Tup
 # weight-gradient split-K: every split stores its fp32 partial tile to a slab and one
 # reduce kernel adds the slabs into the gradient in fixed order (deterministic; fp32
 # atomics from hundreds of blocks on the same addresses serialise at the memory side)
-WGRAD_TARGET_WG = 512          # 2 workgroups per CU
+WGRAD_TARGET_WG = int(os.environ.get("DAMD_WGRAD_TARGET_WG", 512))  # 2 workgroups per CU
 WGRAD_SLAB_MAX = 64 << 20      # bytes of slab per GEMM
 
 
@@ -119,8 +119,8 @@ def wgrad_plan(M: int, N: int, K: int) -> Tuple[int, int, int]:
 # bf16-output GEMMs (conv fwd / dgrad) whose tile count leaves CUs idle are split over K
 # into fp32 slabs; splitk_finish then applies the epilogue (bias, residual, ReLU, BN
 # statistics per FINISH_RB rows, bf16 store)
-SPLIT_MIN_TILES = 320
-SPLIT_TARGET_WG = 384
+SPLIT_MIN_TILES = int(os.environ.get("DAMD_SPLIT_MIN_TILES", 320))
+SPLIT_TARGET_WG = int(os.environ.get("DAMD_SPLIT_TARGET_WG", 384))
 FINISH_RB = 16
 
 
