@@ -120,7 +120,11 @@ def main():
     run(args.steps)
     if engine.name == "fused_convnet":
         engine._flush()  # the last deferred SGD update is part of the timed work
-    engine.sync()
+    if not on_gpu:
+        engine.sync()
+    # on the GPU the device-wide synchronize waits for every stream, the engines' own
+    # (C++-created) step streams included: a second, engine-level host wait would only
+    # add a round trip to the timed window
     device_sync()
     barrier()
     t1 = time.perf_counter()
