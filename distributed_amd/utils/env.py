@@ -38,7 +38,7 @@ def get_str(name: str, default: str) -> str:
 #   DAMD_NATIVE_GRAPH      0/1                 allow the native graph engine (HIP plan + graph, default 1)
 #   DAMD_GRAPH             0/1                 capture steps into hipGraphs (default 1)
 #   DAMD_GRAPH_STEPS       int                 steps per captured graph (default 20)
-#   DAMD_PP                1..4                pooled positions per fused slice (default 4)
+#   DAMD_PP                1..4                pooled positions per fused slice (default 3)
 #   DAMD_DEBUG_SYNC        0/1                 synchronize + error-check after every engine chunk
 #   DAMD_COMM              rccl | torch | gloo | auto   data-plane communicator on GPU (default auto=rccl;
 #                          gloo stages device tensors through host memory: test/debug only)

@@ -67,10 +67,13 @@ def _engine(model, B):
     return eng
 
 
-@pytest.mark.parametrize("B", [64, 40, 100])
-def test_one_step_matches_reference(B, monkeypatch):
+@pytest.mark.parametrize("B,pp", [(64, 3), (40, 3), (100, 3), (64, 4), (100, 2), (64, 1)])
+def test_one_step_matches_reference(B, pp, monkeypatch):
+    """pp = pooled positions per fused slice (DAMD_PP; 3 is the default: 57 slices, the
+    last one partial)."""
     _need_gpu()
     monkeypatch.setenv("DAMD_GRAPH", "0")
+    monkeypatch.setenv("DAMD_PP", str(pp))
     lr = 0.5
     m = _model(lr=lr)
     x, y = _data(300)
