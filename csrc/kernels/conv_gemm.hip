@@ -468,6 +468,7 @@ hipError_t launch_epi(const GemmArgs& a, int epi, int splits, int kb, hipStream_
     case E_BF16: return launch_t<BM, BN, DG, E_BF16>(a, splits, kb, s);
     case E_BIAS | E_BF16: return launch_t<BM, BN, DG, E_BIAS | E_BF16>(a, splits, kb, s);
     case E_BIAS | E_RELU | E_BF16: return launch_t<BM, BN, DG, E_BIAS | E_RELU | E_BF16>(a, splits, kb, s);
+    case E_RELU | E_BF16: return launch_t<BM, BN, DG, E_RELU | E_BF16>(a, splits, kb, s);
     case E_SLAB: return launch_t<BM, BN, DG, E_SLAB>(a, splits, kb, s);
     case E_BF16 | E_STATS: return launch_t<BM, BN, DG, E_BF16 | E_STATS>(a, splits, kb, s);
     case E_BIAS | E_BF16 | E_STATS: return launch_t<BM, BN, DG, E_BIAS | E_BF16 | E_STATS>(a, splits, kb, s);

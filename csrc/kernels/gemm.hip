@@ -478,6 +478,8 @@ hipError_t launch_epi(const GemmArgs& a, int epi, int splits, hipStream_t s) {
     case E_BIAS | E_RELU: return launch_t<BM, BN, AM, BMo, E_BIAS | E_RELU>(a, splits, s);
     case E_BIAS | E_BF16: return launch_t<BM, BN, AM, BMo, E_BIAS | E_BF16>(a, splits, s);
     case E_BIAS | E_RELU | E_BF16: return launch_t<BM, BN, AM, BMo, E_BIAS | E_RELU | E_BF16>(a, splits, s);
+    case E_RELU: return launch_t<BM, BN, AM, BMo, E_RELU>(a, splits, s);
+    case E_RELU | E_BF16: return launch_t<BM, BN, AM, BMo, E_RELU | E_BF16>(a, splits, s);
     case E_ATOMIC: return launch_t<BM, BN, AM, BMo, E_ATOMIC>(a, splits, s);
     case E_SLAB: return launch_t<BM, BN, AM, BMo, E_SLAB>(a, splits, s);
     case E_BF16 | E_STATS: return launch_t<BM, BN, AM, BMo, E_BF16 | E_STATS>(a, splits, s);
