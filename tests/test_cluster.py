@@ -52,3 +52,30 @@ def test_resolve_precedence():
     assert s.source == "torchrun" and s.num_workers == 4 and s.rank == 3 and s.local_rank == 3
     s = cluster.resolve({})
     assert s.num_workers == 1 and s.is_chief
+
+
+def test_tf_config_roundtrip_property():
+    """Any worker list (list or R's auto-unboxed scalar for one worker) and any valid index
+    (int or R's length-1 vector) parses back to the same cluster (hypothesis-drawn)."""
+    hyp = pytest.importorskip("hypothesis")
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    host = st.from_regex(r"[a-z][a-z0-9\-]{0,14}(\.[a-z0-9]{1,8}){0,2}", fullmatch=True)
+    port = st.integers(1, 65535)
+
+    @settings(max_examples=150, deadline=None, derandomize=True, database=None)
+    @given(hosts=st.lists(st.tuples(host, port), min_size=1, max_size=8), data=st.data(),
+           boxed=st.booleans(), scalar=st.booleans())
+    def check(hosts, data, boxed, scalar):
+        workers = [f"{h}:{p}" for h, p in hosts]
+        idx = data.draw(st.integers(0, len(workers) - 1))
+        w = workers[0] if (scalar and len(workers) == 1) else workers
+        raw = json.dumps({"cluster": {"worker": w}, "task": {"type": "worker", "index": [idx] if boxed else idx}})
+        s = cluster.parse_tf_config(raw)
+        assert s.workers == workers and s.num_workers == len(workers)
+        assert s.task_id == idx and s.is_chief == (idx == 0)
+        assert s.chief_address == workers[0]
+        assert cluster.parse_tf_config(cluster.tf_config_json(workers, idx)).workers == workers
+
+    check()
