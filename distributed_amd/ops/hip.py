@@ -141,8 +141,19 @@ def split_plan(M: int, N: int, K: int, tile: int, bk: int = BK) -> Tuple[int, in
     return -(-K // kps), kps
 
 
+def _wgrad_slab1(M: int, N: int, K: int) -> bool:
+    """An unsplit weight-gradient GEMM over few tiles (the classifier's dW: 32 tiles, K =
+    batch): plain stores to one slab + the flat reduce beat the atomic epilogue there
+    (fp32 atomics measured 19 us for the 512 x 1000 dW)."""
+    t, splits, _ = wgrad_plan(M, N, K)
+    bm, bn = (256, 64) if t == 1 else (128, 128)
+    return splits == 1 and -(-M // bm) * -(-N // bn) <= 64 and (M * N) % 4 == 0 and M * N >= 4 * 8192
+
+
 def wgrad_workspace_elems(M: int, N: int, K: int) -> int:
     _, splits, _ = wgrad_plan(M, N, K)
+    if splits == 1 and _wgrad_slab1(M, N, K):
+        return M * N
     return splits * M * N if splits > 1 else 0
 
 
@@ -220,7 +231,8 @@ def conv_wgrad_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
 
 def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
     t, splits, kps = wgrad_plan(M, N, K)
-    if splits == 1:  # one writer per element: the atomic epilogue is an uncontended add
+    if splits == 1 and not (_wgrad_slab1(M, N, K) and workspace is not None and workspace.numel() >= M * N):
+        # one writer per element: the atomic epilogue is an uncontended add
         gemm(A, B, dw, amode=amode, bmode=B_NC, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N, epi=E_ATOMIC, geo=geo,
              tile=t)
         return
