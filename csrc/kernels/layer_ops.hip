@@ -710,6 +710,47 @@ __global__ __launch_bounds__(NT) void gap_fwd_k(const uint16_t* __restrict__ x, 
   }
 }
 
+// One image per block, the pixels split over G = NT / cg thread groups (ResNet-18's 7x7x512
+// head: 4 groups of ~12 pixels, 64 blocks) instead of one thread walking all HW pixels per
+// channel group (16 blocks, a 49-long load chain each); partials combined in group order.
+__global__ __launch_bounds__(NT) void gap_fwd_img_k(const uint16_t* __restrict__ x, int HW, int C, void* y,
+                                                    int y_f32) {
+  __shared__ float part[NT * 8];
+  const int cg = C / 8, G = NT / cg, t = threadIdx.x, n = blockIdx.x;
+  const int c8 = t % cg, g = t / cg;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  if (g < G) {
+    for (int p = g; p < HW; p += G) {
+      float v[8];
+      unpack8(reinterpret_cast<const uint4*>(x)[((long)n * HW + p) * cg + c8], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[t * 8 + e] = acc[e];
+  __syncthreads();
+  if (t >= cg) return;
+  float r[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] = 0.f;
+  for (int q = 0; q < G; ++q)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r[e] += part[(q * cg + t) * 8 + e];
+  const float inv = 1.f / HW;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) r[e] *= inv;
+  if (y_f32) {
+    float* o = (float*)y + (long)n * C + t * 8;
+    *reinterpret_cast<float4*>(o) = float4{r[0], r[1], r[2], r[3]};
+    *reinterpret_cast<float4*>(o + 4) = float4{r[4], r[5], r[6], r[7]};
+  } else {
+    reinterpret_cast<uint4*>(y)[(long)n * cg + t] = pack8(r);
+  }
+}
+
 __global__ __launch_bounds__(NT) void gap_bwd_k(const void* dy, int dy_f32, int N, int HW, int C,
                                                 uint16_t* __restrict__ dx) {
   const int cg = C / 8;
@@ -1117,6 +1158,10 @@ hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, i
 
 hipError_t gap_fwd(const uint16_t* x, int N, int HW, int C, void* y, int y_f32, hipStream_t s) {
   if (C % 8) return hipErrorInvalidValue;
+  if (C / 8 <= NT / 2 && HW >= 8) {
+    hipLaunchKernelGGL(gap_fwd_img_k, dim3(N), dim3(NT), 0, s, x, HW, C, y, y_f32);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(gap_fwd_k, dim3(grid_for((long)N * C / 8)), dim3(NT), 0, s, x, N, HW, C, y, y_f32);
   return hipGetLastError();
 }

@@ -301,3 +301,13 @@ def test_dense_split_k(H, M, K, N, out_bf16):
     close(dx, dy @ w.t(), 1e-2, 4e-3)
     H.dense_dgrad(dy.bfloat16(), w.bfloat16(), dx, accumulate=True, workspace=ws)
     close(dx, 2 * (dy @ w.t()), 1e-2, 8e-3)
+
+
+@pytest.mark.parametrize("n,hw,c,f32", [(64, 7, 512, True), (5, 7, 2048, False), (3, 2, 64, False), (2, 14, 8, True)])
+def test_gap_fwd_paths(H, n, hw, c, f32):
+    """Global average pool: per-image split kernel (C/8 <= 128, HW >= 8) and the
+    per-channel-group kernel, fp32 and bf16 outputs."""
+    x = rb(rnd(n, hw, hw, c, seed=60))
+    y = torch.empty(n, c, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+    H.gap_fwd(x.bfloat16(), y)
+    close(y, x.mean(dim=(1, 2)), 1e-4 if f32 else 1e-2, 1e-5 if f32 else 4e-3)
