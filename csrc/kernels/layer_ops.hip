@@ -391,6 +391,82 @@ __global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_k(const uint16_t* __re
   }
 }
 
+// 3x3/s2 pool, H = 2 Ho, W = 2 Wo, Ho and Wo even: one thread per 2x2 block of outputs.
+// Its 5x5 input patch is walked row by row (5 loads + BN/ReLU each), and every row updates
+// the outputs whose windows contain it, taps in ascending (kh, kw) order with the same
+// strict '>' as bn_relu_maxpool_fwd_k, so values and argmax codes are bitwise equal; 25
+// loads and normalisations per 4 outputs instead of 36.
+template <int PT, int PL>
+__global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_q_k(const uint16_t* __restrict__ x,
+                                                              const float* __restrict__ st, PoolGeo g,
+                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int cg = g.C / 8;
+  const int Ho2 = g.Ho / 2, Wo2 = g.Wo / 2;
+  const long total = (long)g.N * Ho2 * Wo2 * cg;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    long q = i / cg;
+    const int b2 = (int)(q % Wo2);
+    q /= Wo2;
+    const int a2 = (int)(q % Ho2);
+    const int n = (int)(q / Ho2);
+    float sc[8], sh[8];
+    ld8f(st + 2 * g.C + c8 * 8, sc);
+    ld8f(st + 3 * g.C + c8 * 8, sh);
+    float best[4][8];
+    uint32_t code[4][2];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) best[o][e] = -INFINITY;
+      code[o][0] = code[o][1] = 0u;
+    }
+    const int ih0 = 4 * a2 - PT, iw0 = 4 * b2 - PL;
+#pragma unroll
+    for (int pr = 0; pr < 5; ++pr) {
+      const int ih = ih0 + pr;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      float v[5][8];
+      bool ok[5];
+#pragma unroll
+      for (int pc = 0; pc < 5; ++pc) {
+        const int iw = iw0 + pc;
+        ok[pc] = (unsigned)iw < (unsigned)g.W;
+        float xv[8];
+        unpack8(reinterpret_cast<const uint4*>(x)[(((long)n * g.H + ih) * g.W + (ok[pc] ? iw : 0)) * cg + c8], xv);
+        bn_relu8(xv, sc, sh, v[pc]);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int kh = pr - 2 * r;
+        if (kh < 0 || kh > 2) continue;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int o = 2 * r + c;
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const int pc = 2 * c + kw;
+            if (!ok[pc]) continue;
+            const uint32_t idx = (uint32_t)(kh * 3 + kw);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (v[pc][e] > best[o][e]) {
+                best[o][e] = v[pc][e];
+                code[o][e >> 2] = (code[o][e >> 2] & ~(0xffu << (8 * (e & 3)))) | (idx << (8 * (e & 3)));
+              }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const long oi = (((long)n * g.Ho + 2 * a2 + (o >> 1)) * g.Wo + 2 * b2 + (o & 1)) * cg + c8;
+      reinterpret_cast<uint4*>(y)[oi] = pack8(best[o]);
+      reinterpret_cast<uint2*>(arg)[oi] = uint2{code[o][0], code[o][1]};
+    }
+  }
+}
+
 // gradient reaching input pixel (n, ih, iw), channels 8*c8.. through the max-pool windows
 // (fp32 sum, then rounded to bf16 as maxpool_bwd stores it)
 __device__ __forceinline__ void pool_grad8(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg,
@@ -1117,6 +1193,12 @@ hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H,
                                int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s) {
   if (C % 8 || ph * pw > 255) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  if (quad_pool_geo(g) && Ho % 2 == 0 && Wo % 2 == 0) {
+    auto k = g.pt ? (g.pl ? bn_relu_maxpool_fwd_q_k<1, 1> : bn_relu_maxpool_fwd_q_k<1, 0>)
+                  : (g.pl ? bn_relu_maxpool_fwd_q_k<0, 1> : bn_relu_maxpool_fwd_q_k<0, 0>);
+    hipLaunchKernelGGL(k, dim3(grid_for((long)N * Ho * Wo * C / 32)), dim3(NT), 0, s, x, st, g, y, arg);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_relu_maxpool_fwd_k, dim3(grid_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0, s, x, st, g, y,
                      arg);
   return hipGetLastError();
