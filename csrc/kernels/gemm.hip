@@ -533,9 +533,11 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
                                                       const float* __restrict__ bias, const uint16_t* R, int relu,
                                                       float* __restrict__ stats, int rb, uint16_t* out, int ldc) {
   __shared__ float red[2][NT * 8];
-  const int cg = N / 8, rp = NT / cg;  // column groups, rows per pass
+  // blockIdx.y: band of up to NT x 8 columns (wide layers: N > 2048)
+  const int c0 = blockIdx.y * NT * 8, Nb = min(N - c0, NT * 8);
+  const int cg = Nb / 8, rp = NT / cg;  // column groups, rows per pass
   const int t = threadIdx.x, g = t % cg, r0 = t / cg;
-  const int n = 8 * g;
+  const int n = c0 + 8 * g;
   const long row0 = (long)blockIdx.x * rb, row1 = min((long)M, row0 + rb);
   float cs[8], cq[8], bv[8];
 #pragma unroll
@@ -590,15 +592,15 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
     red[1][t * 8 + e] = r0 < rp ? cq[e] : 0.f;
   }
   __syncthreads();
-  for (int c = t; c < N; c += NT) {
+  for (int c = t; c < Nb; c += NT) {
     const int gg = c / 8, e = c % 8;
     float a = 0.f, b = 0.f;
     for (int q = 0; q < rp; ++q) {
       a += red[0][(q * cg + gg) * 8 + e];
       b += red[1][(q * cg + gg) * 8 + e];
     }
-    stats[(size_t)blockIdx.x * 2 * N + c] = a;
-    stats[(size_t)blockIdx.x * 2 * N + N + c] = b;
+    stats[(size_t)blockIdx.x * 2 * N + c0 + c] = a;
+    stats[(size_t)blockIdx.x * 2 * N + N + c0 + c] = b;
   }
 }
 
@@ -676,9 +678,10 @@ hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipS
 
 hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
                          float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s) {
-  if (splits < 1 || N % 8 || N / 8 > NT || ldc % 8 || rows_per_block < 1) return hipErrorInvalidValue;
+  if (splits < 1 || N % 8 || ldc % 8 || rows_per_block < 1) return hipErrorInvalidValue;
   const int grid = (M + rows_per_block - 1) / rows_per_block;
-  hipLaunchKernelGGL(splitk_finish_k, dim3(grid), dim3(NT), 0, s, slab, splits, M, N, bias, R, relu, stats,
+  const int bands = (N / 8 + NT - 1) / NT;
+  hipLaunchKernelGGL(splitk_finish_k, dim3(grid, bands), dim3(NT), 0, s, slab, splits, M, N, bias, R, relu, stats,
                      rows_per_block, out, ldc);
   return hipGetLastError();
 }

@@ -18,9 +18,12 @@ from __future__ import annotations
 
 import torch  # noqa: F401  (must be imported before the native module: shared HIP/RCCL libs)
 
-__version__ = "0.1.0"
-# API level of the TF/Keras surface this framework reproduces (reference README.md:40,266).
+# ``tf.__version__`` reports the API level of the TF surface this framework reproduces
+# (reference README.md:263-266 prints ``2.0.0``); the framework's own release is
+# ``FRAMEWORK_VERSION``.
 API_VERSION = "2.0.0"
+__version__ = API_VERSION
+FRAMEWORK_VERSION = "0.3.0"
 
 from . import utils  # noqa: E402
 from . import parallel  # noqa: E402

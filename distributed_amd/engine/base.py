@@ -90,4 +90,13 @@ def select_engine(model, strategy, per_replica: int, global_batch: int) -> Engin
         if ok:
             return NativeGraphEngine(model, strategy, per_replica, global_batch)
         dlog.debug("native graph engine not used: %s", why)
+    else:
+        why = "DAMD_NATIVE_GRAPH=0"
+    if strategy.device.type == "cuda":
+        # a GPU model outside the native engines' coverage trains through PyTorch eager ops
+        # (vendor libraries): say so loudly, or refuse under DAMD_STRICT_NATIVE=1
+        msg = f"model trains on the PyTorch eager fallback (GenericEngine), not the native HIP engines: {why}"
+        if env.get_bool("DAMD_STRICT_NATIVE", False):
+            raise RuntimeError(msg + " (DAMD_STRICT_NATIVE=1)")
+        dlog.warning(msg)
     return GenericEngine(model, strategy, per_replica, global_batch)

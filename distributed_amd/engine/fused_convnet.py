@@ -149,8 +149,12 @@ class FusedConvNetEngine(Engine):
         if self.world > 1 and mode in ("auto", "xgmi"):
             from ..parallel.communicator import make_peer_allreduce
 
+            # in-kernel wait deadline: the collective watchdog's when one is set, so a missing
+            # peer costs at most that much GPU spinning per wait
+            wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
             self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, C.convnet_grad_count(self.PP),
-                                            blocks=env.get_int("DAMD_PEER_BLOCKS", 64))
+                                            blocks=env.get_int("DAMD_PEER_BLOCKS", 64),
+                                            timeout_s=wd if wd > 0 else 60.0)
             if self.peer is None and mode == "xgmi":
                 raise RuntimeError("DAMD_ALLREDUCE=xgmi but the peer-to-peer all-reduce is unavailable")
         # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
@@ -185,6 +189,7 @@ class FusedConvNetEngine(Engine):
 
     def _ctrl_write(self, updates: dict):
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        self._check_peer()
         c = self.ctrl.cpu()
         for k, v in updates.items():
             c[k] = v
@@ -202,8 +207,8 @@ class FusedConvNetEngine(Engine):
         self.ctrl.copy_(c.to(self.device))
 
     def _watchdog_fired(self):
-        raise RuntimeError(f"collective watchdog: step did not complete within {self.watchdog_s}s; "
-                           "RCCL communicator aborted")
+        what = ("xGMI peer all-reduce wedged" if self.peer is not None else "RCCL communicator aborted")
+        raise RuntimeError(f"collective watchdog: step did not complete within {self.watchdog_s}s; {what}")
 
     def _iterations(self):
         return self._ctrl_host()[C_IT]
@@ -304,6 +309,7 @@ class FusedConvNetEngine(Engine):
     def finish(self):
         self._flush()
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        self._check_peer()  # never hand out weights built from a timed-out (partial) reduction
         opt = self.model.optimizer
         if opt.momentum:
             opt.ensure_slots(NPARAM, self.device)
@@ -315,3 +321,4 @@ class FusedConvNetEngine(Engine):
         # deferred update of the last step is applied first
         self._flush()
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        self._check_peer()  # never hand out weights built from a timed-out (partial) reduction

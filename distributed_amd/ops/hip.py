@@ -320,7 +320,7 @@ def dense_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, accumulate=
     _chk(w, torch.bfloat16, "w")
     _chk(dx, torch.bfloat16, "dx")
     splits, kps = dense_split_plan(M, K, N)
-    if splits > 1 and workspace is not None and workspace.numel() >= splits * M * K and K // 8 <= 256:
+    if splits > 1 and workspace is not None and workspace.numel() >= splits * M * K:
         gemm(dy, w, workspace, amode=A_KC, bmode=B_KC, M=M, N=K, K=N, lda=N, ldc=K, epi=E_SLAB, kc=N,
              splits=splits, k_per_split=kps)
         _C().splitk_finish(_ptr(workspace), splits, M, K, 0, _ptr(dx) if accumulate else 0, 0, 0, FINISH_RB,

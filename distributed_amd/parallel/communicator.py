@@ -224,6 +224,12 @@ def make_peer_allreduce(comm: Communicator, device: int, capacity: int, blocks: 
     W, r = comm.world_size, comm.rank
     if W < 2:
         return None
+    # IPC handles only map on the node that minted them: a multi-host cluster (TF_CONFIG
+    # workers on several machines) must not even try -- it uses RCCL
+    nodes = comm.allgather_object(node_id())
+    if len(set(nodes)) != 1:
+        dlog.info("peer all-reduce: ranks span %d hosts; gradient all-reduce via RCCL", len(set(nodes)))
+        return None
     from ..native import require_C
 
     C = require_C()
@@ -245,12 +251,30 @@ def make_peer_allreduce(comm: Communicator, device: int, capacity: int, blocks: 
     if not all(comm.allgather_object(ok)):
         return None
     if selftest:
-        ok = _peer_selftest(pa, device, int(capacity), W, r)
+        try:
+            ok = _peer_selftest(pa, device, int(capacity), W, r)
+        except Exception as e:  # pragma: no cover - every rank must reach the vote below
+            dlog.warning("peer all-reduce self-test raised on rank %d: %s", r, e)
+            ok = False
         if not all(comm.allgather_object(ok)):
             dlog.warning("peer all-reduce self-test failed; using RCCL")
             return None
     pa.set_timeout(float(timeout_s))
     return pa
+
+
+def node_id() -> str:
+    """Identity of this machine: hostname + kernel boot id (containers on one host that
+    share a hostname but not a kernel still differ)."""
+    import socket
+
+    boot = ""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        pass
+    return f"{socket.gethostname()}/{boot}"
 
 
 def _peer_selftest(pa, device: int, n: int, W: int, r: int) -> bool:

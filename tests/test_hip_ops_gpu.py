@@ -281,11 +281,12 @@ def test_gap_xent_colsum_sgd(H):
     assert torch.equal(Pb, P.bfloat16())
 
 
-@pytest.mark.parametrize("M,K,N", [(64, 512, 1008), (64, 5408, 64), (64, 64, 16)])
+@pytest.mark.parametrize("M,K,N", [(64, 512, 1008), (64, 5408, 64), (64, 64, 16), (64, 256, 4096), (64, 4096, 256)])
 @pytest.mark.parametrize("out_bf16", [False, True])
 def test_dense_split_k(H, M, K, N, out_bf16):
     """Split-K dense forward / backprop-input (workspace given, small-M shapes) against the
-    fp32 reference, including the bias/ReLU and accumulate epilogues of the finish kernels."""
+    fp32 reference, including the bias/ReLU and accumulate epilogues of the finish kernels.
+    N or K = 4096: the finish kernel's column bands (more than 2048 columns per row)."""
     splits, _ = H.dense_split_plan(M, N, K)
     assert splits > 1
     ws = torch.empty(H.dense_workspace_elems(M, N, K), device=dev)
