@@ -10,7 +10,11 @@ master weights, synthetic 28x28x1 data (60000 rows, no network), random-init wei
 Every timed step is a full training step: forward, loss, backward, RCCL all-reduce of
 the gradient (N > 1) and the SGD update (the last deferred update is flushed inside the
 timed region).  Run:  python bench.py --gpus N --steps K --warmup W
-(N > 1 under ``python -m torch.distributed.run --nproc-per-node N ... bench.py``).
+N > 1: either under ``python -m torch.distributed.run --nproc-per-node N ... bench.py``
+(RANK / WORLD_SIZE / MASTER_* in the environment), or plainly -- then this process
+spawns the N ranks itself (one child process per GPU, torchrun-style environment,
+started before anything touches the GPU), prints rank 0's JSON line and exits non-zero
+if any rank fails.
 """
 from __future__ import annotations
 
@@ -22,6 +26,55 @@ import time
 
 BASELINE_IMG_S = 6198.0  # reference 4-worker MWMS steady-state global rate (5,872-6,524)
 METRIC = "images/sec (whole node) MNIST CNN at 1/2/4/8 MI355X; DP scaling efficiency"
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Run ``bench.py argv`` as ``n`` local ranks (reference README.md:363-392: the same
+    script on every worker); returns the gang's exit code.  Rank 0's stdout is relayed."""
+    import signal
+    import subprocess
+
+    from distributed_amd.launch import free_port_base
+
+    port = free_port_base(1)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                    "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
+                                      start_new_session=True, text=True))
+    out = []
+    rc = 0
+    try:
+        for line in procs[0].stdout:
+            out.append(line)
+            print(line, end="", flush=True)
+        deadline = None
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                if deadline is None:
+                    deadline = time.time() + 30  # give the others a moment, then kill the gang
+                if time.time() > deadline:
+                    break
+            time.sleep(0.1)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+                p.wait()
+    rcs = [p.returncode for p in procs]
+    if any(rcs):
+        print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)
+        rc = next(c for c in rcs if c) or 1
+        rc = rc if rc > 0 else 1
+    return rc
 
 
 def main():
@@ -36,6 +89,9 @@ def main():
     ap.add_argument("--samples", type=int, default=None, help="synthetic dataset rows")
     ap.add_argument("--graph-steps", type=int, default=None)
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and "TF_CONFIG" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     if args.engine in ("generic", "native"):
         os.environ["DAMD_FUSED"] = "0"
@@ -99,6 +155,9 @@ def main():
         else:
             engine.run(k)
 
+    fail_at = runtime.fault_injection_step()  # DAMD_FAIL_AT=rank:step (launcher / gang tests)
+    if fail_at is not None and fail_at <= args.warmup:
+        raise RuntimeError(f"injected failure on rank {rt.rank} at step {fail_at} (DAMD_FAIL_AT)")
     run(args.warmup)
     # build the replayed HIP graph(s) now: capture is setup, not part of a timed step
     engine.prepare(args.steps)
@@ -164,9 +223,22 @@ def main():
                 "optimizer": ("SGD(lr=0.1, momentum=0.9)" if resnet else "SGD(lr=1e-3)") + ", fp32 master weights",
             },
             "final_epoch_loss": round(m.get("loss", float("nan")), 4),
+            # how the per-step gradient all-reduce ran, and how many ranks RCCL itself counts
+            "allreduce": getattr(engine, "allreduce_kind", "none"),
+            "rccl_ranks": _rccl_ranks(comm),
         }
         print(json.dumps(out), flush=True)
     runtime.shutdown()
+
+
+def _rccl_ranks(comm):
+    nat = getattr(comm, "native", None)
+    if nat is None:
+        return None
+    try:
+        return int(nat.comm_count)
+    except Exception:
+        return None
 
 
 if __name__ == "__main__":

@@ -97,6 +97,7 @@ PYBIND11_MODULE(_C, m) {
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("nranks", &RcclComm::nranks)
       .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("comm_count", &RcclComm::comm_count)
       .def("allreduce",
            [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int op, uintptr_t st) {
              c.allreduce(P_<void>(s), P_<void>(r), n, dt, op, P_<ihipStream_t>(st));

@@ -29,6 +29,7 @@ static ncclDataType_t to_nccl_dtype(int d) {
     case 2: return ncclFloat16;
     case 3: return ncclInt32;
     case 4: return ncclFloat64;
+    case 5: return ncclInt64;
     default: throw std::invalid_argument("unsupported dtype code");
   }
 }
@@ -104,6 +105,12 @@ bool stream_wait_with_deadline(hipStream_t st, double timeout_s, RcclComm* comm)
     // busy-poll the first 2 ms (step-sized waits), then back off to 20 us sleeps
     if (el > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
+}
+
+int RcclComm::comm_count() const {
+  int n = 0;
+  RCCL_CHECK(ncclCommCount(comm_, &n));
+  return n;
 }
 
 }  // namespace damd

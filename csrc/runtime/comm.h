@@ -25,7 +25,9 @@ class RcclComm {
   int nranks() const { return nranks_; }
   int rank() const { return rank_; }
   ncclComm_t comm() const { return comm_; }
-  // dtype: 0=f32 1=bf16 2=f16 3=i32 4=f64 ; op: 0=sum 1=max 2=min 3=avg
+  // ranks as RCCL itself counts them (ncclCommCount)
+  int comm_count() const;
+  // dtype: 0=f32 1=bf16 2=f16 3=i32 4=f64 5=i64 ; op: 0=sum 1=max 2=min 3=avg
   void allreduce(void* sendbuf, void* recvbuf, size_t count, int dtype, int op, hipStream_t st);
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t st);
   void allgather(const void* sendbuf, void* recvbuf, size_t count, int dtype, hipStream_t st);

@@ -160,6 +160,9 @@ class FusedConvNetEngine(Engine):
         # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
         # time, the gradient/metric buffer all-reduced through the host between steps
         self.host_collective = self.world > 1 and native is None and self.peer is None
+        self.allreduce_kind = ("none" if self.world == 1 and not force else
+                               "xgmi-peer" if self.peer is not None else
+                               "rccl" if native is not None else "host-gloo")
         if self.peer is not None:
             self.trainer.set_peer(self.peer)
         elif native is not None:

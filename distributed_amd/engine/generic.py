@@ -62,6 +62,8 @@ class GenericEngine(Engine):
         from ..utils import env
 
         self.bucketed = self.world > 1 and env.get_float("DAMD_BUCKET_MB", 8.0) > 0
+        self.allreduce_kind = ("none" if self.world == 1 else
+                               f"{self.strategy.communicator.name}{'-bucketed' if self.bucketed else ''}")
         limit = max(1, int(env.get_float("DAMD_BUCKET_MB", 8.0) * 2**20 / 4))
         offs, off = [], 0
         for sz in self.sizes:

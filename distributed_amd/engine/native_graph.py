@@ -205,6 +205,8 @@ class NativeGraphEngine(Engine):
         force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)  # exercise the RCCL path at world 1
         self.native_comm = strategy.communicator.native if (self.world > 1 or force) else None
         self.host_collective = self.world > 1 and self.native_comm is None
+        self.allreduce_kind = ("none" if self.native_comm is None and self.world == 1 else
+                               "rccl-bucketed" if self.native_comm is not None else "host-gloo")
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph = None
         self.feed = None

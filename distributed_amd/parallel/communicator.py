@@ -24,7 +24,7 @@ import torch.distributed as dist
 from ..utils import logging as dlog
 
 _OPS = {"sum": 0, "max": 1, "min": 2, "avg": 3}
-_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.float64: 4}
+_DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.int32: 3, torch.float64: 4, torch.int64: 5}
 
 
 class Communicator:
@@ -177,6 +177,7 @@ class RcclCommunicator(TorchCommunicator):
         C = require_C()
         uid = C.rccl_unique_id() if rank == 0 else None
         uid = self.broadcast_object(uid, root=0) if world_size > 1 else uid
+        self.uid = uid  # every rank holds rank 0's ncclUniqueId from here on
         self._comm = C.RcclComm(world_size, rank, uid, device)
         self.device = device
         dlog.debug("RCCL communicator up: rank %d/%d on hip device %d (RCCL %s)", rank, world_size, device,

@@ -1,0 +1,45 @@
+"""bench.py contract on CPU: ``python bench.py --gpus N`` without torchrun spawns the N
+ranks itself and prints ONE JSON line for the whole job (reference README.md:363-392:
+the same script runs on every worker)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=600):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TF_CONFIG", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["DAMD_DEVICE"] = "cpu"
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd="/tmp", env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    return r, lines
+
+
+@pytest.mark.dist
+def test_bench_spawns_its_own_ranks():
+    r, lines = _run(["--gpus", "2", "--engine", "generic", "--steps", "3", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2
+    assert out["config"]["global_batch"] == 128 and out["config"]["parallelism"] == "dp2"
+    assert out["steps"] == 3 and out["warmup"] == 1
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+    assert out["allreduce"].startswith("torch")
+
+
+@pytest.mark.dist
+def test_bench_gang_fails_if_a_rank_fails():
+    # rank 1 raises at its first step: the gang must exit non-zero, not hang
+    r, lines = _run(["--gpus", "2", "--engine", "generic", "--steps", "3", "--warmup", "1"],
+                    {"DAMD_FAIL_AT": "1:0"}, timeout=300)
+    assert r.returncode != 0
+    assert not lines

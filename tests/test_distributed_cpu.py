@@ -256,3 +256,20 @@ def test_injected_failure_gang_restart_resumes_from_backup(tmp_path):
     # the resumed attempt trained epochs 3-4 only
     assert len(j_ft["history"]["loss"]) == 2
     np.testing.assert_allclose(j_ft["history"]["loss"], j_ref["history"]["loss"][2:], rtol=1e-6)
+
+
+@pytest.mark.timeout(120)
+def test_rccl_communicator_bootstrap_two_ranks(tmp_path):
+    """The RCCL world>1 path up to communicator construction: rank 0's ncclUniqueId is
+    broadcast over the gloo control plane (TF_CONFIG rendezvous) to every rank, which then
+    calls ncclCommInitRank on its own device (here: no device, so it stops at hipSetDevice)."""
+    worker = os.path.join(ROOT, "tests", "helpers", "rccl_bootstrap_worker.py")
+    res = launch.launch_script([worker], nproc=2, env=_env(tmp_path), timeout=100)
+    assert res.ok, res.returncodes
+    outs = [json.load(open(tmp_path / f"rccl{r}.json")) for r in (0, 1)]
+    assert outs[0]["uid"] and outs[0]["uid"] == outs[1]["uid"] and len(outs[0]["uid"]) == 256
+    for o in outs:
+        if o["status"] == "constructed":
+            assert o["comm_count"] == 2
+        else:
+            assert "hipSetDevice" in o["error"] or "device" in o["error"].lower(), o["error"]
