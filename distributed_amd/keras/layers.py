@@ -36,10 +36,14 @@ def _current_device() -> torch.device:
 class Variable:
     """A named model variable; storage may be relocated into a flat engine buffer."""
 
-    def __init__(self, name: str, value: torch.Tensor, trainable: bool = True):
+    def __init__(self, name: str, value: torch.Tensor, trainable: bool = True, aggregation: str = "none"):
         self.name = name
         self._t = value
         self.trainable = trainable
+        # tf.VariableAggregation of a mirrored variable read across replicas: "mean" marks
+        # the SyncOnRead BN moving statistics (each replica updates its own copy, readers
+        # see the replica mean), "none" variables are kept identical by construction
+        self.aggregation = aggregation
         # weakref to the engine whose flat buffer holds this variable: host writes go
         # through its before/after hooks (flush a deferred update, refresh bf16 shadows)
         self._engine_ref = None
@@ -110,10 +114,10 @@ class Layer:
         self.output_shape = None
 
     # --- weights -------------------------------------------------------------
-    def add_weight(self, name, shape, initializer="zeros", trainable=True) -> Variable:
+    def add_weight(self, name, shape, initializer="zeros", trainable=True, aggregation="none") -> Variable:
         init = _init.get(initializer)
         val = init(tuple(shape)).to(torch.float32).to(_current_device())
-        v = Variable(f"{self.name}/{name}:0", val, trainable)
+        v = Variable(f"{self.name}/{name}:0", val, trainable, aggregation)
         self._weights.append(v)
         return v
 
@@ -431,8 +435,13 @@ class ZeroPadding2D(Layer):
 
 
 class BatchNormalization(Layer):
-    """Keras BN over channels (axis=-1).  Under MWMS statistics are per replica, as
-    tf.keras 2.0's (non-synced) BatchNormalization."""
+    """Keras BN over channels (axis=-1).  Under MWMS the batch statistics are per
+    replica, as tf.keras 2.0's (non-synced) BatchNormalization; the moving
+    statistics are SyncOnRead variables with MEAN aggregation (created inside
+    ``strategy.scope()``, reference README.md:134-151): every replica updates its own
+    copy and the model averages them across replicas at each epoch end (before
+    validation, callbacks and checkpoints read them), so every worker holds, saves and
+    evaluates with the replica mean."""
 
     def __init__(self, axis=-1, momentum=0.99, epsilon=1e-3, center=True, scale=True, **kw):
         super().__init__(**kw)
@@ -442,8 +451,9 @@ class BatchNormalization(Layer):
         c = int(input_shape[-1])
         self.gamma = self.add_weight("gamma", (c,), "ones") if self.scale else None
         self.beta = self.add_weight("beta", (c,), "zeros") if self.center else None
-        self.moving_mean = self.add_weight("moving_mean", (c,), "zeros", trainable=False)
-        self.moving_variance = self.add_weight("moving_variance", (c,), "ones", trainable=False)
+        self.moving_mean = self.add_weight("moving_mean", (c,), "zeros", trainable=False, aggregation="mean")
+        self.moving_variance = self.add_weight("moving_variance", (c,), "ones", trainable=False,
+                                               aggregation="mean")
 
     def call(self, x, training=False):
         g = self.gamma.value if self.gamma is not None else torch.ones(x.shape[-1], device=x.device)

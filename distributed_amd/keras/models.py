@@ -25,6 +25,7 @@ import torch
 from ..parallel import runtime as _runtime
 from ..parallel.strategy import MultiWorkerMirroredStrategy, get_strategy
 from ..utils import debug as _debug
+from ..utils import env
 from ..utils import logging as dlog
 from ..utils import profile as _profile
 from . import backend as K
@@ -141,6 +142,33 @@ class Model(L.Layer):
         if self._engine is not None:
             self._engine.sync()
 
+    def sync_on_read_variables(self):
+        """Average the MEAN-aggregated variables (BN moving statistics) across replicas,
+        in place.  Collective: every replica calls it at the same point (``fit`` does at
+        each epoch end).  The moving-average update is linear in the statistic, so the
+        replica mean of the per-replica moving averages equals the moving average of the
+        mean batch statistics: averaging in place changes nothing a later read would see
+        under TF's SyncOnRead semantics, and it keeps the copies mirrored bitwise."""
+        st = self._strategy
+        world = st.num_replicas_in_sync
+        vs = [w for w in self.weights if getattr(w, "aggregation", "none") == "mean"]
+        if world <= 1 or not vs:
+            return
+        if not env.get_bool("DAMD_BN_SYNC", True):
+            return
+        self._sync_engine()
+        flat = torch.cat([w.value.detach().reshape(-1).to(torch.float32) for w in vs])
+        st.communicator.allreduce_(flat, "sum")
+        flat.div_(float(world))
+        off = 0
+        with torch.no_grad():
+            for w in vs:
+                n = w.value.numel()
+                w.value.copy_(flat[off:off + n].view(w.value.shape).to(w.value.dtype))
+                off += n
+        if flat.is_cuda:
+            torch.cuda.synchronize(flat.device)
+
     # --- compile -------------------------------------------------------------------
     def compile(self, optimizer="rmsprop", loss=None, metrics=None, loss_weights=None, run_eagerly=None, **kw):
         self.optimizer = _opts.get(optimizer)
@@ -245,6 +273,7 @@ class Model(L.Layer):
                         cl.on_train_batch_end(done - 1, logs)
                         last_ui = time.time()
                 logs = self._public(engine.end_epoch())
+                self.sync_on_read_variables()  # BN moving statistics: replica mean (all ranks)
                 logs["seen"] = min(done * batch_size, n) if steps_per_epoch is None else done * batch_size
                 if validation_data is not None and (epoch + 1) % validation_freq == 0:
                     vres = self.evaluate(validation_data[0], validation_data[1], batch_size=batch_size, verbose=0,

@@ -273,3 +273,26 @@ def test_rccl_communicator_bootstrap_two_ranks(tmp_path):
             assert o["comm_count"] == 2
         else:
             assert "hipSetDevice" in o["error"] or "device" in o["error"].lower(), o["error"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("epoch_sync", [True, False])
+def test_batchnorm_moving_stats_are_replica_mean(tmp_path, epoch_sync):
+    """BN moving statistics under MWMS (reference README.md:134-151: variables created in
+    scope are mirrored; TF makes BN statistics SyncOnRead / MEAN).  Ranks see different
+    data, so their local statistics differ; after fit every replica holds the replica
+    mean, and the mirror check over ALL variables (statistics included) passes."""
+    worker = os.path.join(ROOT, "tests", "helpers", "bn_worker.py")
+    # without the epoch-end sync the in-fit mirror check would (rightly) raise: skip it there
+    extra = {"DAMD_CHECK_MIRRORS": 1} if epoch_sync else {"DAMD_BN_SYNC": "0"}
+    res = launch.launch_script([worker], nproc=2, env=_env(tmp_path, **extra), timeout=240)
+    assert res.ok, res.returncodes
+    outs = [json.load(open(tmp_path / f"bn{r}.json")) for r in (0, 1)]
+    assert outs[0]["n_stats"] == 4
+    assert outs[0]["fingerprint"] == outs[1]["fingerprint"]
+    w0 = list(np.load(tmp_path / "bn0.npz").values())
+    w1 = list(np.load(tmp_path / "bn1.npz").values())
+    assert all(np.array_equal(a, b) for a, b in zip(w0, w1))
+    if not epoch_sync:
+        assert outs[0]["differed"], "per-rank statistics should differ before the sync"
+        assert outs[0]["max_err"] < 1e-6
