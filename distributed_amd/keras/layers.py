@@ -86,12 +86,17 @@ class Variable:
 
 
 class KerasTensor:
-    """Symbolic tensor of the functional API (shape excludes nothing: batch is None)."""
+    """Symbolic tensor of the functional API (shape excludes nothing: batch is None).
 
-    def __init__(self, shape, layer=None, inputs=None):
+    ``node_index`` numbers the calls of ``layer`` (a layer applied twice owns two nodes):
+    Keras' ``inbound_nodes`` / ``input_layers`` entries are ``[layer_name, node_index,
+    tensor_index]``."""
+
+    def __init__(self, shape, layer=None, inputs=None, node_index=0):
         self.shape = tuple(shape)
         self.layer = layer
         self.inputs = inputs or []
+        self.node_index = node_index
 
     def __repr__(self):
         return f"<KerasTensor shape={self.shape}>"
@@ -168,7 +173,8 @@ class Layer:
             ins = list(x) if isinstance(x, (list, tuple)) else [x]
             shp = [t.shape for t in ins] if isinstance(x, (list, tuple)) else x.shape
             self._maybe_build(shp)
-            return KerasTensor(self.compute_output_shape(shp), self, ins)
+            self._n_nodes = getattr(self, "_n_nodes", 0) + 1
+            return KerasTensor(self.compute_output_shape(shp), self, ins, node_index=self._n_nodes - 1)
         shp = [tuple(t.shape) for t in x] if isinstance(x, (list, tuple)) else tuple(x.shape)
         self._maybe_build(shp)
         return self.call(x, training=training)
@@ -185,16 +191,21 @@ class Layer:
 
 
 class InputLayer(Layer):
-    def __init__(self, input_shape=None, batch_size=None, name=None, **kw):
+    def __init__(self, input_shape=None, batch_size=None, name=None, sparse=False, **kw):
         super().__init__(name=name or K.unique_name("input"), input_shape=input_shape, **kw)
 
     def call(self, x, training=False):
         return x
 
+    def get_config(self):
+        return {"batch_input_shape": list(self._batch_input_shape), "dtype": "float32", "sparse": False,
+                "name": self.name}
+
 
 def Input(shape, batch_size=None, name=None):  # noqa: N802
     lyr = InputLayer(input_shape=tuple(shape), name=name)
-    t = KerasTensor((batch_size,) + tuple(shape), lyr, [])
+    lyr._n_nodes = 1
+    t = KerasTensor((batch_size,) + tuple(shape), lyr, [], node_index=0)
     lyr.built = True
     lyr.output_shape = t.shape
     return t

@@ -378,7 +378,24 @@ class Model(L.Layer):
                 if not isinstance(l, L.InputLayer)]
 
     def get_config(self):
-        return {"name": self.name, "layers": self._layer_configs()}
+        """tf.keras functional-model config: every layer with its ``inbound_nodes`` (the
+        [layer, node, tensor, kwargs] entries each call consumed), plus ``input_layers`` /
+        ``output_layers``, so Keras (and :func:`model_from_config`) can rebuild the graph
+        (reference README.md:237-247: saved models are reloaded for scoring)."""
+        if self._inputs is None:
+            return {"name": self.name, "layers": self._layer_configs()}
+        calls = {}
+        for t in self._nodes:
+            calls.setdefault(id(t.layer), []).append(t)
+        layers = []
+        for l in self.layers:
+            nodes = sorted(calls.get(id(l), []), key=lambda t: t.node_index)
+            inbound = [[[i.layer.name, i.node_index, 0, {}] for i in t.inputs] for t in nodes]
+            layers.append({"name": l.name, "class_name": type(l).__name__, "config": l.get_config(),
+                           "inbound_nodes": inbound})
+        return {"name": self.name, "layers": layers,
+                "input_layers": [[t.layer.name, t.node_index, 0] for t in self._inputs],
+                "output_layers": [[t.layer.name, t.node_index, 0] for t in self._outputs]}
 
     def to_json(self, **kw):
         return json.dumps({"class_name": type(self).__name__, "config": self.get_config(),
@@ -459,20 +476,75 @@ class Sequential(Model):
         return {"name": self.name, "layers": self._layer_configs()}
 
 
+_IGNORED_CFG = ("kernel_regularizer", "bias_regularizer", "activity_regularizer", "kernel_constraint",
+                "bias_constraint", "noise_shape", "seed", "sparse", "ragged")
+
+
+def _layer_from_config(lc: dict) -> L.Layer:
+    cls = L.LAYER_CLASSES.get(lc["class_name"])
+    if cls is None:
+        raise ValueError(f"unknown layer class {lc['class_name']!r}")
+    cfg = dict(lc["config"])
+    cfg.pop("dtype", None)
+    for k in _IGNORED_CFG:
+        cfg.pop(k, None)
+    if "batch_input_shape" in cfg:
+        cfg["input_shape"] = tuple(cfg.pop("batch_input_shape")[1:])
+    return cls(**cfg)
+
+
+def _functional_from_config(cfg: dict) -> Model:
+    """Rebuild a functional model from a tf.keras config (layers with inbound_nodes).
+    Nodes are applied as soon as their inputs exist, so a shared layer's later calls may
+    consume its own earlier outputs."""
+    out = {}  # (layer name, node index) -> KerasTensor
+    objs, done = {}, {}
+    entries = []
+    for lc in cfg["layers"]:
+        name = lc.get("name", lc["config"].get("name"))
+        entries.append((name, lc))
+        done[name] = 0
+    total = sum(1 if lc["class_name"] == "InputLayer" else len(lc.get("inbound_nodes", [])) for _, lc in entries)
+    built = 0
+    while built < total:
+        progress = False
+        for name, lc in entries:
+            if lc["class_name"] == "InputLayer":
+                if done[name] == 0:
+                    c = lc["config"]
+                    out[(name, 0)] = L.Input(shape=tuple(c["batch_input_shape"][1:]), name=name)
+                    done[name] = 1
+                    built += 1
+                    progress = True
+                continue
+            nodes = lc.get("inbound_nodes", [])
+            while done[name] < len(nodes):
+                node = nodes[done[name]]
+                if not all((e[0], e[1]) in out for e in node):
+                    break
+                if name not in objs:
+                    objs[name] = _layer_from_config(lc)
+                layer = objs[name]
+                args = [out[(e[0], e[1])] for e in node]
+                out[(name, done[name])] = layer(args if (len(args) > 1 or isinstance(layer, L.Add)) else args[0])
+                done[name] += 1
+                built += 1
+                progress = True
+        if not progress:
+            raise ValueError("model config has a cycle or a missing inbound layer")
+    ins = [out[(e[0], e[1])] for e in cfg["input_layers"]]
+    outs = [out[(e[0], e[1])] for e in cfg["output_layers"]]
+    return Model(ins if len(ins) > 1 else ins[0], outs if len(outs) > 1 else outs[0], name=cfg.get("name"))
+
+
 def model_from_config(config: dict) -> Model:
+    if config["class_name"] in ("Model", "Functional"):
+        return _functional_from_config(config["config"])
     if config["class_name"] != "Sequential":
-        raise NotImplementedError("only Sequential model configs can be rebuilt from JSON")
+        raise NotImplementedError(f"cannot rebuild a {config['class_name']!r} model from its config")
     m = Sequential(name=config["config"].get("name"))
     for lc in config["config"]["layers"]:
-        cls = L.LAYER_CLASSES[lc["class_name"]]
-        cfg = dict(lc["config"])
-        cfg.pop("dtype", None)
-        for k in ("kernel_regularizer", "bias_regularizer", "activity_regularizer", "kernel_constraint",
-                  "bias_constraint", "noise_shape", "seed"):
-            cfg.pop(k, None)
-        if "batch_input_shape" in cfg:
-            cfg["input_shape"] = tuple(cfg.pop("batch_input_shape")[1:])
-        m.add(cls(**cfg))
+        m.add(_layer_from_config(lc))
     return m
 
 

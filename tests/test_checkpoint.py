@@ -129,3 +129,54 @@ def test_model_checkpoint_and_backup_restore(tmp_path):
     for a, b in zip(m2.get_weights(), ref.get_weights()):
         np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
     assert not os.path.exists(os.path.join(bdir, "chief.h5"))  # cleaned after success
+
+
+def test_functional_resnet_save_load_predict_roundtrip(tmp_path):
+    """A functional (residual, BN) model saved as Keras HDF5 carries its graph
+    (inbound_nodes / input_layers / output_layers) and reloads to the same predictions."""
+    tf.set_seed(4)
+    m = tf.models.resnet18(classes=10, input_shape=(16, 16, 3), widths=(8, 16, 16, 16), blocks=(1, 1, 1, 1))
+    tf.models.compile_resnet(m, 0.05, 0.9)
+    rng = np.random.default_rng(2)
+    x = rng.random((64, 16, 16, 3), dtype=np.float32)
+    y = rng.integers(0, 10, 64)
+    m.fit(x, y, batch_size=32, epochs=1, verbose=0)
+    p = str(tmp_path / "resnet.h5")
+    m.save(p)
+    cfg = json.loads(m.to_json())
+    assert cfg["class_name"] == "Model"
+    c = cfg["config"]
+    assert c["input_layers"] == [["input_1", 0, 0]] and c["output_layers"] == [["predictions", 0, 0]]
+    by = {l["name"]: l for l in c["layers"]}
+    assert by["input_1"]["inbound_nodes"] == []
+    assert by["conv1_conv"]["inbound_nodes"] == [[["input_1", 0, 0, {}]]]
+    add = by["conv3_block1_add"]["inbound_nodes"][0]
+    assert [e[0] for e in add] == ["conv3_block1_bn2", "conv3_block1_proj_bn"]
+    m2 = tf.keras.models.load_model(p)
+    assert [l.name for l in m2.layers] == [l.name for l in m.layers]
+    for a, b in zip(m.get_weights(), m2.get_weights()):
+        assert np.array_equal(a, b)
+    np.testing.assert_array_equal(m.predict(x[:16]), m2.predict(x[:16]))
+    assert m2.optimizer.momentum == pytest.approx(0.9)
+    if shutil.which(H5DUMP) or os.path.exists(H5DUMP):
+        out = subprocess.run([H5DUMP, "-a", "/model_config", p], capture_output=True, text=True).stdout
+        assert "inbound_nodes" in out and "conv3_block1_add" in out
+
+
+def test_shared_layer_node_indices():
+    """A layer applied twice owns two nodes; its second call is referenced as node 1."""
+    L = tf.keras.layers
+    inp = tf.keras.Input(shape=(6,))
+    d = L.Dense(6, name="shared")
+    h = d(d(inp))
+    out = L.Dense(2, name="head")(h)
+    m = tf.keras.Model(inp, out)
+    c = json.loads(m.to_json())["config"]
+    by = {l["name"]: l for l in c["layers"]}
+    assert by["shared"]["inbound_nodes"] == [[["input_1" if "input_1" in by else c["input_layers"][0][0], 0, 0, {}]],
+                                             [["shared", 0, 0, {}]]]
+    assert by["head"]["inbound_nodes"] == [[["shared", 1, 0, {}]]]
+    m2 = tf.keras.models.model_from_json(m.to_json())
+    m2.set_weights(m.get_weights())
+    xx = np.random.default_rng(0).random((4, 6), dtype=np.float32)
+    np.testing.assert_array_equal(m.predict(xx), m2.predict(xx))
