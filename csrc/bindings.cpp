@@ -48,7 +48,15 @@ class ConvNetTrainer : public StepExecutor {
     b_.W1alt = P_<float>(g("w1alt")); b_.V1alt = P_<float>(g("v1alt")); b_.w1bf = P_<uint16_t>(g("w1bf"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
     b_.fuse_head = bufs.contains("fuse_head") ? (int)g("fuse_head") : 0;
+    b_.kernels = bufs.contains("kernels") ? (int)g("kernels") : 2;
+    if (b_.kernels != 2 && b_.kernels != 3) throw std::invalid_argument("kernels must be 2 or 3");
+    b_.hacc = bufs.contains("hacc") ? P_<long long>(g("hacc")) : nullptr;
+    b_.hconv = bufs.contains("hconv") ? P_<long long>(g("hconv")) : nullptr;
+    b_.calt = bufs.contains("calt") ? P_<float>(g("calt")) : nullptr;
+    if (b_.kernels == 2 && (!b_.hacc || !b_.hconv || !b_.calt))
+      throw std::invalid_argument("2-launch step needs hacc / hconv / calt");
     HIP_CHECK(convnet_set_lds_limits());
+    HIP_CHECK(convnet2_set_lds_limits());
   }
   // X [n][784] (fp32, or uint8 holding k for inputs k/255) and labels [n] int32:
   // epoch-permuted copies (stable pointers).
@@ -56,19 +64,28 @@ class ConvNetTrainer : public StepExecutor {
     b_.X = P_<const void>(X); b_.labels = P_<const int>(labels); b_.x_u8 = x_u8;
     invalidate_graphs();
   }
-  void flush() { HIP_CHECK(convnet_launch_flush(b_, PP_, stream_)); }
+  void flush() {
+    if (b_.kernels == 2) HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
+    else HIP_CHECK(convnet_launch_flush(b_, PP_, stream_));
+  }
+  int kernels() const { return b_.kernels; }
   int num_slices() const { return convnet_num_slices(PP_); }
   int batch() const { return B_; }
 
  protected:
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
-    HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
+    if (b_.kernels == 2) HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
+    else HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
     if (!grad_allreduce_) return;
+    // the 2-launch step keeps the conv gradient as int64 fixed point (hconv): reduced
+    // exactly, in the same call as the fp32 gradient + metric buffer
+    long long* aux = b_.kernels == 2 ? b_.hconv : nullptr;
+    const long n64 = b_.kernels == 2 ? 2 * kConvNetNConv : 0;  // both parities (see convnet_step2.hip)
     if (peer_)  // native xGMI two-shot all-reduce
-      peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_);
+      peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, aux, n64);
     else if (comm_)  // comm set only when a reduction is wanted
-      comm_->allreduce(b_.G, b_.G, convnet_grad_count(PP_), 0, 0, stream_);
+      comm_->allreduce_f32_i64(b_.G, convnet_grad_count(PP_), aux, (size_t)n64, stream_);
   }
 
  private:
@@ -81,6 +98,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CONVNET_NPARAM") = kConvNetNParam;
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
   m.attr("CONVNET_REC") = kConvNetRec;
+  m.attr("CONVNET_NCONV") = kConvNetNConv;
+  m.def("convnet2_lds_bytes", [](int PP) { return py::make_tuple(convnet2_fwd_lds(PP, 4), convnet2_bwd_lds(PP)); });
   m.def("convnet_num_slices", &convnet_num_slices);
   m.def("convnet_grad_count", &convnet_grad_count);
   m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP, 4), convnet_f1_lds(PP, 6), convnet_f3_lds(PP)); });
@@ -114,6 +133,10 @@ PYBIND11_MODULE(_C, m) {
            [](RcclComm& c, uintptr_t s, uintptr_t r, size_t n, int dt, int op, uintptr_t st) {
              c.reduce_scatter(P_<const void>(s), P_<void>(r), n, dt, op, P_<ihipStream_t>(st));
            })
+      .def("allreduce_f32_i64",
+           [](RcclComm& c, uintptr_t d, size_t n, uintptr_t a, size_t n64, uintptr_t st) {
+             c.allreduce_f32_i64(P_<float>(d), n, P_<long long>(a), n64, P_<ihipStream_t>(st));
+           })
       .def("abort", &RcclComm::abort)
       .def_property_readonly("aborted", &RcclComm::aborted);
 
@@ -133,9 +156,11 @@ PYBIND11_MODULE(_C, m) {
              p.open(v);
            })
       .def("allreduce",
-           [](PeerAllreduce& p, uintptr_t data, long n, uintptr_t st) {
-             p.allreduce(P_<float>(data), n, P_<ihipStream_t>(st));
-           })
+           [](PeerAllreduce& p, uintptr_t data, long n, uintptr_t st, uintptr_t aux64, long n64) {
+             p.allreduce(P_<float>(data), n, P_<ihipStream_t>(st), P_<long long>(aux64), n64);
+           },
+           py::arg("data"), py::arg("n"), py::arg("stream"), py::arg("aux64") = 0, py::arg("n64") = 0)
+      .def_static("message_words", &PeerAllreduce::message_words)
       .def("link_local", &PeerAllreduce::link_local)
       .def("status", &PeerAllreduce::status)
       .def("clear_status", &PeerAllreduce::clear_status)
@@ -161,6 +186,7 @@ PYBIND11_MODULE(_C, m) {
       .def("invalidate_graphs", &ConvNetTrainer::invalidate_graphs)
       .def_property_readonly("num_graphs", &ConvNetTrainer::num_graphs)
       .def_property_readonly("num_slices", &ConvNetTrainer::num_slices)
+      .def_property_readonly("kernels", &ConvNetTrainer::kernels)
       .def_property_readonly("batch", &ConvNetTrainer::batch)
       .def_property_readonly("stream", [](ConvNetTrainer& t) { return reinterpret_cast<uintptr_t>(t.stream()); });
 

@@ -15,7 +15,13 @@ struct ConvNetBuffers {
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
   // 1: the head (F2) runs inside F1 (hacc + counters in `slabs`, see convnet_fused.hip)
   int fuse_head;
+  // 2-launch step (convnet_step2.hip): fixed-point accumulators of the cross-block sums
+  long long* hacc;   // [2][B][64] dense-1 pre-activations x 2^32, by step parity
+  long long* hconv;  // [2][320] conv weight/bias gradient x 2^40, by step parity (both all-reduced)
+  float* calt;       // [2][320] alternate conv parameters / velocity (double buffer by parity)
+  int kernels;       // 2 (default) or 3 (convnet_fused.hip)
 };
+constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;
 constexpr int kConvNetNGrad = 347152;
 constexpr int kConvNetRec = 716;  // F2 record columns (hpart is [kConvNetRec][B])
@@ -25,6 +31,12 @@ size_t convnet_f1_lds(int PP, int lg);
 size_t convnet_f3_lds(int PP);
 hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st);
+// the 2-launch step (convnet_step2.hip)
+size_t convnet2_fwd_lds(int PP, int lg);
+size_t convnet2_bwd_lds(int PP);
+hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
+hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st);
+hipError_t convnet2_set_lds_limits();
 // elements of the all-reduced gradient buffer
 size_t convnet_grad_count(int PP);
 hipError_t convnet_set_lds_limits();

@@ -46,8 +46,8 @@ struct Ctrl {
   int   global_batch;       // 5
   int   cursor;             // 6  step index inside the epoch (advanced on device)
   int   iterations;         // 7  optimizer iterations (advanced on device)
-  int   cnt_a;              // 8  arrival counter, kernel F2
-  int   cnt_b;              // 9  arrival counter, kernel F3
+  int   cnt_a;              // 8  arrival ticket of the 2-launch step's forward kernel (counts forever)
+  int   cnt_b;              // 9  arrival ticket of its backward kernel
   float acc_loss;           // 10 epoch accumulators (sum of per-sample loss)
   float acc_correct;        // 11
   float acc_count;          // 12
@@ -56,7 +56,11 @@ struct Ctrl {
   int   cur3;               // 15 step index as seen by the 3rd kernel (set by the 2nd)
   int   wpar;               // 16 which W1 buffer is current (0: inside P, 1: the alternate)
   int   flush_ticket;       // 17 arrival counter of flush_pending (its last block resets wpar)
-  int   pad[14];
+  int   pending;            // 18 1: the gradient buffers hold a step's gradient whose SGD update
+                            //    is still to be applied (set by the last kernel of a step,
+                            //    cleared by flush: the first step after a flush applies none)
+  int   par2;               // 19 step parity as seen by the 2nd kernel of a 2-launch step (set by the 1st)
+  int   pad[12];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 
@@ -100,7 +104,7 @@ __device__ __forceinline__ bool last_arriver(int* counter, int nblocks, int* fla
 // and written once at kernel end (a mid-kernel store makes hipcc wait vmcnt(0) and
 // distorts what it measures).  `st` is null unless DAMD_STAMPS is set on the host.
 struct Stamps {
-  unsigned long long t[8];
+  unsigned long long t[12];
 };
 __device__ __forceinline__ void stamp(Stamps& s, unsigned long long* st, int idx) {
   if (st != nullptr) s.t[idx] = __builtin_amdgcn_s_memrealtime();

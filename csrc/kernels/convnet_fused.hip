@@ -45,174 +45,10 @@
 // dense/bias, dense_1/kernel (64,10), dense_1/bias; the gradient buffer tail carries
 // [loss_sum, correct, count], so ONE all-reduce per step moves grads + metrics.  Inputs are epoch-permuted copies of
 // the dataset (row g of the epoch = global sample g), read without an index gather.
-#include "convnet.h"
-#include "damd_common.h"
+#include "convnet_dev.h"
 
 namespace damd {
 namespace convnet {
-
-constexpr int IMG = 28, NPIX = IMG * IMG;
-constexpr int PO = 13, NPOS = PO * PO;      // pooled 13x13
-constexpr int NF = 32;                       // conv filters
-constexpr int FEAT = NPOS * NF;              // 5408
-constexpr int HID = 64, NCLS = 10;
-constexpr int OFF_WC = 0, OFF_BC = 288, NCONV = 320;
-constexpr int OFF_W1 = NCONV, OFF_B1 = OFF_W1 + FEAT * HID;
-constexpr int OFF_W2 = OFF_B1 + HID, OFF_B2 = OFF_W2 + HID * NCLS;
-constexpr int NPARAM = OFF_B2 + NCLS;        // 347146
-constexpr int OFF_LOSS = NPARAM, OFF_CORR = NPARAM + 1, OFF_CNT = NPARAM + 2;
-constexpr int NGRAD = NPARAM + 6;            // padded to 16 B: 347152
-constexpr int NSMALL = HID + HID * NCLS + NCLS;  // b1, W2, b2 contiguous: 714
-constexpr int REC = NSMALL + 2;              // F2 record columns: dW2[640] db2[10] db1[64] loss corr
-constexpr int NAUX = NSMALL + 3;             // F3 "aux" elements: b1/W2/b2 + metric tail
-constexpr int CH = 64;                       // images per chunk
-constexpr int XR = 6;                        // staged input rows per image
-constexpr int MAXPP = 4;                     // max pooled positions per F1/F3 block
-constexpr int XS_BYTES = CH * XR * IMG * 4;  // 43008
-constexpr int HP = 72;                       // bf16 pitch of 64-wide tiles (conflict-free)
-static_assert(NPARAM == kConvNetNParam && NGRAD == kConvNetNGrad, "param count");
-static_assert(REC == kConvNetRec, "record count");
-
-__host__ __device__ constexpr int kpitch(int pp) { return pp * 32 + 8; }
-__host__ __device__ constexpr int nsp(int ns) { return (ns + 3) & ~3; }
-
-typedef short s16x8 __attribute__((ext_vector_type(8)));
-
-__device__ __forceinline__ uint16_t bf16_lo(float v, uint16_t hi) { return f2bf(v - bf2f(hi)); }
-
-// next step index (wraps for benchmark epochs)
-__device__ __forceinline__ int next_cursor(const Ctrl& c, int cur) {
-  return (c.wrap > 0 && cur + 1 >= c.wrap) ? 0 : cur + 1;
-}
-
-// ---- staged input rows: registers first (loads in flight early), LDS later ------------
-struct XStage {
-  float4 v[6];
-};
-// Input rows [r0, r0+nrows) of images b < nimg (valid if b < nvalid and row_base+b <
-// nsamples).  U8: the dataset is kept as uint8 (inputs that are exactly k/255, e.g.
-// MNIST) -- 4x fewer bytes -- and k/255.f (correctly rounded, == float32(k/255.0)) is
-// formed when staging; otherwise fp32 rows.  One unit = 16 B (fp32) or 4 B (u8).
-template <bool U8>
-__device__ __forceinline__ void x_load(XStage& st, const void* __restrict__ X, long row_base, int nsamples,
-                                       int nvalid, int nimg, int r0, int nrows) {
-  const int per_img = nrows * 7, total = nimg * per_img;
-#pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    const int i = min((int)threadIdx.x + u * 512, total - 1);
-    const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-    const long g = row_base + b;
-    const bool ok = ((int)threadIdx.x + u * 512 < total) && b < nvalid && g < nsamples;
-    const long gs = max(0L, min(g, (long)nsamples - 1));
-    if constexpr (U8) {
-      const uint32_t w = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + gs * NPIX +
-                                                           (r0 + r) * IMG)[q];
-      st.v[u].x = __uint_as_float(ok ? w : 0u);
-    } else {
-      const float4 v = reinterpret_cast<const float4*>(static_cast<const float*>(X) + gs * NPIX + (r0 + r) * IMG)[q];
-      st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  }
-}
-template <bool U8>
-__device__ __forceinline__ void x_store(const XStage& st, float* xs, int nimg, int nrows) {
-  const int per_img = nrows * 7, total = nimg * per_img;
-#pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    const int i = threadIdx.x + u * 512;
-    if (i < total) {
-      const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-      float4 v = st.v[u];
-      if constexpr (U8) {
-        const uint32_t w = __float_as_uint(st.v[u].x);
-        v = make_float4((float)(w & 0xff) / 255.f, (float)((w >> 8) & 0xff) / 255.f,
-                        (float)((w >> 16) & 0xff) / 255.f, (float)(w >> 24) / 255.f);
-      }
-      reinterpret_cast<float4*>(xs + (b * XR + r) * IMG)[q] = v;
-    }
-  }
-}
-
-// ---- conv 3x3 + bias + ReLU + 2x2 max-pool of a slice on MFMA (shared by F1 and F3) ----
-// One 16x16x32 bf16 MFMA per tile with a split-precision K packing:
-//   k in [0,9): x_hi*w_hi   [9,18): x_lo*w_hi   [18,27): x_hi*w_lo   [27,32): 0
-// (x = hi + lo, w = hi + lo in bf16) -> ~16-bit-mantissa conv outputs, so the pool
-// argmax / ReLU mask match an fp32 conv; the 23 spare K slots of a 9-tap conv pay it.
-// Row tile rt = 4 pool windows x 4 sub-pixels (window wi = pl*64 + image), so the 4
-// pixels of one window are the 4 accumulator rows of one lane: bias + ReLU + max +
-// first-max argmax happen in registers.  Per-lane tap offsets / bit masks make the
-// hi/lo selection branch-free (a ?: on the value turns into divergent control flow that
-// serialises the LDS reads).
-struct ConvFrag {
-  bf16x8 w[2];
-  float bias[2];
-  int toff[8];
-  uint32_t lomask[8], zmask[8];
-};
-__device__ __forceinline__ void conv_setup(ConvFrag& f, const float* cw, int lane) {
-  const int kg = lane >> 4;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
-    f.toff[j] = (tap / 3) * IMG + (tap % 3);
-    f.lomask[j] = part == 1 ? 0xffffu : 0u;
-    f.zmask[j] = k >= 27 ? 0u : 0xffffu;
-  }
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    s16x8 t;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
-      const float w32 = cw[min(tap, 8) * NF + 16 * nt + (lane & 15)];
-      const uint32_t hi = f2bf(w32), lo = bf16_lo(w32, (uint16_t)hi);
-      const uint32_t wlomask = part == 2 ? 0xffffu : 0u;
-      t[j] = (short)((hi ^ ((hi ^ lo) & wlomask)) & f.zmask[j]);
-    }
-    f.w[nt] = __builtin_bit_cast(bf16x8, t);
-    f.bias[nt] = cw[OFF_BC + 16 * nt + (lane & 15)];
-  }
-}
-// emit(image, pl, channel, pooled_bf16, code) for every pooled output of the slice
-template <class Emit>
-__device__ __forceinline__ void conv_pool(const ConvFrag& f, const float* xs, int p0, int np, int r0, int lg,
-                                          int wave, int lane, Emit&& emit) {
-  const int nrt = (np << lg) >> 2;  // np positions x 2^lg images / 4 windows per tile
-  for (int rt = wave; rt < nrt; rt += 8) {
-    s16x8 at;
-    {
-      const int r = lane & 15, wi = 4 * rt + (r >> 2), sub = r & 3;
-      const int pl = wi >> lg, b = wi & ((1 << lg) - 1), pos = p0 + pl, py = pos / PO, px = pos - py * PO;
-      const float* base = xs + (b * XR + 2 * py - r0 + (sub >> 1)) * IMG + 2 * px + (sub & 1);
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = base[f.toff[j]];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const uint32_t hi = f2bf(v[j]), lo = bf16_lo(v[j], (uint16_t)hi);
-        at[j] = (short)((hi ^ ((hi ^ lo) & f.lomask[j])) & f.zmask[j]);
-      }
-    }
-    const bf16x8 a = __builtin_bit_cast(bf16x8, at);
-    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    const f32x4 c0 = mfma16(a, f.w[0], zero);
-    const f32x4 c1 = mfma16(a, f.w[1], zero);
-    const int wo = 4 * rt + (lane >> 4), plo = wo >> lg, bo = wo & ((1 << lg) - 1);
-#pragma unroll
-    for (int nt = 0; nt < 2; ++nt) {
-      const f32x4 cc = nt ? c1 : c0;
-      float best = fmaxf(cc[0] + f.bias[nt], 0.f);
-      int arg = 0;
-#pragma unroll
-      for (int j = 1; j < 4; ++j) {
-        const float v = fmaxf(cc[j] + f.bias[nt], 0.f);
-        arg = v > best ? j : arg;
-        best = fmaxf(best, v);
-      }
-      emit(bo, plo, 16 * nt + (lane & 15), f2bf(best), (uint8_t)(arg | (best > 0.f ? 4 : 0)));
-    }
-  }
-}
 
 // =================================================================================
 // Head fused into F1 (opt-in, DAMD_CONVNET_FUSE_HEAD=1; measured 37.5 vs 30.0 us/step for the
@@ -419,7 +255,7 @@ __global__ __launch_bounds__(512) void f1_forward(
   stamp(sts, st, 1);
 
   // ---- issue every independent load of the prologue ----
-  XStage xst;
+  XStage<U8> xst;
   x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
   const int n4 = K * HID / 4;  // <= 2048
   float4 wv[4], gv[4], vv[4];
@@ -480,7 +316,7 @@ __global__ __launch_bounds__(512) void f1_forward(
     cw[tid] = wn;
   }
   stamp(sts, st, 2);
-  x_store<U8>(xst, xs, IB, nrows);
+  x_store<U8>(xst, xs);
   lds_barrier();
   stamp(sts, st, 3);
 
@@ -755,7 +591,7 @@ __global__ __launch_bounds__(512) void f3_backward(
 #pragma unroll
   for (int u = 0; u < 2; ++u)
     wv[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n8 - 1)];
-  XStage xst;
+  XStage<U8> xst;
   // named registers, not arrays: arrays captured by the lambdas below end up in scratch
   uint4 dq0, dq1, dq2, dq3;  // dh hi/lo [b][n] rows, dh hi/lo [n][b] rows
   uint4 pv0, pv1;            // pooled [k][b] rows of the slice
@@ -800,7 +636,7 @@ __global__ __launch_bounds__(512) void f3_backward(
       const int bb = tid / kc, q = tid - bb * kc;
       *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
     }
-    x_store<U8>(xst, xs, CH, nrows);
+    x_store<U8>(xst, xs);
   };
   load_chunk(0);
 #pragma unroll

@@ -1,0 +1,777 @@
+// Two-launch data-parallel training step for the reference MNIST CNN (gfx950 / MI355X).
+//
+// Model (reference README.md:58-73): Conv2D(32,3x3,valid)+bias+ReLU
+// -> MaxPool 2x2 -> Flatten(NHWC, 5408) -> Dense(64)+bias+ReLU -> Dense(10) ->
+// SparseCategoricalCrossentropy(from_logits); SGD(lr, momentum, nesterov) on fp32 masters.
+//
+// Why two launches: at B = 64 the step is a chain of dependent memory round trips, and
+// every launch costs ~2.5-3 us of prologue latency plus ~2.8 us of drain + dispatch
+// (profiles/r02_mnist phase stamps).  The 3-launch step (convnet_fused.hip) needed its
+// middle kernel only to combine the 57 dense-1 split-K slabs per row; here those partial
+// sums, and the conv-gradient partials, are combined by integer atomics on fixed-point
+// values, so the combine needs no extra launch and -- unlike fp32 atomics -- its result
+// does not depend on arrival order: every step is bitwise reproducible.
+//
+//   fwd (grid NS slices x IG image groups, 512 thr): the pending SGD update of the W1
+//       slice and of the conv parameters (both double-buffered by step parity: every
+//       block updates in registers, one owner block writes the next buffer) and of
+//       b1/W2/b2 (two owner blocks); conv + bias + ReLU + 2x2 max-pool on MFMA (pooled
+//       tile + argmax codes stored for bwd); the dense-1 partial of the slice on MFMA,
+//       added into hacc[par][row][n] as round(v * 2^32) with 64-bit atomics.
+//   bwd (grid NS slices, 512 thr): every block converts hacc back, adds b1, and runs the
+//       whole head redundantly: Dense(10) logits on f32 MFMA (16x16x4, exact fp32) with
+//       softmax-xent / accuracy / dz by 16-lane shuffles in the same waves, dh as a bf16
+//       hi+lo pair in both MFMA operand layouts in LDS (no global round trip for dh), its
+//       share of the b1/W2/b2 gradient and of the metric tail (fixed row order);
+//       dW1 = P^T dh and dP = dh W1^T on MFMA; MaxPool/ReLU backward through the stored
+//       argmax codes fused into this slice's conv weight-gradient partial, added into
+//       hconv[par] as round(v * 2^40) with 64-bit atomics; the dead parity of hacc is
+//       zeroed for the next step.
+//   No block waits on another: there is no ticket / last-arriver hand-off inside either
+//   launch (a returning atomic on a contended counter stalled its wave ~1.5-2 us).
+//
+// Fixed point: h partials are fp32 MFMA sums of |v| < 2^31; x 2^32 keeps every bit a
+// float carries down to 2^-32 (the sum of 57 roundings is < 1.4e-8 absolute); conv
+// gradient partials x 2^40 (resolution 9e-13, range 8e6).  Integer addition is
+// associative, so ranks and replays agree bitwise; the all-reduce sums both int64
+// parities exactly too (the dead one is re-zeroed before its next use).
+//
+// Step counter / parity without intra-kernel races: fwd block 0 copies ctrl.cursor and
+// ctrl.wpar to cur2 / par2; bwd reads those and its block 0 advances cursor / iterations,
+// flips wpar and sets `pending`; no kernel uses a ctrl field that the same kernel writes.
+#include "convnet_dev.h"
+
+namespace damd {
+namespace convnet2 {
+using namespace convnet;
+
+constexpr float HSCALE = 4294967296.f;          // 2^32
+constexpr double HINV = 1.0 / 4294967296.0;
+constexpr float CSCALE = 1099511627776.f;       // 2^40
+constexpr double CINV = 1.0 / 1099511627776.0;
+constexpr int NAUX2 = NSMALL + 3;               // b1/W2/b2 gradients + [loss, correct, count]
+constexpr int HPITCH = HID + 1;                 // fp32 pitch of the h tile in LDS
+constexpr int ZP = 11;                          // pitch of the logit / dz rows
+constexpr int HEAD_FLOATS = CH * HPITCH + 716 + CH * ZP + 2 * CH + 16 * HID + CH;
+constexpr int HEAD_BYTES = HEAD_FLOATS * 4;
+
+__device__ __forceinline__ long long to_fix(float v, float scale) { return (long long)__builtin_rintf(v * scale); }
+__device__ __forceinline__ float from_fix(long long q, double inv) { return (float)((double)q * inv); }
+
+__device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {
+  __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Reductions over the 16 lanes of a DPP row (one MFMA output column group) on DPP moves:
+// quad swaps, then half-row and row mirrors; every lane ends with the row's result, and
+// the combination order is fixed (deterministic).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_QSWAP1 = 0xB1, DPP_QSWAP2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dppf<DPP_QSWAP1>(v));
+  v = fmaxf(v, dppf<DPP_QSWAP2>(v));
+  v = fmaxf(v, dppf<DPP_HMIRROR>(v));
+  return fmaxf(v, dppf<DPP_MIRROR>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v += dppf<DPP_QSWAP1>(v);
+  v += dppf<DPP_QSWAP2>(v);
+  v += dppf<DPP_HMIRROR>(v);
+  return v + dppf<DPP_MIRROR>(v);
+}
+__device__ __forceinline__ int row16_min(int v) {
+  v = min(v, dppi<DPP_QSWAP1>(v));
+  v = min(v, dppi<DPP_QSWAP2>(v));
+  v = min(v, dppi<DPP_HMIRROR>(v));
+  return min(v, dppi<DPP_MIRROR>(v));
+}
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void sgd_or_keep(bool pend, float w, float g, float v, const Ctrl& c, float& wn,
+                                            float& vn) {
+  if (pend) {
+    sgd_update(w, g, v, c.lr, c.momentum, c.nesterov, wn, vn);
+  } else {
+    wn = w;
+    vn = v;
+  }
+}
+
+// =================================================================================
+// fwd: grid (NS slices, IG image groups of IB = 2^lg images)
+// =================================================================================
+template <bool U8>
+__global__ __launch_bounds__(512) void fwd(const void* __restrict__ X, float* __restrict__ P,
+                                           const float* __restrict__ G, float* __restrict__ V,
+                                           float* __restrict__ W1alt, float* __restrict__ V1alt,
+                                           uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
+                                           uint16_t* __restrict__ pooled, uint8_t* __restrict__ code,
+                                           long long* __restrict__ hacc, long long* __restrict__ hconv,
+                                           float* __restrict__ calt, int B, int PP, int lg,
+                                           unsigned long long* st) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int nblk = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + s;
+  Stamps sts;
+  stamp(sts, st, 0);
+  const int IB = 1 << lg, img0 = blockIdx.y * IB;
+  const int BP = (B + CH - 1) / CH * CH;
+  const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
+  const int KP = kpitch(PP);
+  float* xs = reinterpret_cast<float*>(smem);                              // [IB][XR][28]; later [IB][64] partials
+  uint16_t* as = reinterpret_cast<uint16_t*>(smem + IB * XR * IMG * 4);    // [IB][KP] pooled tile
+  uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
+  float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
+  float* lut = cw + NCONV + IB * PP * 32 / 4;                              // [256] k / 255
+  const Ctrl c = *ctrl;
+  const int par = c.wpar;
+  if (lin == 0 && tid == 0) {
+    ctrl->cur2 = c.cursor;
+    ctrl->par2 = par;
+  }
+  const bool pend = c.pending != 0;
+  const long row_base = (long)c.cursor * c.global_batch + c.row0 + img0;
+  const int r0 = 2 * (p0 / PO);
+  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
+  const bool mom = c.momentum != 0.f;
+
+  // ---- issue every independent load of the prologue ----
+  XStage<U8> xst;
+  x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
+  const int n4 = K * HID / 4;  // <= 2048
+  float4 wv[4], gv[4], vv[4];
+  const float* Wcur = c.wpar ? W1alt : P + OFF_W1;
+  const float* Vcur = c.wpar ? V1alt : V + OFF_W1;
+  float* Wnext = c.wpar ? P + OFF_W1 : W1alt;
+  float* Vnext = c.wpar ? V + OFF_W1 : V1alt;
+  const float4* P4 = reinterpret_cast<const float4*>(Wcur + p0 * 32 * HID);
+  const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
+  const float4* V4 = reinterpret_cast<const float4*>((mom ? Vcur : Wcur) + p0 * 32 * HID);
+  const bool owner = blockIdx.y == 0;
+  float4* Wn4 = reinterpret_cast<float4*>(Wnext + p0 * 32 * HID);
+  float4* Vn4 = reinterpret_cast<float4*>(Vnext + p0 * 32 * HID);
+  uint2* Wb = reinterpret_cast<uint2*>(w1bf + p0 * 32 * HID);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int ic = min(tid + u * 512, n4 - 1);
+    wv[u] = P4[ic];
+    gv[u] = G4[ic];
+    vv[u] = V4[ic];
+  }
+  // conv parameters: current buffer by parity; their gradient is the previous step's
+  // (bwd added it into hconv[par ^ 1])
+  const int tcl = min(tid, NCONV - 1);
+  const float cp = (par ? calt : P)[tcl], cv = (par ? calt + NCONV : V)[tcl];
+  const long long cq = hconv[(par ^ 1) * NCONV + tcl];
+  // b1/W2/b2: the grid's last two blocks own their pending update (nobody else in this
+  // launch reads them; bwd reads the updated values)
+  const int si = (lin - (nblk - 2)) * 512 + tid;
+  const bool small_on = lin >= nblk - 2 && si >= 0 && si < NSMALL;
+  const int sic = OFF_B1 + max(0, min(si, NSMALL - 1));
+  const float sp = P[sic], sg = G[sic], sv = V[sic];
+  if (U8 && tid < 256) lut[tid] = (float)tid / 255.f;
+  lds_barrier();  // the table is read by x_store (the loads above stay in flight)
+
+  // ---- pending SGD updates ----
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = tid + u * 512;
+    if (i < n4) {
+      float4 wn, vn;
+      sgd_or_keep(pend, wv[u].x, gv[u].x, vv[u].x, c, wn.x, vn.x);
+      sgd_or_keep(pend, wv[u].y, gv[u].y, vv[u].y, c, wn.y, vn.y);
+      sgd_or_keep(pend, wv[u].z, gv[u].z, vv[u].z, c, wn.z, vn.z);
+      sgd_or_keep(pend, wv[u].w, gv[u].w, vv[u].w, c, wn.w, vn.w);
+      const int e = i * 4, kr = e >> 6, n = e & 63;
+      const uint16_t h0 = f2bf(wn.x), h1 = f2bf(wn.y), h2 = f2bf(wn.z), h3 = f2bf(wn.w);
+      w1t[(n + 0) * KP + kr] = h0;
+      w1t[(n + 1) * KP + kr] = h1;
+      w1t[(n + 2) * KP + kr] = h2;
+      w1t[(n + 3) * KP + kr] = h3;
+      if (owner) {
+        Wn4[i] = wn;
+        if (mom) Vn4[i] = vn;
+        Wb[i] = make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), (uint32_t)h2 | ((uint32_t)h3 << 16));
+      }
+    }
+  }
+  float cwn = 0.f, cvn = 0.f;
+  if (tid < NCONV) {
+    sgd_or_keep(pend, cp, from_fix(cq, CINV), cv, c, cwn, cvn);
+    cw[tid] = cwn;
+  }
+  if (small_on) {
+    float wn, vn;
+    sgd_or_keep(pend, sp, sg, sv, c, wn, vn);
+    P[sic] = wn;
+    if (mom) V[sic] = vn;
+  }
+  // the owner writes the next conv buffer and zeroes the hconv parity bwd adds into next
+  if (lin == 0 && tid < NCONV) {
+    (par ? P : calt)[tid] = cwn;
+    if (mom) (par ? V : calt + NCONV)[tid] = cvn;
+    hconv[par * NCONV + tid] = 0;
+  }
+  stamp(sts, st, 1);
+  x_store<U8>(xst, xs, lut);
+  lds_barrier();
+  stamp(sts, st, 2);
+
+  ConvFrag cf;
+  conv_setup(cf, cw, lane);
+  uint8_t* csl = reinterpret_cast<uint8_t*>(cw + NCONV);  // [IB][K] argmax codes
+  conv_pool(cf, xs, p0, np, r0, lg, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t cd) {
+    as[bo * KP + plo * 32 + ch] = hb;
+    csl[bo * K + plo * 32 + ch] = cd;
+  });
+  lds_barrier();
+  stamp(sts, st, 3);
+  // pooled tile (feature-major [k][b]: bwd's dW1 operand) and argmax codes ([b][k]) for
+  // bwd, from LDS as contiguous 8-byte / 4-byte stores instead of scattered 1-2 B stores
+  for (int i = tid; i < K * (IB / 4); i += 512) {
+    const int kk = i / (IB / 4), bo = 4 * (i - kk * (IB / 4));
+    uint16_t v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = as[(bo + e) * KP + kk];
+    uint16_t* dst = pooled + (long)(p0 * NF + kk) * BP + img0 + bo;
+    if (img0 + bo + 3 < B) {
+      *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)v[0] | ((uint32_t)v[1] << 16),
+                                                 (uint32_t)v[2] | ((uint32_t)v[3] << 16));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (img0 + bo + e < B) dst[e] = v[e];
+    }
+  }
+  for (int i = tid; i < IB * (K / 4); i += 512) {
+    const int bo = i / (K / 4), w = i - bo * (K / 4);
+    if (img0 + bo < B)
+      *reinterpret_cast<uint32_t*>(code + (long)(img0 + bo) * FEAT + p0 * NF + 4 * w) =
+          reinterpret_cast<const uint32_t*>(csl + bo * K)[w];
+  }
+  // ---- dense-1 partial of the slice: part[row][n] = sum_k pooled[row][k] W1[k][n] ----
+  const int ko = 8 * (lane >> 4);
+  const int ntiles = (IB >> 4) * 4;
+  float* part = xs;  // [IB][64] (the staged rows are dead)
+  for (int t = wave; t < ntiles; t += 8) {
+    const int mt = t >> 2, nt = t & 3;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const int ar = 16 * mt + (lane & 15), bn = 16 * nt + (lane & 15);
+    for (int ks = 0; ks < np; ++ks) {
+      const bf16x8 a = ld_frag(as + ar * KP + ks * 32 + ko);
+      const bf16x8 bb = ld_frag(w1t + bn * KP + ks * 32 + ko);
+      acc = mfma16(a, bb, acc);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[(16 * mt + 4 * (lane >> 4) + j) * HID + bn] = acc[j];
+  }
+  lds_barrier();
+  // one wave instruction = one 512-B row of 64 int64 adds
+  long long* hp = hacc + (long)par * B * HID;
+  for (int r = wave; r < IB; r += 8)
+    if (img0 + r < B) atomic_add_i64(hp + (long)(img0 + r) * HID + lane, to_fix(part[r * HID + lane], HSCALE));
+  stamp(sts, st, 4);
+  if (st != nullptr && tid == 0 && lin < 256)
+    for (int i = 0; i < 5; ++i) st[lin * 16 + i] = sts.t[i];
+}
+
+// =================================================================================
+// bwd: grid NS slices
+// =================================================================================
+// aux element e (parameter order at G + OFF_B1): [0,64) db1, [64,704) dW2
+// (k = (e-64)/10, c = (e-64)%10), [704,714) db2, then 714 loss, 715 correct, 716 count.
+template <bool U8, bool ONE>  // ONE: B <= 64, a single chunk (no loop-carried prefetch registers)
+__global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int* __restrict__ labels,
+                                           const float* __restrict__ P, float* __restrict__ G,
+                                           const uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
+                                           const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
+                                           long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
+                                           int PP, unsigned long long* st) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  Stamps sts;
+  stamp(sts, st, 0);
+  const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x;
+  const int p0 = s * PP, p1 = min(NPOS, p0 + PP), np = p1 - p0, K = np * 32;
+  const int KD = PP * 32 + 4;   // dps pitch (f32)
+  const int KC = PP * 32;       // code pitch (bytes)
+  const int RB = max(CH * KD * 4, HEAD_BYTES);
+  float* xs = reinterpret_cast<float*>(smem);                              // [CH][XR][28]
+  float* dps = reinterpret_cast<float*>(smem + XS_BYTES);                  // [CH][KD] (after the head)
+  uint16_t* pt = reinterpret_cast<uint16_t*>(smem + XS_BYTES + RB);        // [PP*32][HP]
+  uint16_t* dht = pt + PP * 32 * HP;                                       // [2][HID][HP] dh^T hi, lo
+  uint16_t* dhs = dht + 2 * HID * HP;                                      // [2][CH][HP]  dh hi, lo
+  uint16_t* w1s = dhs + 2 * CH * HP;                                       // [PP*32][HP]
+  uint8_t* cs = reinterpret_cast<uint8_t*>(w1s + PP * 32 * HP);            // [CH][KC] argmax codes
+  float* red = reinterpret_cast<float*>(pt);  // [16][320] reduction scratch, after the MFMAs
+  // head scratch (aliases dps: used before the dP MFMA of each chunk)
+  float* hs = dps;                 // [CH][HPITCH] h = relu(dense-1)
+  float* spl = hs + CH * HPITCH;   // [716] b1[64] W2[64][10] b2[10]
+  float* zs = spl + 716;           // [CH][ZP] logits, then dz
+  float* rl = zs + CH * ZP;        // [CH] per-row loss
+  float* rc = rl + CH;             // [CH] per-row correct
+  float* db1p = rc + CH;           // [16][64] db1 partials
+  int* ylds = reinterpret_cast<int*>(db1p + 16 * HID);  // [CH] label of the row, -1 if invalid
+  float* lut = reinterpret_cast<float*>(cs + CH * KC + 16);  // [256] k / 255 (after the codes)
+  const Ctrl c = *ctrl;
+  const int cur = c.cur2, par = c.par2;
+  const long long* hcur = hacc + (long)par * B * HID;
+  if (s == 0 && tid == 0) {
+    ctrl->cursor = next_cursor(c, cur);
+    ctrl->iterations = c.iterations + 1;
+    ctrl->wpar = c.wpar ^ 1;  // fwd of this step wrote the next W1 buffer
+    ctrl->pending = 1;
+  }
+  const long gstart = (long)cur * c.global_batch;
+  const long row_base = gstart + c.row0;
+  const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
+  const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
+  const int r0 = 2 * (p0 / PO);
+  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int ko = 8 * (lane >> 4), lr16 = lane & 15;
+
+  // ---- this block's aux elements ----
+  const int chunk_aux = (NAUX2 + NS - 1) / NS;
+  const int tpe = max(1, min(512 / chunk_aux, 64));  // threads per aux element
+  const int ae_local = tid / tpe, aq = tid - ae_local * tpe;
+  const int ae = s * chunk_aux + ae_local;
+  const bool aux_on = ae_local < chunk_aux && ae < NAUX2;
+  const int aec = min(ae, NAUX2 - 1);
+  const float ag_old = G[OFF_LOSS + max(0, min(aec - NSMALL, 2))];  // previous step's reduced metric
+  float arsum = 0.f;
+
+  // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
+  const float spv0 = P[OFF_B1 + tid], spv1 = P[OFF_B1 + min(tid + 512, NSMALL - 1)];
+
+  // ---- prologue loads ----
+  const int n8 = K * HID / 8;
+  uint4 wv[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    wv[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n8 - 1)];
+  XStage<U8> xst;
+  uint4 hq0, hq1, hq2, hq3;  // hacc row (tid >> 3), columns 8 (tid & 7) .. + 8
+  uint4 pv0, pv1;
+  uint4 cv;
+  int ylab = 0;
+  bool yval = false;
+  const int BP = (B + CH - 1) / CH * CH;
+  const int kc = K / 16;
+  auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
+    {
+      const int r = tid >> 3, q = tid & 7;
+      const int row = min(chunk * CH + r, B - 1);
+      const uint4* hp = reinterpret_cast<const uint4*>(hcur + (long)row * HID + q * 8);
+      hq0 = hp[0];
+      hq1 = hp[1];
+      hq2 = hp[2];
+      hq3 = hp[3];
+    }
+    {
+      const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
+      pv0 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i0 >> 3)) * BP + chunk * CH + (i0 & 7) * 8);
+      pv1 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i1 >> 3)) * BP + chunk * CH + (i1 & 7) * 8);
+    }
+    {
+      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
+      const bool ok = i < CH * kc && lb < B;
+      const uint4 v = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF +
+                                                      min(q, kc - 1) * 16);
+      cv = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+    }
+    {
+      const int b = chunk * CH + min(tid, CH - 1);
+      const long g = row_base + b;
+      yval = tid < CH && b < B && g < c.nsamples;
+      ylab = labels[max(0L, min(g, (long)c.nsamples - 1))];
+    }
+    x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
+  };
+  auto store_chunk = [&](int chunk) __attribute__((always_inline)) {
+    if (tid < K * 8) *reinterpret_cast<uint4*>(pt + (tid >> 3) * HP + (tid & 7) * 8) = pv0;
+    if (tid + 512 < K * 8) *reinterpret_cast<uint4*>(pt + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = pv1;
+    if (tid < CH * kc) {
+      const int bb = tid / kc, q = tid - bb * kc;
+      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
+    }
+    x_store<U8>(xst, xs, lut);
+    spl[tid] = spv0;
+    if (tid + 512 < NSMALL) spl[tid + 512] = spv1;
+    if (tid < CH) ylds[tid] = yval ? ylab : -1;
+  };
+  load_chunk(0);
+  if (U8 && tid < 256) lut[tid] = (float)tid / 255.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = tid + u * 512;
+    if (i < n8) *reinterpret_cast<uint4*>(w1s + (i >> 3) * HP + (i & 7) * 8) = wv[u];
+  }
+  lds_barrier();  // lut visible to x_store
+
+  const int dn = wave & 3, dm0 = wave >> 2;
+  f32x4 accw[MAXPP];
+#pragma unroll
+  for (int i = 0; i < MAXPP; ++i) accw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int ch = tid & 31, grp = tid >> 5;
+  float gw[9], gb = 0.f;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) gw[t] = 0.f;
+  const int nchunks = ONE ? 1 : (B + CH - 1) / CH;
+
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    if (chunk) {
+      lds_barrier();
+      load_chunk(chunk);
+    }
+    store_chunk(chunk);
+    lds_barrier();
+    stamp(sts, st, 1);
+    // ---- head (every block, redundantly): h = relu(hacc / 2^32 + b1) ----
+    {
+      const int r = tid >> 3, q = tid & 7;
+      const bool rv = chunk * CH + r < B;
+      const uint4 hq[4] = {hq0, hq1, hq2, hq3};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long a = (long long)(((unsigned long long)hq[u].y << 32) | hq[u].x);
+        const long long b = (long long)(((unsigned long long)hq[u].w << 32) | hq[u].z);
+        const int n = q * 8 + 2 * u;
+        hs[r * HPITCH + n] = rv ? fmaxf(from_fix(a, HINV) + spl[n], 0.f) : 0.f;
+        hs[r * HPITCH + n + 1] = rv ? fmaxf(from_fix(b, HINV) + spl[n + 1], 0.f) : 0.f;
+      }
+    }
+    lds_barrier();
+    stamp(sts, st, 6);
+    // logits on f32 MFMA (wave mt: rows 16 mt .. 16 mt + 15, 16 columns, 10 used), then
+    // softmax-xent / accuracy / dz over each row's 16 lanes (DPP row reductions); the four
+    // rows j of a lane are independent chains, interleaved
+    if (wave < 4) {
+      const int mt = wave, lr = lane & 15, kq = lane >> 4;
+      float av[HID / 4], bv[HID / 4];  // all operands first: one LDS wait, then 16 MFMAs
+#pragma unroll
+      for (int ks = 0; ks < HID / 4; ++ks) {
+        const int k = 4 * ks + kq;
+        av[ks] = hs[(16 * mt + lr) * HPITCH + k];
+        bv[ks] = spl[HID + k * NCLS + min(lr, NCLS - 1)];
+      }
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < HID / 4; ++ks) acc = mfma4(av[ks], lr < NCLS ? bv[ks] : 0.f, acc);
+      const float b2v = lr < NCLS ? spl[HID + HID * NCLS + lr] : 0.f;
+      float v[4], m[4], e[4], lse[4];
+      int am[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = lr < NCLS ? acc[j] + b2v : -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) m[j] = row16_max(v[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = lr < NCLS ? __expf(v[j] - m[j]) : 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) e[j] = row16_sum(e[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lse[j] = m[j] + __logf(e[j]);
+        am[j] = row16_min(v[j] == m[j] ? lr : 16);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 16 * mt + 4 * kq + j;
+        const int yv = ylds[r];
+        const bool valid = yv >= 0;
+        const int y = valid ? yv : 0;
+        if (lr < NCLS) zs[r * ZP + lr] = valid ? (__expf(v[j] - lse[j]) - (lr == y ? 1.f : 0.f)) * inv : 0.f;
+        if (lr == y) rl[r] = valid ? (lse[j] - v[j]) : 0.f;
+        if (lr == 0) rc[r] = (valid && am[j] == y) ? 1.f : 0.f;
+      }
+    }
+    lds_barrier();
+    stamp(sts, st, 7);
+    // dh = (dz W2^T) * [h > 0] on f32 MFMA: 16 tiles of 16x16, two per wave, K = 10 (three
+    // k-steps of 4, zero-padded); a lane's 4 outputs are 4 consecutive rows of one column,
+    // so dh^T is stored 8 bytes at a time
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+      const int t = wave + 8 * ti, mt = t >> 2, nt = t & 3, lr = lane & 15, kq = lane >> 4;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int k = 4 * ks + kq;
+        const float a = k < NCLS ? zs[(16 * mt + lr) * ZP + k] : 0.f;
+        const float b = k < NCLS ? spl[HID + (16 * nt + lr) * NCLS + k] : 0.f;
+        acc = mfma4(a, b, acc);
+      }
+      const int n = 16 * nt + lr, rb = 16 * mt + 4 * kq;
+      uint16_t hi[4], lo[4];
+      float dsum = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = hs[(rb + j) * HPITCH + n] > 0.f ? acc[j] : 0.f;
+        dsum += d;
+        hi[j] = f2bf(d);
+        lo[j] = bf16_lo(d, hi[j]);
+        dhs[(rb + j) * HP + n] = hi[j];
+        dhs[CH * HP + (rb + j) * HP + n] = lo[j];
+      }
+      *reinterpret_cast<uint2*>(dht + n * HP + rb) =
+          make_uint2((uint32_t)hi[0] | ((uint32_t)hi[1] << 16), (uint32_t)hi[2] | ((uint32_t)hi[3] << 16));
+      *reinterpret_cast<uint2*>(dht + HID * HP + n * HP + rb) =
+          make_uint2((uint32_t)lo[0] | ((uint32_t)lo[1] << 16), (uint32_t)lo[2] | ((uint32_t)lo[3] << 16));
+      db1p[(4 * mt + kq) * HID + n] = dsum;  // [16][64]: partial over rows rb .. rb + 3
+    }
+    lds_barrier();
+    stamp(sts, st, 8);
+    // this block's aux elements over the chunk's rows (fixed order: deterministic)
+    if (aux_on) {
+      // element order = parameter order of b1[64], W2[64][10], b2[10] (G + OFF_B1)
+      float a = 0.f;
+      if (aec < HID) {
+        if (aq == 0)
+#pragma unroll
+          for (int q = 0; q < 16; ++q) a += db1p[q * HID + aec];
+      } else if (aec < HID + HID * NCLS) {
+        const int kk = (aec - HID) / NCLS, cc = aec - HID - kk * NCLS;
+        for (int r = aq; r < CH; r += tpe) a = fmaf(hs[r * HPITCH + kk], zs[r * ZP + cc], a);
+      } else if (aec < NSMALL) {
+        const int cc = aec - HID - HID * NCLS;
+        for (int r = aq; r < CH; r += tpe) a += zs[r * ZP + cc];
+      } else if (aec < NSMALL + 2) {
+        const float* src = aec == NSMALL ? rl : rc;
+        for (int r = aq; r < CH; r += tpe) a += src[r];
+      }
+      arsum += a;
+    }
+    lds_barrier();  // the head scratch (dps) is overwritten by dP below
+    stamp(sts, st, 2);
+    // dW1[k][n] += sum_b P[b][k] (dh_hi + dh_lo)[b][n]
+#pragma unroll
+    for (int i = 0; i < MAXPP; ++i) {
+      if (i >= np) break;
+      const int mt = dm0 + 2 * i;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 a = ld_frag(pt + (16 * mt + lr16) * HP + kk * 32 + ko);
+        const bf16x8 bh = ld_frag(dht + (16 * dn + lr16) * HP + kk * 32 + ko);
+        const bf16x8 bl = ld_frag(dht + HID * HP + (16 * dn + lr16) * HP + kk * 32 + ko);
+        accw[i] = mfma16(a, bh, accw[i]);
+        accw[i] = mfma16(a, bl, accw[i]);
+      }
+    }
+    // dP[b][k] = sum_n (dh_hi + dh_lo)[b][n] W1[k][n]
+    {
+      const int pm = wave & 3;
+#pragma unroll
+      for (int i = 0; i < MAXPP; ++i) {
+        if (i >= np) break;
+        const int nt = (wave >> 2) + 2 * i;
+        f32x4 a4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const bf16x8 ah = ld_frag(dhs + (16 * pm + lr16) * HP + kk * 32 + ko);
+          const bf16x8 al = ld_frag(dhs + CH * HP + (16 * pm + lr16) * HP + kk * 32 + ko);
+          const bf16x8 bb = ld_frag(w1s + (16 * nt + lr16) * HP + kk * 32 + ko);
+          a4 = mfma16(ah, bb, a4);
+          a4 = mfma16(al, bb, a4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dps[(16 * pm + 4 * (lane >> 4) + j) * KD + 16 * nt + lr16] = a4[j];
+      }
+    }
+    lds_barrier();
+    stamp(sts, st, 3);
+    // MaxPool + ReLU backward fused into the conv weight-gradient accumulation
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int bb = grp * 4 + ii;
+      for (int pl = 0; pl < np; ++pl) {
+        const int cd = cs[bb * KC + pl * 32 + ch];
+        const int pos = p0 + pl, py = pos / PO, px = pos - py * PO;
+        const float dv0 = dps[bb * KD + pl * 32 + ch];
+        const float d = (cd & 4) ? dv0 : 0.f;
+        const int y0 = 2 * py + ((cd >> 1) & 1) - r0, x0 = 2 * px + (cd & 1);
+        const float* xp = xs + (bb * XR + y0) * IMG + x0;
+        float xv[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) xv[t] = xp[(t / 3) * IMG + (t % 3)];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) gw[t] = fmaf(d, xv[t], gw[t]);
+        gb += d;
+      }
+    }
+  }
+  stamp(sts, st, 4);
+  // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
+#pragma unroll
+  for (int i = 0; i < MAXPP; ++i) {
+    if (i >= np) break;
+    const int mt = dm0 + 2 * i;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = 16 * mt + 4 * (lane >> 4) + j;
+      G[OFF_W1 + (long)(p0 * 32 + k) * HID + 16 * dn + lr16] = accw[i][j];
+    }
+  }
+  lds_barrier();  // pt/dht region becomes `red`, dps becomes `ared`
+#pragma unroll
+  for (int t = 0; t < 9; ++t) red[grp * NCONV + t * NF + ch] = gw[t];
+  red[grp * NCONV + OFF_BC + ch] = gb;
+  float* ared = dps;
+  ared[tid] = arsum;
+  lds_barrier();
+  // this slice's conv-gradient partial, fixed order over the 16 thread groups, then a
+  // 64-bit fixed-point atomic add (order-independent sum over the slices)
+  for (int i = tid; i < NCONV; i += 512) {
+    float a = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
+    atomic_add_i64(hconv + par * NCONV + i, to_fix(a, CSCALE));
+  }
+  // ---- aux: new b1/W2/b2 gradient, metric tail ----
+  if (aux_on && aq == 0) {
+    float tot = 0.f;
+    for (int q = 0; q < tpe; ++q) tot += ared[ae_local * tpe + q];
+    if (ae < NSMALL) {
+      G[OFF_B1 + ae] = tot;
+    } else {
+      const int m = ae - NSMALL;  // 0 loss, 1 correct, 2 count
+      float* accp = m == 0 ? &ctrl->acc_loss : (m == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
+      const float old = m == 0 ? c.acc_loss : (m == 1 ? c.acc_correct : c.acc_count);
+      *accp = old + ag_old;  // fold the previous step's all-reduced metric into the epoch total
+      G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
+    }
+  }
+  // zero the dead hacc parity (read by the previous step's bwd) for the next fwd,
+  // spread over the blocks
+  {
+    uint4* h4 = reinterpret_cast<uint4*>(hacc + (long)(par ^ 1) * B * HID);
+    for (int i = s * 512 + tid; i < B * HID / 2; i += NS * 512) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  stamp(sts, st, 5);
+  stamp_flush(sts, st, 9);
+}
+
+// =================================================================================
+// flush: apply the pending (deferred) update to every parameter, zero the gradient
+// buffers, fold the pending metrics into the epoch accumulators, clear `pending`.
+// =================================================================================
+__global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
+                                             const float* __restrict__ W1alt, const float* __restrict__ V1alt,
+                                             long long* __restrict__ hconv, const float* __restrict__ calt,
+                                             long long* __restrict__ hacc, int B, Ctrl* __restrict__ ctrl) {
+  const Ctrl c = *ctrl;
+  const bool mom = c.momentum != 0.f, pend = c.pending != 0;
+  // after a step's bwd: current W1 / conv parameters live in the alternates when wpar is
+  // set; the pending conv gradient is in hconv[wpar ^ 1]
+  const long long* hg = hconv + (c.wpar ^ 1) * NCONV;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NPARAM; i += gridDim.x * blockDim.x) {
+    const bool alt1 = c.wpar && i >= OFF_W1 && i < OFF_B1, altc = c.wpar && i < NCONV;
+    const float w = alt1 ? W1alt[i - OFF_W1] : (altc ? calt[i] : P[i]);
+    const float v = alt1 ? V1alt[i - OFF_W1] : (altc ? calt[NCONV + i] : V[i]);
+    const float g = i < NCONV ? from_fix(hg[i], CINV) : G[i];
+    float wn, vn;
+    sgd_or_keep(pend, w, g, v, c, wn, vn);
+    P[i] = wn;
+    if (mom) V[i] = vn;
+    G[i] = 0.f;
+  }
+  // both parities of the fixed-point accumulators start the next step at zero
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * NCONV + 2 * B * HID; i += gridDim.x * blockDim.x) {
+    if (i < 2 * NCONV) hconv[i] = 0;
+    else hacc[i - 2 * NCONV] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctrl->acc_loss = c.acc_loss + G[OFF_LOSS];
+    ctrl->acc_correct = c.acc_correct + G[OFF_CORR];
+    ctrl->acc_count = c.acc_count + G[OFF_CNT];
+    for (int i = NPARAM; i < NGRAD; ++i) G[i] = 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(&ctrl->flush_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        (int)gridDim.x - 1) {
+      ctrl->wpar = 0;
+      ctrl->pending = 0;
+      ctrl->flush_ticket = 0;
+    }
+  }
+}
+
+}  // namespace convnet2
+
+// ---------------------------------------------------------------------------------
+// Host-side launchers (no allocation / sync: capturable into a hipGraph).
+// ---------------------------------------------------------------------------------
+size_t convnet2_fwd_lds(int PP, int lg) {
+  using namespace convnet;
+  const int KP = kpitch(PP), IB = 1 << lg;
+  const size_t xsb = (size_t)IB * XR * IMG * 4, partb = (size_t)IB * HID * 4;
+  return (xsb > partb ? xsb : partb) + (size_t)(IB + HID) * KP * 2 + NCONV * 4 + (size_t)IB * PP * 32 + 256 * 4;
+}
+size_t convnet2_bwd_lds(int PP) {
+  using namespace convnet;
+  const int KD = PP * 32 + 4;
+  const size_t dpsb = (size_t)CH * KD * 4;
+  const size_t rb = dpsb > (size_t)convnet2::HEAD_BYTES ? dpsb : (size_t)convnet2::HEAD_BYTES;
+  const size_t redb = (size_t)16 * NCONV * 4;  // `red` spans pt + dht after the MFMAs
+  const size_t ptdht = (size_t)PP * 32 * HP * 2 + (size_t)2 * HID * HP * 2;
+  return XS_BYTES + rb + (ptdht > redb ? ptdht : redb) + (size_t)2 * CH * HP * 2 + (size_t)PP * 32 * HP * 2 +
+         (size_t)CH * PP * 32 + 16 + 256 * 4;
+}
+
+template <bool U8>
+static void launch2_impl(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+  using namespace convnet;
+  const int NS = convnet_num_slices(PP);
+  const int lg = convnet_f1_lg(B);
+  const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
+  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.X, b.P, b.G, b.V, b.W1alt,
+                     b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, b.stamps);
+  if (B <= CH)
+    hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.X, b.labels, b.P,
+                       b.G, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, B, PP,
+                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+  else
+    hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.X, b.labels,
+                       b.P, b.G, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, B, PP,
+                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+}
+
+hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+  if (!b.hacc || !b.hconv || !b.calt) return hipErrorInvalidValue;
+  if (convnet2_bwd_lds(PP) > 160 * 1024) return hipErrorInvalidValue;
+  if (b.x_u8) launch2_impl<true>(b, B, PP, st);
+  else launch2_impl<false>(b, B, PP, st);
+  return hipGetLastError();
+}
+
+hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {
+  hipLaunchKernelGGL(convnet2::flush, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.hconv, b.calt,
+                     b.hacc, B, b.ctrl);
+  return hipGetLastError();
+}
+
+hipError_t convnet2_set_lds_limits() {
+  const void* fns[6] = {(const void*)convnet2::fwd<false>,        (const void*)convnet2::fwd<true>,
+                        (const void*)convnet2::bwd<false, true>,  (const void*)convnet2::bwd<true, true>,
+                        (const void*)convnet2::bwd<false, false>, (const void*)convnet2::bwd<true, false>};
+  for (const void* f : fns) {
+    hipFuncAttributes at;
+    hipError_t e = hipFuncGetAttributes(&at, f);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)at.sharedSizeBytes);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace damd

@@ -53,29 +53,69 @@ __device__ __forceinline__ void wait_all(const PeerArgs& a, int phase, unsigned 
   __syncthreads();
 }
 
-__global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __restrict__ data, long n) {
+// Message word g (a multiple of 4): fp32 data below nfp = n rounded up to 4, then the
+// int64 segment (two words per value) -- a 16-byte word is never mixed.
+__device__ __forceinline__ float4 msg_load(const float* __restrict__ data, long n, const long long* __restrict__ aux,
+                                           long n64, long nfp, long g) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < nfp) {
+    if (g + 3 < n) {
+      v = *reinterpret_cast<const float4*>(data + g);
+    } else {
+      v.x = g < n ? data[g] : 0.f;
+      v.y = g + 1 < n ? data[g + 1] : 0.f;
+      v.z = g + 2 < n ? data[g + 2] : 0.f;
+    }
+  } else {
+    const long j = (g - nfp) / 2;
+    const long long q0 = j < n64 ? aux[j] : 0, q1 = j + 1 < n64 ? aux[j + 1] : 0;
+    v = make_float4(__int_as_float((int)(q0 & 0xffffffffLL)), __int_as_float((int)(q0 >> 32)),
+                    __int_as_float((int)(q1 & 0xffffffffLL)), __int_as_float((int)(q1 >> 32)));
+  }
+  return v;
+}
+__device__ __forceinline__ void msg_store(float* __restrict__ data, long n, long long* __restrict__ aux, long n64,
+                                          long nfp, long g, float4 v) {
+  if (g < nfp) {
+    if (g + 3 < n) {
+      *reinterpret_cast<float4*>(data + g) = v;
+    } else {
+      if (g < n) data[g] = v.x;
+      if (g + 1 < n) data[g + 1] = v.y;
+      if (g + 2 < n) data[g + 2] = v.z;
+    }
+  } else {
+    const long j = (g - nfp) / 2;
+    if (j < n64) aux[j] = (long long)(((unsigned long long)__float_as_uint(v.y) << 32) | __float_as_uint(v.x));
+    if (j + 1 < n64) aux[j + 1] = (long long)(((unsigned long long)__float_as_uint(v.w) << 32) | __float_as_uint(v.z));
+  }
+}
+__device__ __forceinline__ float4 msg_add(float4 a, float4 b, bool i64) {
+  if (i64) {
+    const unsigned long long a0 = ((unsigned long long)__float_as_uint(a.y) << 32) | __float_as_uint(a.x);
+    const unsigned long long a1 = ((unsigned long long)__float_as_uint(a.w) << 32) | __float_as_uint(a.z);
+    const unsigned long long b0 = ((unsigned long long)__float_as_uint(b.y) << 32) | __float_as_uint(b.x);
+    const unsigned long long b1 = ((unsigned long long)__float_as_uint(b.w) << 32) | __float_as_uint(b.z);
+    const unsigned long long s0 = a0 + b0, s1 = a1 + b1;
+    return make_float4(__uint_as_float((unsigned)s0), __uint_as_float((unsigned)(s0 >> 32)),
+                       __uint_as_float((unsigned)s1), __uint_as_float((unsigned)(s1 >> 32)));
+  }
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+__global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __restrict__ data, long n,
+                                                       long long* __restrict__ aux, long n64) {
   const int b = blockIdx.x, t = threadIdx.x, W = a.world;
   const long chunk = a.chunk, shard = chunk * a.nblk;
   const unsigned e = a.epoch[b] + 1;
   const long c4 = chunk / 4;
+  const long nfp = (n + 3) / 4 * 4;
 
-  // A: local gradient -> own `in` (chunk set b), zero beyond n
+  // A: local message -> own `in` (chunk set b), zero beyond the message
   float4* in_own = reinterpret_cast<float4*>(a.in[a.rank]);
   for (int s = 0; s < W; ++s) {
     const long base = s * shard + (long)b * chunk;
-    for (long i = t; i < c4; i += NT) {
-      const long g = base + 4 * i;
-      float4 v;
-      if (g + 3 < n) {
-        v = *reinterpret_cast<const float4*>(data + g);
-      } else {
-        v.x = g < n ? data[g] : 0.f;
-        v.y = g + 1 < n ? data[g + 1] : 0.f;
-        v.z = g + 2 < n ? data[g + 2] : 0.f;
-        v.w = 0.f;
-      }
-      in_own[base / 4 + i] = v;
-    }
+    for (long i = t; i < c4; i += NT) in_own[base / 4 + i] = msg_load(data, n, aux, n64, nfp, base + 4 * i);
   }
   signal_all(a, 0, e);
   wait_all(a, 0, e);
@@ -88,12 +128,11 @@ __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __rest
 #pragma unroll
       for (int p = 0; p < kPeerMaxRanks; ++p)
         if (p < W) v[p] = reinterpret_cast<const float4*>(a.in[p])[base4 + i];
+      const bool i64 = 4 * (base4 + i) >= nfp;
       float4 acc = v[0];
 #pragma unroll
       for (int p = 1; p < kPeerMaxRanks; ++p)
-        if (p < W) {
-          acc.x += v[p].x; acc.y += v[p].y; acc.z += v[p].z; acc.w += v[p].w;
-        }
+        if (p < W) acc = msg_add(acc, v[p], i64);
 #pragma unroll
       for (int p = 0; p < kPeerMaxRanks; ++p)
         if (p < W) reinterpret_cast<float4*>(a.out[p])[base4 + i] = acc;
@@ -106,29 +145,19 @@ __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __rest
   const float4* out_own = reinterpret_cast<const float4*>(a.out[a.rank]);
   for (int s = 0; s < W; ++s) {
     const long base = s * shard + (long)b * chunk;
-    for (long i = t; i < c4; i += NT) {
-      const long g = base + 4 * i;
-      const float4 v = out_own[base / 4 + i];
-      if (g + 3 < n) {
-        *reinterpret_cast<float4*>(data + g) = v;
-      } else {
-        if (g < n) data[g] = v.x;
-        if (g + 1 < n) data[g + 1] = v.y;
-        if (g + 2 < n) data[g + 2] = v.z;
-      }
-    }
+    for (long i = t; i < c4; i += NT) msg_store(data, n, aux, n64, nfp, base + 4 * i, out_own[base / 4 + i]);
   }
   if (t == 0) a.epoch[b] = e;
 }
 
 }  // namespace
 
-hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, hipStream_t st) {
+hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, long long* aux64, long n64, hipStream_t st) {
   if (a.world < 1 || a.world > kPeerMaxRanks || a.nblk < 1 || a.nblk > kPeerMaxBlocks || a.chunk % 4)
     return hipErrorInvalidValue;
-  if ((long)a.world * a.nblk * a.chunk < n) return hipErrorInvalidValue;
+  if ((long)a.world * a.nblk * a.chunk < (n + 3) / 4 * 4 + 2 * n64) return hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(data) % 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, data, n);
+  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, data, n, aux64, n64);
   return hipGetLastError();
 }
 

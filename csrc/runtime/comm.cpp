@@ -107,6 +107,13 @@ bool stream_wait_with_deadline(hipStream_t st, double timeout_s, RcclComm* comm)
   }
 }
 
+void RcclComm::allreduce_f32_i64(float* data, size_t n, long long* aux, size_t n64, hipStream_t st) {
+  RCCL_CHECK(ncclGroupStart());
+  RCCL_CHECK(ncclAllReduce(data, data, n, ncclFloat32, ncclSum, comm_, st));
+  if (n64) RCCL_CHECK(ncclAllReduce(aux, aux, n64, ncclInt64, ncclSum, comm_, st));
+  RCCL_CHECK(ncclGroupEnd());
+}
+
 int RcclComm::comm_count() const {
   int n = 0;
   RCCL_CHECK(ncclCommCount(comm_, &n));

@@ -29,6 +29,8 @@ class RcclComm {
   int comm_count() const;
   // dtype: 0=f32 1=bf16 2=f16 3=i32 4=f64 5=i64 ; op: 0=sum 1=max 2=min 3=avg
   void allreduce(void* sendbuf, void* recvbuf, size_t count, int dtype, int op, hipStream_t st);
+  // in-place SUM of n fp32 values and n64 int64 values as ONE grouped RCCL launch
+  void allreduce_f32_i64(float* data, size_t n, long long* aux, size_t n64, hipStream_t st);
   void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t st);
   void allgather(const void* sendbuf, void* recvbuf, size_t count, int dtype, hipStream_t st);
   void reduce_scatter(const void* sendbuf, void* recvbuf, size_t count, int dtype, int op,

@@ -108,11 +108,12 @@ void PeerAllreduce::link_local(const std::vector<PeerAllreduce*>& peers) {
   opened_ = true;
 }
 
-void PeerAllreduce::allreduce(float* data, long n, hipStream_t st) {
+void PeerAllreduce::allreduce(float* data, long n, hipStream_t st, long long* aux64, long n64) {
   if (!opened_) throw std::runtime_error("peer all-reduce: open() the peers' handles first");
-  if (n > cap_) throw std::invalid_argument("peer all-reduce: message larger than the capacity");
+  if (n64 < 0 || (n64 > 0 && !aux64)) throw std::invalid_argument("peer all-reduce: bad int64 segment");
+  if (message_words(n, n64) > cap_) throw std::invalid_argument("peer all-reduce: message larger than the capacity");
   if (a_.world == 1) return;
-  HIP_CHECK(peer_allreduce_launch(a_, data, n, st));
+  HIP_CHECK(peer_allreduce_launch(a_, data, n, aux64, n64, st));
 }
 
 unsigned PeerAllreduce::status() const {

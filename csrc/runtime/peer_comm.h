@@ -50,7 +50,10 @@ struct PeerArgs {
   unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
 
-hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, hipStream_t st);
+// Message of one call: n fp32 values at `data`, then (optionally) n64 int64 values at
+// `aux64` (fixed-point accumulators, summed exactly as integers) starting at the next
+// 16-byte word boundary; every rank ends with the same bits.
+hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, long long* aux64, long n64, hipStream_t st);
 
 class PeerAllreduce {
  public:
@@ -67,8 +70,11 @@ class PeerAllreduce {
   // test/benchmark only: peers that live in THIS process on the same device (no IPC)
   void link_local(const std::vector<PeerAllreduce*>& peers);
   bool ready() const { return opened_; }
-  // in-place SUM all-reduce of n fp32 values at `data` on `st` (capturable)
-  void allreduce(float* data, long n, hipStream_t st);
+  // in-place SUM all-reduce of n fp32 values at `data` (and n64 int64 values at `aux64`)
+  // on `st` (capturable)
+  void allreduce(float* data, long n, hipStream_t st, long long* aux64 = nullptr, long n64 = 0);
+  // message words (fp32 slots) of a call with n floats and n64 int64 values
+  static long message_words(long n, long n64) { return (n + 3) / 4 * 4 + 2 * n64; }
   // 0 = every wait so far completed; otherwise a wait timed out (peer missing / wedged)
   unsigned status() const;
   void clear_status();

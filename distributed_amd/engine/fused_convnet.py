@@ -28,7 +28,8 @@ NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 REC = 716
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
-C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR = range(17)
+(C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
+ C_FLUSHT, C_PEND, C_PAR2) = range(20)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -103,6 +104,15 @@ class FusedConvNetEngine(Engine):
         self.w1bf = torch.zeros(FEAT * HID, dtype=torch.bfloat16, device=dev)
         self.pooled = torch.zeros(FEAT, BP, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
+        # DAMD_CONVNET_KERNELS=2 (default): the 2-launch step (convnet_step2.hip) with
+        # int64 fixed-point cross-block sums -- bitwise reproducible; 3: the older 3-launch
+        # step (convnet_fused.hip, fp32 atomics for the conv gradient)
+        self.kernels = env.get_int("DAMD_CONVNET_KERNELS", 2)
+        if self.kernels not in (2, 3):
+            raise ValueError("DAMD_CONVNET_KERNELS must be 2 or 3")
+        self.hacc = torch.zeros(2 * B * HID, dtype=torch.int64, device=dev)  # by step parity
+        self.hconv = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
+        self.calt = torch.zeros(2 * NCONV, **f32)  # alternate conv parameters + velocity
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
         off = 0
@@ -127,7 +137,8 @@ class FusedConvNetEngine(Engine):
                     ctrl=self.ctrl.data_ptr(),
                     slabs=self.slabs.data_ptr(), dhq=self.dhq.data_ptr(), hpart=self.hpart.data_ptr(),
                     pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
-                    v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr())
+                    v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr(), kernels=self.kernels,
+                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr())
         # DAMD_CONVNET_FUSE_HEAD=1: the head (F2) folded into F1 by last-arriver tails with
         # fp32 atomics (csrc/kernels/convnet_fused.hip). Measured slower on MI355X (37.5 vs
         # 30.0 us/step at B=64: same-address atomic serialisation + a serial tail on the
@@ -152,7 +163,9 @@ class FusedConvNetEngine(Engine):
             # in-kernel wait deadline: the collective watchdog's when one is set, so a missing
             # peer costs at most that much GPU spinning per wait
             wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
-            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, C.convnet_grad_count(self.PP),
+            n64 = 2 * NCONV if self.kernels == 2 else 0
+            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0,
+                                            C.PeerAllreduce.message_words(C.convnet_grad_count(self.PP), n64),
                                             blocks=env.get_int("DAMD_PEER_BLOCKS", 64),
                                             timeout_s=wd if wd > 0 else 60.0)
             if self.peer is None and mode == "xgmi":
@@ -271,6 +284,8 @@ class FusedConvNetEngine(Engine):
                 self.trainer.step(1)
                 self.trainer.sync(0.0)
                 self.strategy.communicator.allreduce_(self.G, "sum")
+                if self.kernels == 2:
+                    self.strategy.communicator.allreduce_(self.hconv, "sum")  # exact int64 sum
                 torch.cuda.synchronize(self.device)
             self._pending = True
             self.steps_done += n_steps

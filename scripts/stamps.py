@@ -33,12 +33,17 @@ def main():
     eng.sync()
     st = eng.stamps.cpu().numpy()
     NS = eng.trainer.num_slices
-    grids = {"F1": NS * ((B + 15) // 16), "F2": B, "F3": NS}
-    names = {"F1": ["start", "ctrl", "sgd+loads", "xs staged", "conv done", "end"],
-             "F2": ["start", "slabs+params", "end"],
-             "F3": ["start", "loads staged", "mfma", "convgrad", "end"]}
+    if eng.trainer.kernels == 2:
+        grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, NS)}
+        names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued"],
+                 "bwd": ["start", "loads staged", "head done", "mfma", "convgrad", "end", "h", "softmax", "dh"]}
+    else:
+        grids = {"F1": (0, NS * ((B + 15) // 16)), "F2": (1, B), "F3": (2, NS)}
+        names = {"F1": ["start", "ctrl", "sgd+loads", "xs staged", "conv done", "end"],
+                 "F2": ["start", "slabs+params", "end"],
+                 "F3": ["start", "loads staged", "mfma", "convgrad", "end"]}
     t0 = None
-    for k, (kn, n) in enumerate(grids.items()):
+    for kn, (k, n) in grids.items():
         a = st[k, :n].astype(np.int64)
         base = a[:, 0][a[:, 0] > 0].min()
         t0 = base if t0 is None else t0

@@ -20,7 +20,7 @@ def main():
     comm = strategy.communicator
     W, r = comm.world_size, comm.rank
     dev = strategy.device
-    cap = 347152
+    cap = 347152 + 2 * 320
     pa = make_peer_allreduce(comm, dev.index or 0, cap, blocks=int(os.environ.get("DAMD_PEER_BLOCKS", "64")),
                              timeout_s=30.0)
     res = {"ok": pa is not None, "rank": r, "world": W, "errors": []}
@@ -39,6 +39,21 @@ def main():
                 torch.cuda.synchronize(dev)
                 if not torch.equal(d.cpu(), want):
                     res["errors"].append(f"eager n={n} rep={rep} maxdiff={(d.cpu() - want).abs().max().item()}")
+        # fp32 values + an int64 segment (the 2-launch step's fixed-point conv gradient):
+        # the integers are summed exactly, including carries across the 32-bit halves
+        for n, n64 in ((1000, 320), (347152, 320), (6, 3)):
+            x = torch.randn(n, generator=g)
+            q = torch.randint(-(2 ** 60), 2 ** 60, (n64,), generator=g, dtype=torch.int64)
+            xs, qs = comm.allgather_object(x), comm.allgather_object(q)
+            want_x = xs[0].clone()
+            for p in range(1, W):
+                want_x += xs[p]
+            want_q = sum(qs[1:], qs[0].clone())
+            dx, dq = x.to(dev), q.to(dev)
+            pa.allreduce(dx.data_ptr(), n, s.cuda_stream, dq.data_ptr(), n64)
+            torch.cuda.synchronize(dev)
+            if not (torch.equal(dx.cpu(), want_x) and torch.equal(dq.cpu(), want_q)):
+                res["errors"].append(f"int64 segment n={n} n64={n64}")
         # captured: 3 all-reduces per graph, replayed twice
         n = cap
         buf = torch.zeros(n, device=dev)
