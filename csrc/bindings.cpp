@@ -57,6 +57,19 @@ class ConvNetTrainer : public StepExecutor {
       throw std::invalid_argument("2-launch step needs hacc / hconv / calt");
     HIP_CHECK(convnet_set_lds_limits());
     HIP_CHECK(convnet2_set_lds_limits());
+    HIP_CHECK(convnet_persist_set_lds_limits());
+    if (bufs.contains("phacc")) {
+      phacc_ = P_<long long>(g("phacc"));
+      phconv_ = P_<long long>(g("phconv"));
+      psync_ = P_<unsigned>(g("psync"));
+    }
+  }
+  // k training steps in ONE launch of the persistent kernel (world 1; no graph needed)
+  void run_persistent(int k, double timeout_s) {
+    if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
+    if (!phacc_) throw std::runtime_error("ConvNetTrainer: persistent buffers not given");
+    if (k <= 0) return;
+    HIP_CHECK(convnet_persist_launch(b_, B_, k, phacc_, phconv_, psync_, timeout_s, stream_));
   }
   // X [n][784] (fp32, or uint8 holding k for inputs k/255) and labels [n] int32:
   // epoch-permuted copies (stable pointers).
@@ -91,6 +104,9 @@ class ConvNetTrainer : public StepExecutor {
  private:
   ConvNetBuffers b_;
   int B_, PP_, grad_allreduce_;
+  long long* phacc_ = nullptr;
+  long long* phconv_ = nullptr;
+  unsigned* psync_ = nullptr;
 };
 
 PYBIND11_MODULE(_C, m) {
@@ -99,6 +115,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
   m.attr("CONVNET_REC") = kConvNetRec;
   m.attr("CONVNET_NCONV") = kConvNetNConv;
+  m.def("convnet_persist_lds_bytes", &convnet_persist_lds);
   m.def("convnet2_lds_bytes", [](int PP) { return py::make_tuple(convnet2_fwd_lds(PP, 4), convnet2_bwd_lds(PP)); });
   m.def("convnet_num_slices", &convnet_num_slices);
   m.def("convnet_grad_count", &convnet_grad_count);
@@ -180,6 +197,8 @@ PYBIND11_MODULE(_C, m) {
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
       .def("capture", &ConvNetTrainer::capture)
       .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
+      .def("run_persistent", &ConvNetTrainer::run_persistent, py::arg("steps"), py::arg("timeout_s") = 5.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("flush", &ConvNetTrainer::flush)
       .def("sync", &ConvNetTrainer::sync, py::arg("timeout_s") = 0.0,
            py::call_guard<py::gil_scoped_release>())

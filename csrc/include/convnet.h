@@ -37,6 +37,11 @@ size_t convnet2_bwd_lds(int PP);
 hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st);
 hipError_t convnet2_set_lds_limits();
+// the persistent multi-step kernel (convnet_persist.hip): world 1, B <= 64, 3 positions per slice
+size_t convnet_persist_lds();
+hipError_t convnet_persist_launch(const ConvNetBuffers& b, int B, int nsteps, long long* hacc3, long long* hconv3,
+                                  unsigned* sync, double timeout_s, hipStream_t st);
+hipError_t convnet_persist_set_lds_limits();
 // elements of the all-reduced gradient buffer
 size_t convnet_grad_count(int PP);
 hipError_t convnet_set_lds_limits();

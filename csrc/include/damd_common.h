@@ -60,7 +60,8 @@ struct Ctrl {
                             //    is still to be applied (set by the last kernel of a step,
                             //    cleared by flush: the first step after a flush applies none)
   int   par2;               // 19 step parity as seen by the 2nd kernel of a 2-launch step (set by the 1st)
-  int   pad[12];
+  int   pad[12];              // 20 pad[0]: persistent kernel's global step (buffer rotation / barrier
+                              //    targets); 21 pad[1]: its error word (a grid wait timed out)
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

@@ -45,68 +45,11 @@ namespace damd {
 namespace convnet2 {
 using namespace convnet;
 
-constexpr float HSCALE = 4294967296.f;          // 2^32
-constexpr double HINV = 1.0 / 4294967296.0;
-constexpr float CSCALE = 1099511627776.f;       // 2^40
-constexpr double CINV = 1.0 / 1099511627776.0;
 constexpr int NAUX2 = NSMALL + 3;               // b1/W2/b2 gradients + [loss, correct, count]
 constexpr int HPITCH = HID + 1;                 // fp32 pitch of the h tile in LDS
 constexpr int ZP = 11;                          // pitch of the logit / dz rows
 constexpr int HEAD_FLOATS = CH * HPITCH + 716 + CH * ZP + 2 * CH + 16 * HID + CH;
 constexpr int HEAD_BYTES = HEAD_FLOATS * 4;
-
-__device__ __forceinline__ long long to_fix(float v, float scale) { return (long long)__builtin_rintf(v * scale); }
-__device__ __forceinline__ float from_fix(long long q, double inv) { return (float)((double)q * inv); }
-
-__device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {
-  __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Reductions over the 16 lanes of a DPP row (one MFMA output column group) on DPP moves:
-// quad swaps, then half-row and row mirrors; every lane ends with the row's result, and
-// the combination order is fixed (deterministic).
-template <int CTRL>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ int dppi(int v) {
-  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
-}
-constexpr int DPP_QSWAP1 = 0xB1, DPP_QSWAP2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
-__device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dppf<DPP_QSWAP1>(v));
-  v = fmaxf(v, dppf<DPP_QSWAP2>(v));
-  v = fmaxf(v, dppf<DPP_HMIRROR>(v));
-  return fmaxf(v, dppf<DPP_MIRROR>(v));
-}
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dppf<DPP_QSWAP1>(v);
-  v += dppf<DPP_QSWAP2>(v);
-  v += dppf<DPP_HMIRROR>(v);
-  return v + dppf<DPP_MIRROR>(v);
-}
-__device__ __forceinline__ int row16_min(int v) {
-  v = min(v, dppi<DPP_QSWAP1>(v));
-  v = min(v, dppi<DPP_QSWAP2>(v));
-  v = min(v, dppi<DPP_HMIRROR>(v));
-  return min(v, dppi<DPP_MIRROR>(v));
-}
-
-__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void sgd_or_keep(bool pend, float w, float g, float v, const Ctrl& c, float& wn,
-                                            float& vn) {
-  if (pend) {
-    sgd_update(w, g, v, c.lr, c.momentum, c.nesterov, wn, vn);
-  } else {
-    wn = w;
-    vn = v;
-  }
-}
 
 // =================================================================================
 // fwd: grid (NS slices, IG image groups of IB = 2^lg images)

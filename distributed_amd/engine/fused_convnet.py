@@ -29,7 +29,7 @@ HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 REC = 716
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
 (C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
- C_FLUSHT, C_PEND, C_PAR2) = range(20)
+ C_FLUSHT, C_PEND, C_PAR2, C_PSTEP, C_PERR) = range(22)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -110,6 +110,15 @@ class FusedConvNetEngine(Engine):
         self.kernels = env.get_int("DAMD_CONVNET_KERNELS", 2)
         if self.kernels not in (2, 3):
             raise ValueError("DAMD_CONVNET_KERNELS must be 2 or 3")
+        # persistent multi-step kernel (convnet_persist.hip): world 1, B <= 64, 3 positions
+        # per slice.  Opt-in (DAMD_PERSIST=1): measured at parity with the 2-launch step
+        # (24.7 vs 24.1 us/step, profiles/r03_mnist): it keeps W1 resident and has no launch
+        # boundaries, but runs the whole step on 57 CUs, where the 2-launch forward uses 228
+        self.persist = (env.get_bool("DAMD_PERSIST", False) and self.kernels == 2 and B <= 64 and self.PP == 3
+                        and self.world == 1 and not env.get_bool("DAMD_FORCE_ALLREDUCE", False))
+        self.phacc = torch.zeros(3 * 64 * HID, dtype=torch.int64, device=dev)
+        self.phconv = torch.zeros(64 * NCONV, dtype=torch.int64, device=dev)  # >= 57 x 320 fp32 slab
+        self.psync = torch.zeros(2, dtype=torch.int32, device=dev)
         self.hacc = torch.zeros(2 * B * HID, dtype=torch.int64, device=dev)  # by step parity
         self.hconv = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
         self.calt = torch.zeros(2 * NCONV, **f32)  # alternate conv parameters + velocity
@@ -138,7 +147,8 @@ class FusedConvNetEngine(Engine):
                     slabs=self.slabs.data_ptr(), dhq=self.dhq.data_ptr(), hpart=self.hpart.data_ptr(),
                     pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
                     v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr(), kernels=self.kernels,
-                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr())
+                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr(),
+                    phacc=self.phacc.data_ptr(), phconv=self.phconv.data_ptr(), psync=self.psync.data_ptr())
         # DAMD_CONVNET_FUSE_HEAD=1: the head (F2) folded into F1 by last-arriver tails with
         # fp32 atomics (csrc/kernels/convnet_fused.hip). Measured slower on MI355X (37.5 vs
         # 30.0 us/step at B=64: same-address atomic serialisation + a serial tail on the
@@ -202,6 +212,15 @@ class FusedConvNetEngine(Engine):
     def _check_peer(self):
         if self.peer is not None and self.peer.status():
             raise RuntimeError("xGMI peer all-reduce: a wait for a peer timed out (peer missing or wedged)")
+        if self.persist and int(self.ctrl[C_PERR].item()) != 0:
+            # a grid-wide wait of the persistent kernel timed out (workgroups not co-resident):
+            # its state is inconsistent -- reset the rotation / counters and fail loudly
+            self.ctrl[C_PERR] = 0
+            self.ctrl[C_PSTEP] = 0
+            self.phacc.zero_()
+            self.phconv.zero_()
+            self.psync.zero_()
+            raise RuntimeError("persistent ConvNet kernel: a grid-wide wait timed out (set DAMD_PERSIST=0)")
 
     def _ctrl_write(self, updates: dict):
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
@@ -279,6 +298,13 @@ class FusedConvNetEngine(Engine):
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
 
     def run(self, n_steps):
+        if self.persist and n_steps > 0:
+            # the deferred update of a previous 2-launch step is applied first; the persistent
+            # kernel applies every update of its own steps before it returns
+            self._flush()
+            self.trainer.run_persistent(n_steps, env.get_float("DAMD_PERSIST_TIMEOUT_S", 5.0))
+            self.steps_done += n_steps
+            return
         if self.host_collective:
             for _ in range(n_steps):
                 self.trainer.step(1)
@@ -300,6 +326,8 @@ class FusedConvNetEngine(Engine):
         self.steps_done += n_steps
 
     def prepare(self, n_steps):
+        if self.persist:
+            return
         if self.use_graph and not self.host_collective and n_steps >= self.graph_steps:
             self.trainer.capture(self.graph_steps)
 

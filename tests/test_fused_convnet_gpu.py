@@ -285,3 +285,55 @@ def test_two_and_three_launch_steps_agree(B, monkeypatch):
     for a, b in zip(outs[0][0], outs[1][0]):
         np.testing.assert_allclose(a, b, rtol=1e-4, atol=2e-6)
     assert abs(outs[0][1]["loss"] - outs[1][1]["loss"]) < 1e-5
+
+
+@pytest.mark.parametrize("B", [64, 40])
+def test_persistent_kernel_matches_two_launch_step(B, monkeypatch):
+    """The persistent multi-step kernel (one launch for all steps, W1 slices resident in
+    registers, grid-wide int64 hand-offs) against the 2-launch step over 12 momentum steps
+    crossing an epoch flush; the b1/W2/b2 gradient sums run in a different fixed order."""
+    _need_gpu()
+    x, y = _data(1024)
+    outs = []
+    for persist in ("1", "0"):
+        monkeypatch.setenv("DAMD_PERSIST", persist)  # opt-in persistent kernel vs the default
+        m = _model(lr=0.05, momentum=0.9, seed=19)
+        eng = _engine(m, B)
+        assert eng.persist == (persist == "1")
+        eng.bind(x, y)
+        mets = []
+        for ep in range(2):
+            eng.start_epoch(ep, shuffle=True)
+            eng.run(5)
+            eng.run(1)
+            mets.append(eng.end_epoch())
+        eng.finish()
+        outs.append((m.get_weights(), mets, int(m.optimizer.iterations)))
+    for a, b in zip(outs[0][0], outs[1][0]):
+        np.testing.assert_allclose(a, b, rtol=2e-4, atol=2e-6)
+    for ma, mb in zip(outs[0][1], outs[1][1]):
+        assert abs(ma["loss"] - mb["loss"]) < 1e-5 and ma["accuracy"] == mb["accuracy"]
+    assert outs[0][2] == outs[1][2] == 12
+
+
+def test_persistent_kernel_one_step_and_metrics(monkeypatch):
+    """Opt-in persistent kernel: one step against the bf16-mirrored fp64 reference, loss and
+    accuracy metrics included."""
+    _need_gpu()
+    monkeypatch.setenv("DAMD_PERSIST", "1")
+    lr = 0.5
+    m = _model(lr=lr)
+    x, y = _data(300)
+    w0 = m.get_weights()
+    eng = _engine(m, 64)
+    assert eng.persist
+    eng.bind(x, y)
+    eng.start_epoch(0, shuffle=False)
+    eng.run(1)
+    met = eng.end_epoch()
+    eng.finish()
+    gq, lsum, corr = _ref_step(w0, x[:64], y[:64], 64, quant=True)
+    for a, b, g in zip(w0, m.get_weights(), gq):
+        assert np.linalg.norm((a - b) / lr - g) / (np.linalg.norm(g) + 1e-12) < 5e-3
+    assert abs(met["loss"] - lsum / 64) < 2e-2
+    assert abs(met["accuracy"] - corr / 64) < 1.5 / 64
