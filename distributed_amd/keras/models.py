@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 import time
 
 import numpy as np
@@ -248,6 +249,12 @@ class Model(L.Layer):
         mirror_every = _debug.mirror_check_every()
         refresh_s = 0.5
         global_step = 0
+        from ..utils import watchdog as _wd
+
+        watchdog = _wd.for_strategy(st)  # a hung collective -> exit for a gang restart
+        if watchdog is not None:
+            watchdog.arm("first step (includes graph capture / communicator set-up)")
+        hang_at = _hang_injection()
         try:
             for epoch in range(initial_epoch, epochs):
                 cl.on_epoch_begin(epoch)
@@ -258,6 +265,10 @@ class Model(L.Layer):
                     k = min(chunk, steps - done)
                     if fail_at is not None and global_step <= fail_at < global_step + k:
                         raise RuntimeError(f"DAMD_FAIL_AT: injected failure at step {fail_at}")
+                    if hang_at is not None and global_step <= hang_at < global_step + k:
+                        dlog.warning("DAMD_HANG_AT: this rank stops responding at step %d", hang_at)
+                        while True:  # a wedged worker: only the gang restart ends it
+                            time.sleep(3600)
                     prof = _profile.active()
                     rec = prof.begin(k, batch_size, st.device) if prof else None
                     engine.run(k)
@@ -266,14 +277,20 @@ class Model(L.Layer):
                     _debug.debug_sync(st.device)
                     done += k
                     global_step += k
+                    if watchdog is not None:
+                        # the host loop is alive; a hang inside a collective or a device wait
+                        # stops these beats (the next host sync blocks)
+                        watchdog.beat(f"epoch {epoch + 1} step {done}")
                     if per_hook or (verbose == 1 and time.time() - last_ui > refresh_s):
                         logs = self._public(engine.metrics())
                         logs["seen"] = min(done * batch_size, n) if steps_per_epoch is None else done * batch_size
                         logs["size"] = batch_size
                         cl.on_train_batch_end(done - 1, logs)
                         last_ui = time.time()
-                logs = self._public(engine.end_epoch())
+                logs = self._public(engine.end_epoch())  # host sync: the epoch's device work is done
                 self.sync_on_read_variables()  # BN moving statistics: replica mean (all ranks)
+                if watchdog is not None:
+                    watchdog.beat(f"epoch {epoch + 1} end")
                 logs["seen"] = min(done * batch_size, n) if steps_per_epoch is None else done * batch_size
                 if validation_data is not None and (epoch + 1) % validation_freq == 0:
                     vres = self.evaluate(validation_data[0], validation_data[1], batch_size=batch_size, verbose=0,
@@ -288,6 +305,8 @@ class Model(L.Layer):
             self._failed = True
             raise
         finally:
+            if watchdog is not None:
+                watchdog.close()
             engine.finish()
         self._failed = False
         for c in cb_list:
@@ -535,6 +554,18 @@ def _functional_from_config(cfg: dict) -> Model:
     ins = [out[(e[0], e[1])] for e in cfg["input_layers"]]
     outs = [out[(e[0], e[1])] for e in cfg["output_layers"]]
     return Model(ins if len(ins) > 1 else ins[0], outs if len(outs) > 1 else outs[0], name=cfg.get("name"))
+
+
+def _hang_injection():
+    """``DAMD_HANG_AT=rank:step[:attempt]``: this rank stops responding (sleeps forever) at
+    that global step -- the collective-watchdog test's wedged worker."""
+    v = os.environ.get("DAMD_HANG_AT")
+    if not v:
+        return None
+    parts = v.split(":")
+    if len(parts) > 2 and int(os.environ.get("DAMD_RESTART_COUNT", "0")) != int(parts[2]):
+        return None
+    return int(parts[1]) if int(parts[0]) == _runtime.get().rank else None
 
 
 def model_from_config(config: dict) -> Model:

@@ -94,8 +94,10 @@ def _kill_all(procs):
 
 def launch_script(argv: Sequence[str], nproc: int, port_base: Optional[int] = None, max_restarts: int = 0,
                   timeout: Optional[float] = None, env: Optional[dict] = None, python: str = sys.executable,
-                  stdout=None, stderr=None) -> GangResult:
-    """Run ``python argv...`` as ``nproc`` ranks; gang-restart on any failure."""
+                  stdout=None, stderr=None, on_failure=None) -> GangResult:
+    """Run ``python argv...`` as ``nproc`` ranks; gang-restart on any failure.
+    ``on_failure(returncodes)`` is called for every failed attempt (after the gang is
+    killed): a rank's own exit status is kept, the killed survivors read -15 / -9."""
     attempt = 0
     while True:
         base = port_base if port_base is not None else free_port_base(nproc)
@@ -122,6 +124,8 @@ def launch_script(argv: Sequence[str], nproc: int, port_base: Optional[int] = No
         if failed:
             _kill_all(procs)
         rcs = [p.returncode if p.returncode is not None else -9 for p in procs]
+        if failed and on_failure is not None:
+            on_failure(rcs)
         if not failed or attempt >= max_restarts:
             return GangResult(rcs, attempt + 1)
         attempt += 1

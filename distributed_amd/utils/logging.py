@@ -32,3 +32,7 @@ def warning(msg, *a):
 
 def debug(msg, *a):
     get_logger().debug(msg, *a)
+
+
+def error(msg, *a):
+    get_logger().error(msg, *a)

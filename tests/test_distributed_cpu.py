@@ -296,3 +296,52 @@ def test_batchnorm_moving_stats_are_replica_mean(tmp_path, epoch_sync):
     if not epoch_sync:
         assert outs[0]["differed"], "per-rank statistics should differ before the sync"
         assert outs[0]["max_err"] < 1e-6
+
+
+@pytest.mark.timeout(300)
+def test_watchdog_turns_a_hung_rank_into_a_gang_restart(tmp_path):
+    """Rank 1 stops responding in the middle of epoch 3 (first attempt only).  Rank 0 blocks
+    in the gradient all-reduce; its collective watchdog fires after DAMD_WATCHDOG_S, exits
+    with status 75, the launcher kills the gang and restarts it, and BackupAndRestore
+    resumes from the epoch-2 backup: the result equals an uninterrupted run."""
+    from distributed_amd.utils.watchdog import EXIT_CODE
+
+    ft = os.path.join(ROOT, "tests", "helpers", "ft_worker.py")
+    ref = tmp_path / "ref"
+    ref.mkdir()
+    res = launch.launch_script([ft], nproc=2, env=_env(ref), timeout=240)
+    assert res.ok, res.returncodes
+    run = tmp_path / "hang"
+    run.mkdir()
+    attempts = []
+    res = launch.launch_script([ft], nproc=2, env=_env(run, DAMD_HANG_AT="1:7:0", DAMD_WATCHDOG_S=4), timeout=240,
+                               max_restarts=1, on_failure=lambda rcs: attempts.append(list(rcs)))
+    assert res.ok, res.returncodes
+    assert res.attempts == 2
+    assert EXIT_CODE in attempts[0], attempts  # the watchdog, not the launcher's timeout, ended attempt 1
+    w_ref, j_ref = _load(ref, 0)
+    w_h, j_h = _load(run, 0)
+    assert j_h["attempt"] == 1 and j_h["iterations"] == j_ref["iterations"] == 12
+    for a, b in zip(w_h, w_ref):
+        np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
+    assert len(j_h["history"]["loss"]) == 2  # resumed at epoch 3
+
+
+def test_watchdog_unit():
+    from distributed_amd.utils.watchdog import Watchdog
+
+    fired, aborted = [], []
+    wd = Watchdog(0.3, on_expire=fired.append)
+    wd.add_abort(lambda: aborted.append(1))
+    wd.arm("unit")
+    for _ in range(6):  # beats keep it quiet
+        import time as _t
+
+        _t.sleep(0.1)
+        wd.beat()
+    assert not fired
+    import time as _t
+
+    _t.sleep(1.0)
+    assert fired and aborted == [1] and "unit" in fired[0]
+    wd.close()
