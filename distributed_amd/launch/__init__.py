@@ -98,6 +98,19 @@ def launch_script(argv: Sequence[str], nproc: int, port_base: Optional[int] = No
     """Run ``python argv...`` as ``nproc`` ranks; gang-restart on any failure.
     ``on_failure(returncodes)`` is called for every failed attempt (after the gang is
     killed): a rank's own exit status is kept, the killed survivors read -15 / -9."""
+    return launch_command([python] + list(argv), nproc, port_base=port_base, max_restarts=max_restarts,
+                          timeout=timeout, env=env, stdout=stdout, stderr=stderr, on_failure=on_failure)
+
+
+def launch_command(cmd: Sequence[str], nproc: int, port_base: Optional[int] = None, max_restarts: int = 0,
+                   timeout: Optional[float] = None, env: Optional[dict] = None, stdout=None, stderr=None,
+                   on_failure=None, rank_arg: bool = False) -> GangResult:
+    """Gang-run any command (an ``Rscript`` runner for the R ``spark_apply``, a Python script,
+    ...) as ``nproc`` ranks with the per-rank environment of :func:`rank_env`
+    (``rank_arg=True`` also appends the rank to the command line).  All-or-nothing: the
+    gang's exit statuses are polled; the first failure (or the ``timeout``) kills every
+    survivor's process group and the whole gang restarts, up to ``max_restarts`` times
+    (Spark barrier-stage semantics, reference README.md:171-223)."""
     attempt = 0
     while True:
         base = port_base if port_base is not None else free_port_base(nproc)
@@ -106,8 +119,8 @@ def launch_script(argv: Sequence[str], nproc: int, port_base: Optional[int] = No
             e = dict(os.environ)
             e.update(env or {})
             e.update(rank_env(r, nproc, base, attempt))
-            procs.append(subprocess.Popen([python] + list(argv), env=e, stdout=stdout, stderr=stderr,
-                                          start_new_session=True))
+            argv = list(cmd) + ([str(r)] if rank_arg else [])
+            procs.append(subprocess.Popen(argv, env=e, stdout=stdout, stderr=stderr, start_new_session=True))
         t0 = time.time()
         failed = False
         while True:
