@@ -88,6 +88,9 @@ def main():
                     help="mnist = the headline config (BASELINE.json); resnet18 = BASELINE.json config 4")
     ap.add_argument("--samples", type=int, default=None, help="synthetic dataset rows")
     ap.add_argument("--graph-steps", type=int, default=None)
+    ap.add_argument("--phases", type=int, default=0,
+                    help="after the timed run, time N more eager steps phase by phase (forward / backward / "
+                         "all-reduce / optimizer) and add them to the JSON line as phases_ms")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and "TF_CONFIG" not in os.environ:
@@ -191,6 +194,7 @@ def main():
     if n > 1:
         dts = comm.allgather_object(dt)
         dt = max(dts)
+    phases = engine.phase_times(args.phases) if args.phases > 0 else None
     m = engine.metrics()
     ms = dt * 1e3 / args.steps
     value = GB * args.steps / dt
@@ -227,6 +231,8 @@ def main():
             "allreduce": getattr(engine, "allreduce_kind", "none"),
             "rccl_ranks": _rccl_ranks(comm),
         }
+        if phases is not None:
+            out["phases_ms"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in phases.items()}
         print(json.dumps(out), flush=True)
     runtime.shutdown()
 

@@ -8,6 +8,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 #include "comm.h"
 #include "convnet.h"
@@ -63,6 +64,35 @@ class ConvNetTrainer : public StepExecutor {
       phconv_ = P_<long long>(g("phconv"));
       psync_ = P_<unsigned>(g("psync"));
     }
+  }
+  // Phase timing: k eager steps of the 2-launch step with HIP events
+  // between the forward launch, the backward launch and the gradient all-reduce; returns
+  // per step [forward_ms, backward_ms, allreduce_ms] (the SGD update is fused into the
+  // forward kernel: it applies the previous step's deferred update)
+  std::vector<std::vector<float>> phase_times(int k) {
+    if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
+    if (b_.kernels != 2) throw std::runtime_error("phase timing covers the 2-launch step");
+    hipEvent_t ev[4];
+    for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+    std::vector<std::vector<float>> out;
+    for (int i = 0; i < k; ++i) {
+      HIP_CHECK(hipEventRecord(ev[0], stream_));
+      HIP_CHECK(convnet2_launch_fwd(b_, B_, PP_, stream_));
+      HIP_CHECK(hipEventRecord(ev[1], stream_));
+      HIP_CHECK(convnet2_launch_bwd(b_, B_, PP_, stream_));
+      HIP_CHECK(hipEventRecord(ev[2], stream_));
+      if (grad_allreduce_) {
+        if (peer_) peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, b_.hconv, 2 * kConvNetNConv);
+        else if (comm_) comm_->allreduce_f32_i64(b_.G, convnet_grad_count(PP_), b_.hconv, 2 * kConvNetNConv, stream_);
+      }
+      HIP_CHECK(hipEventRecord(ev[3], stream_));
+      HIP_CHECK(hipEventSynchronize(ev[3]));
+      std::vector<float> r(3);
+      for (int j = 0; j < 3; ++j) HIP_CHECK(hipEventElapsedTime(&r[j], ev[j], ev[j + 1]));
+      out.push_back(r);
+    }
+    for (auto& e : ev) hipEventDestroy(e);
+    return out;
   }
   // k training steps in ONE launch of the persistent kernel (world 1; no graph needed)
   void run_persistent(int k, double timeout_s) {
@@ -199,6 +229,7 @@ PYBIND11_MODULE(_C, m) {
       .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
       .def("run_persistent", &ConvNetTrainer::run_persistent, py::arg("steps"), py::arg("timeout_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
+      .def("phase_times", &ConvNetTrainer::phase_times, py::arg("steps"), py::call_guard<py::gil_scoped_release>())
       .def("flush", &ConvNetTrainer::flush)
       .def("sync", &ConvNetTrainer::sync, py::arg("timeout_s") = 0.0,
            py::call_guard<py::gil_scoped_release>())

@@ -35,6 +35,9 @@ hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st)
 size_t convnet2_fwd_lds(int PP, int lg);
 size_t convnet2_bwd_lds(int PP);
 hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
+// the two launches separately (phase timing)
+hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
+hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st);
 hipError_t convnet2_set_lds_limits();
 // the persistent multi-step kernel (convnet_persist.hip): world 1, B <= 64, 3 positions per slice

@@ -672,13 +672,19 @@ size_t convnet2_bwd_lds(int PP) {
 }
 
 template <bool U8>
-static void launch2_impl(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
   const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
   hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.X, b.P, b.G, b.V, b.W1alt,
                      b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, b.stamps);
+}
+
+template <bool U8>
+static void launch2_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+  using namespace convnet;
+  const int NS = convnet_num_slices(PP);
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.X, b.labels, b.P,
                        b.G, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, B, PP,
@@ -689,12 +695,24 @@ static void launch2_impl(const ConvNetBuffers& b, int B, int PP, hipStream_t st)
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
 }
 
-hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+  if (!b.hacc || !b.hconv || !b.calt) return hipErrorInvalidValue;
+  if (b.x_u8) launch2_fwd<true>(b, B, PP, st);
+  else launch2_fwd<false>(b, B, PP, st);
+  return hipGetLastError();
+}
+
+hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   if (!b.hacc || !b.hconv || !b.calt) return hipErrorInvalidValue;
   if (convnet2_bwd_lds(PP) > 160 * 1024) return hipErrorInvalidValue;
-  if (b.x_u8) launch2_impl<true>(b, B, PP, st);
-  else launch2_impl<false>(b, B, PP, st);
+  if (b.x_u8) launch2_bwd<true>(b, B, PP, st);
+  else launch2_bwd<false>(b, B, PP, st);
   return hipGetLastError();
+}
+
+hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+  hipError_t e = convnet2_launch_fwd(b, B, PP, st);
+  return e != hipSuccess ? e : convnet2_launch_bwd(b, B, PP, st);
 }
 
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {

@@ -56,6 +56,18 @@ class Engine:
     def sync(self):
         pass
 
+    def phase_times(self, n_steps: int) -> dict:
+        """Mean milliseconds per step of the step's phases (forward / backward / all-reduce /
+        optimizer) over ``n_steps`` real training steps run eagerly with timing points between
+        the phases.  Engines override; the base reports the whole step only."""
+        import time
+
+        self.sync()
+        t0 = time.perf_counter()
+        self.run(n_steps)
+        self.sync()
+        return {"step": (time.perf_counter() - t0) * 1e3 / max(n_steps, 1)}
+
     def _own_variables(self, variables):
         """Route host writes of these variables (set_weights, load_weights, layer-level
         assign) through before/after_external_write."""

@@ -325,6 +325,23 @@ class FusedConvNetEngine(Engine):
         self._pending = True
         self.steps_done += n_steps
 
+    def phase_times(self, n_steps: int) -> dict:
+        """forward (incl. the fused SGD update of the previous step's gradient), backward and
+        gradient all-reduce, from HIP events between the launches of eager 2-launch steps."""
+        if self.kernels != 2 or self.host_collective:
+            return super().phase_times(n_steps)
+        self.sync()
+        rows = self.trainer.phase_times(int(n_steps))
+        self._pending = True
+        self.steps_done += n_steps
+        n = max(len(rows), 1)
+        fwd = sum(r[0] for r in rows) / n
+        bwd = sum(r[1] for r in rows) / n
+        ar = sum(r[2] for r in rows) / n
+        return {"forward": fwd, "backward": bwd, "allreduce": ar, "optimizer": 0.0,
+                "step": fwd + bwd + ar, "note": "SGD update fused into the forward kernel",
+                "allreduce_kind": self.allreduce_kind}
+
     def prepare(self, n_steps):
         if self.persist:
             return

@@ -98,6 +98,40 @@ class GenericEngine(Engine):
         self.step_in_epoch = 0
         self.acc.zero_()
 
+    def _tick(self, name):
+        ph = getattr(self, "_phases", None)
+        if ph is None:
+            return
+        import time
+
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        t = time.perf_counter()
+        ph[name] = ph.get(name, 0.0) + (t - self._t_last) * 1e3
+        self._t_last = t
+
+    def phase_times(self, n_steps: int) -> dict:
+        """Host-timed phases (device synchronised at each point): forward + loss, backward
+        (bucketed all-reduces already launched inside it), the wait for the all-reduce,
+        optimizer."""
+        import time
+
+        self.sync()
+        self._phases = {}
+        try:
+            for _ in range(n_steps):
+                left = self.feed.n // max(self.global_batch, 1) - self.step_in_epoch
+                if left <= 0:
+                    self.start_epoch(0, False)
+                self._t_last = time.perf_counter()
+                self._one_step()
+            out = {k: v / max(n_steps, 1) for k, v in self._phases.items()}
+        finally:
+            self._phases = None
+        out["step"] = sum(out.values())
+        out["allreduce_kind"] = self.allreduce_kind
+        return out
+
     def _one_step(self):
         feed, model = self.feed, self.model
         s = self.step_in_epoch
@@ -112,6 +146,7 @@ class GenericEngine(Engine):
             out = model(xb, training=True)
             ls = self.loss.per_sample(yb, out)
             loss = ls.sum() * (1.0 / gcount)
+            self._tick("forward")
             with torch.no_grad():
                 G[self.n] = ls.detach().sum()
                 G[self.n + 1] = float(idx.numel())
@@ -129,14 +164,17 @@ class GenericEngine(Engine):
             # sequence as the others: one all-reduce per bucket, in bucket order
             comm = self.strategy.communicator
             works = [comm.allreduce_async(G[lo:hi], "sum") for (lo, hi, _) in self.buckets]
+        self._tick("backward")
         if works is not None:
             for w in works:
                 w.wait()
         elif self.world > 1:
             self.strategy.communicator.allreduce_(G, "sum")
+        self._tick("allreduce")
         self.model.optimizer.apply_flat(self.P, G[: self.n])
         self.acc += G[self.n:].double()
         self.step_in_epoch += 1
+        self._tick("optimizer")
 
     def _backward_bucketed(self, loss):
         comm, G = self.strategy.communicator, self.G

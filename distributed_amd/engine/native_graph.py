@@ -209,6 +209,7 @@ class NativeGraphEngine(Engine):
                                "rccl-bucketed" if self.native_comm is not None else "host-gloo")
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph = None
+        self._phase_events = None  # phase_times(): (name, event) marks of an eager step
         self.feed = None
         self._plan()
         self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0))
@@ -641,9 +642,17 @@ class NativeGraphEngine(Engine):
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
 
     # --- the step ----------------------------------------------------------------------------
+    def _mark(self, name):
+        ev = self._phase_events
+        if ev is not None:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ev.append((name, e))
+
     def _step_body(self):
         C, B = self.C, self.B
         s = H.stream_handle()
+        self._mark("start")
         h, w, c = self.in_shape
         self.G.zero_()
         C.gather_batch(self.x_ep.data_ptr(), int(self.feed.x_u8), 255.0, self.y_ep.data_ptr(), self.ctrl.data_ptr(),
@@ -653,6 +662,7 @@ class NativeGraphEngine(Engine):
             getattr(self, "_fwd_" + nd.kind)(nd)
         H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:],
                        ctrl=self.ctrl)
+        self._mark("forward")
         for t in self._all_tensors():
             t.root().written = False
         self._bucket_begin()
@@ -661,9 +671,12 @@ class NativeGraphEngine(Engine):
             self._bucket_progress(nd)
         if self._wgrad_stream is not None:  # join the weight-gradient branch
             torch.cuda.current_stream(self.device).wait_stream(self._wgrad_stream)
+        self._mark("backward")
         self._bucket_progress(None, final=True)
+        self._mark("allreduce")  # the part of the all-reduce not hidden behind backward
         if not self.host_collective:
             self._optimizer_step()
+        self._mark("optimizer")
 
     def _optimizer_step(self):
         self.C.sgd_step(self.P.data_ptr(), self.G.data_ptr(), self.V.data_ptr(), self.Pb.data_ptr(), self.nparam,
@@ -982,6 +995,25 @@ class NativeGraphEngine(Engine):
             if self.graph is None:
                 self._capture_safe()
             self.graph.replay()
+
+    def phase_times(self, n_steps: int) -> dict:
+        """Per-phase device time of eager steps: forward (incl. loss), backward, the exposed
+        all-reduce (what is left after the buckets overlapped backward), optimizer."""
+        if self.host_collective:
+            return super().phase_times(n_steps)
+        self.sync()
+        acc = {}
+        for _ in range(n_steps):
+            self._phase_events = []
+            self._step_body()
+            evs, self._phase_events = self._phase_events, None
+            torch.cuda.synchronize(self.device)
+            for (_, a), (name, b) in zip(evs, evs[1:]):
+                acc[name] = acc.get(name, 0.0) + a.elapsed_time(b)
+        out = {k: v / max(n_steps, 1) for k, v in acc.items()}
+        out["step"] = sum(out.values())
+        out["allreduce_kind"] = self.allreduce_kind
+        return out
 
     def prepare(self, n_steps):
         if self.use_graph and not self.host_collective and self.graph is None and n_steps > 0:

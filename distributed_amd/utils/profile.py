@@ -5,6 +5,11 @@ per engine chunk (a run of k training steps), device time from HIP events and ho
 time, and writes a JSON summary (steps, mean/min/max ms per step, images/sec).  Chunks
 are also bracketed by roctx ranges (``torch.cuda.nvtx`` maps to roctx on ROCm), so a
 ``rocprofv3 --marker-trace`` run shows them on the timeline next to the kernels.
+
+:func:`step_phases` breaks a training step into forward / backward / all-reduce /
+optimizer time (HIP events between the phases of eager steps; the engines'
+``phase_times``), which is how the all-reduce share of a multi-GPU step is reported
+(``bench.py --phases``).
 """
 from __future__ import annotations
 
@@ -84,3 +89,25 @@ def profile(path: Optional[str] = None):
     finally:
         p, _ACTIVE = _ACTIVE, prev
         p.write()
+
+
+def step_phases(model, x, y, batch_size: int, steps: int = 20, path: Optional[str] = None) -> dict:
+    """Mean ms per step of each phase over ``steps`` real training steps of ``model`` on
+    (x, y) at global ``batch_size`` (the model trains: run it on a copy if that matters).
+    Every replica must call it (the steps contain the gradient all-reduce)."""
+    st = model._strategy
+    per = batch_size // st.num_replicas_in_sync
+    eng = model._get_engine(per, batch_size)
+    eng.bind(x, y)
+    eng.start_epoch(0, False)
+    eng.run(1)  # warm (plans, graph capture of the timed engines is not used here)
+    eng.sync()
+    out = eng.phase_times(steps)
+    out = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in out.items()}
+    out["engine"] = eng.name
+    out["steps"] = steps
+    if path:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    return out
+

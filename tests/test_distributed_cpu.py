@@ -345,3 +345,23 @@ def test_watchdog_unit():
     _t.sleep(1.0)
     assert fired and aborted == [1] and "unit" in fired[0]
     wd.close()
+
+
+@pytest.mark.timeout(200)
+def test_step_phases_include_the_allreduce_share(tmp_path):
+    """bench.py --phases on 2 gloo ranks: forward / backward / all-reduce / optimizer times
+    of the generic engine, reported next to the throughput."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "TF_CONFIG", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["DAMD_DEVICE"] = "cpu"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--engine", "generic",
+                        "--steps", "2", "--warmup", "1", "--phases", "3"], cwd=str(tmp_path), env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    ph = out["phases_ms"]
+    for k in ("forward", "backward", "allreduce", "optimizer", "step"):
+        assert ph[k] >= 0, ph
+    assert ph["forward"] > 0 and ph["backward"] > 0
+    assert abs(ph["step"] - (ph["forward"] + ph["backward"] + ph["allreduce"] + ph["optimizer"])) < 1e-3

@@ -337,3 +337,20 @@ def test_persistent_kernel_one_step_and_metrics(monkeypatch):
         assert np.linalg.norm((a - b) / lr - g) / (np.linalg.norm(g) + 1e-12) < 5e-3
     assert abs(met["loss"] - lsum / 64) < 2e-2
     assert abs(met["accuracy"] - corr / 64) < 1.5 / 64
+
+
+def test_phase_times_fused_step():
+    """HIP-event phase split of the 2-launch step: forward, backward, all-reduce (world 1:
+    none) -- and the steps it ran are real training steps."""
+    _need_gpu()
+    m = _model(lr=0.05)
+    x, y = _data(1024)
+    eng = _engine(m, 64)
+    eng.bind(x, y)
+    eng.start_epoch(0, shuffle=False)
+    it0 = int(m.optimizer.iterations)
+    ph = eng.phase_times(5)
+    eng.end_epoch()
+    print("fused step phases (ms):", ph)
+    assert ph["forward"] > 0 and ph["backward"] > 0 and ph["allreduce"] >= 0
+    assert int(m.optimizer.iterations) == it0 + 5

@@ -398,3 +398,26 @@ def test_u8_batch_gather_matches_float_feed():
     for a, b in zip(wa, wb):
         np.testing.assert_allclose(a, b, rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-6)
+
+
+def test_phase_times_native_graph():
+    import numpy as np
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import distributed_amd as tf
+    from distributed_amd.utils.profile import step_phases
+
+    tf.set_seed(3)
+    m = tf.models.resnet18(classes=10, input_shape=(32, 32, 3), widths=(16, 32, 32, 64), blocks=(1, 1, 1, 1))
+    tf.models.compile_resnet(m, 0.05, 0.9)
+    rng = np.random.default_rng(0)
+    x = rng.random((256, 32, 32, 3), dtype=np.float32)
+    y = rng.integers(0, 10, 256)
+    ph = step_phases(m, x, y, batch_size=32, steps=4)
+    print("native graph phases (ms):", ph)
+    assert ph["engine"] == "native_graph"
+    for k in ("forward", "backward", "allreduce", "optimizer"):
+        assert ph[k] >= 0
+    assert ph["forward"] > 0 and ph["backward"] > 0
