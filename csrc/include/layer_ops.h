@@ -53,6 +53,18 @@ hipError_t gap_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* d
 // Elementwise -----------------------------------------------------------------------------
 // dz = dy * [y > 0]  (bf16)
 hipError_t relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, long n, hipStream_t s);
+// y = act(x) / dx = dy * act'(y), kind 0 relu, 1 sigmoid, 2 tanh (bf16, any length, in place ok)
+hipError_t act_fwd(const uint16_t* x, uint16_t* y, long n, int kind, hipStream_t s);
+hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, int kind, hipStream_t s);
+// y = x * keep / (1 - rate), keep from a counter hash of (seed, ctrl->cur3, element): the
+// same call with the same seed is the backward (dx from dy)
+hipError_t dropout(const uint16_t* x, uint16_t* y, long n, const Ctrl* ctrl, uint32_t seed, float rate,
+                   hipStream_t s);
+// average pooling, divisor = in-bounds taps (TF 'same' semantics)
+hipError_t avgpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
+                       int pad_l, int Ho, int Wo, uint16_t* y, hipStream_t s);
+hipError_t avgpool_bwd(const uint16_t* dy, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
+                       int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s);
 // out = a + b (bf16)
 hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n, hipStream_t s);
 // fp32 -> bf16
@@ -84,13 +96,22 @@ hipError_t sgd_flat(float* P, const float* G, float* V, uint16_t* Pb, long n, fl
 struct Ctrl;
 hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ctrl* ctrl, const float* tail,
                     hipStream_t s);
+// kind 0 SGD (S0 momentum; flag = nesterov), 1 Adam (S0 m, S1 v, S2 vhat; flag = amsgrad),
+// 2 RMSprop (S0 rms, S1 momentum, S2 mean gradient; flag = centered)
+struct OptArgs {
+  int kind;
+  float b1, b2, eps, rho, mom;
+  int flag;
+};
+hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, uint16_t* Pb, long n, Ctrl* ctrl,
+                    const float* tail, const OptArgs& o, hipStream_t s);
 
 // Data / layout glue -------------------------------------------------------------------------
 // the step's rows of the (epoch-permuted) dataset: row = (cursor*global_batch + row0 + i)
 // mod nsamples (cursor from ctrl); x fp32 or uint8 (k / scale, i.e. exactly float32(k/255)
 // for scale 255) [n][HW][Cin] -> bf16
 // [per][HW][Cp] zero-padded channels; labels int32.
-hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, const Ctrl* ctrl, int per,
+hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
                         int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s);
 // fp32 [R][C1][C2] -> bf16 [R][C1p][C2p] (zero padding)
 hipError_t pad_cast(const float* src, int R, int C1, int C2, int C1p, int C2p, uint16_t* dst, hipStream_t s);

@@ -342,6 +342,82 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_k(const uint16_t* __restrict__
   }
 }
 
+// Average pooling (Keras AveragePooling2D): the divisor is the number of in-bounds taps, so
+// 'same' windows that overhang the border average only real pixels (TF's avg_pool) and
+// 'valid' windows divide by ph*pw.  The backward is a gather over the output windows that
+// cover each input pixel (no atomics, every dx written once).
+__device__ __forceinline__ float pool_inv_count(int oh, int ow, const PoolGeo& g) {
+  const int h0 = oh * g.sh - g.pt, w0 = ow * g.sw - g.pl;
+  const int nh = min(h0 + g.ph, g.H) - max(h0, 0), nw = min(w0 + g.pw, g.W) - max(w0, 0);
+  return 1.f / (float)(nh * nw);
+}
+
+__global__ __launch_bounds__(NT) void avgpool_fwd_k(const uint16_t* __restrict__ x, PoolGeo g,
+                                                    uint16_t* __restrict__ y) {
+  const int cg = g.C / 8;
+  const long total = (long)g.N * g.Ho * g.Wo * cg;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    long pix = i / cg;
+    const int ow = (int)(pix % g.Wo);
+    pix /= g.Wo;
+    const int oh = (int)(pix % g.Ho);
+    const int n = (int)(pix / g.Ho);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int kh = 0; kh < g.ph; ++kh) {
+      const int ih = oh * g.sh - g.pt + kh;
+      if ((unsigned)ih >= (unsigned)g.H) continue;
+      for (int kw = 0; kw < g.pw; ++kw) {
+        const int iw = ow * g.sw - g.pl + kw;
+        if ((unsigned)iw >= (unsigned)g.W) continue;
+        float v[8];
+        unpack8(reinterpret_cast<const uint4*>(x)[(((long)n * g.H + ih) * g.W + iw) * cg + c8], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    }
+    const float inv = pool_inv_count(oh, ow, g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    reinterpret_cast<uint4*>(y)[i] = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(NT) void avgpool_bwd_k(const uint16_t* __restrict__ dy, PoolGeo g,
+                                                    uint16_t* __restrict__ dx) {
+  const int cg = g.C / 8;
+  const long total = (long)g.N * g.H * g.W * cg;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
+    const int c8 = (int)(i % cg);
+    long pix = i / cg;
+    const int iw = (int)(pix % g.W);
+    pix /= g.W;
+    const int ih = (int)(pix % g.H);
+    const int n = (int)(pix / g.H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const int ohlo = max(0, (ih + g.pt - g.ph + g.sh) / g.sh), ohhi = min(g.Ho - 1, (ih + g.pt) / g.sh);
+    const int owlo = max(0, (iw + g.pl - g.pw + g.sw) / g.sw), owhi = min(g.Wo - 1, (iw + g.pl) / g.sw);
+    for (int oh = ohlo; oh <= ohhi; ++oh) {
+      const int kh = ih - (oh * g.sh - g.pt);
+      if (kh < 0 || kh >= g.ph) continue;
+      for (int ow = owlo; ow <= owhi; ++ow) {
+        const int kw = iw - (ow * g.sw - g.pl);
+        if (kw < 0 || kw >= g.pw) continue;
+        float d[8];
+        unpack8(reinterpret_cast<const uint4*>(dy)[(((long)n * g.Ho + oh) * g.Wo + ow) * cg + c8], d);
+        const float inv = pool_inv_count(oh, ow, g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += d[e] * inv;
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = pack8(acc);
+  }
+}
+
 // ---- stem fusion: BatchNorm -> ReLU -> MaxPool without the normalised tensor ----------
 // Forward: the pool reads the conv output x and normalises on the fly (the BN+ReLU output
 // is never stored); each candidate is rounded to bf16 exactly as bn_apply stores it, so
@@ -856,6 +932,91 @@ __global__ __launch_bounds__(NT) void relu_bwd_k(const uint16_t* dy, const uint1
   }
 }
 
+// Pointwise activations on bf16 tensors (kind 0 relu, 1 sigmoid, 2 tanh).  The backward
+// reads the stored output y: relu' = [y > 0], sigmoid' = y (1 - y), tanh' = 1 - y^2.  A
+// thread owns 8 elements (one 16-byte access); the last, partial group of a length that
+// is not a multiple of 8 goes element by element.
+__device__ __forceinline__ float act_f(float z, int kind) {
+  if (kind == 1) return 1.f / (1.f + __expf(-z));
+  if (kind == 2) return tanhf(z);
+  return fmaxf(z, 0.f);
+}
+__device__ __forceinline__ float act_df(float y, int kind) {
+  if (kind == 1) return y * (1.f - y);
+  if (kind == 2) return 1.f - y * y;
+  return y > 0.f ? 1.f : 0.f;
+}
+
+__global__ __launch_bounds__(NT) void act_fwd_k(const uint16_t* x, uint16_t* y, long n, int kind) {
+  const long n8 = (n + 7) / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    if (8 * i + 8 <= n) {
+      float v[8];
+      unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_f(v[e], kind);
+      reinterpret_cast<uint4*>(y)[i] = pack8(v);
+    } else {
+      for (long j = 8 * i; j < n; ++j) y[j] = f2bf(act_f(bf2f(x[j]), kind));
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void act_bwd_k(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n,
+                                                int kind) {
+  const long n8 = (n + 7) / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    if (8 * i + 8 <= n) {
+      float d[8], yv[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[i], d);
+      unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] *= act_df(yv[e], kind);
+      reinterpret_cast<uint4*>(dx)[i] = pack8(d);
+    } else {
+      for (long j = 8 * i; j < n; ++j) dx[j] = f2bf(bf2f(dy[j]) * act_df(bf2f(y[j]), kind));
+    }
+  }
+}
+
+// Dropout with a counter-based mask: element j of step t is kept iff
+// drop_hash(key_t, j) >= rate * 2^32, key_t = mix32(seed + t * golden), t = ctrl->cur3 (the
+// step's iteration, set by gather_batch).  No mask tensor and no RNG state: the backward
+// regenerates the same mask from (seed, t, j), and a graph replay draws a fresh mask
+// because t advances on the device.  Kept elements are scaled by 1 / (1 - rate).
+// distributed_amd/engine/native_graph.py:dropout_mask_reference is the host oracle.
+__device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+
+__global__ __launch_bounds__(NT) void dropout_k(const uint16_t* x, uint16_t* y, long n, const Ctrl* ctrl,
+                                                uint32_t seed, uint32_t thr, float scale) {
+  const uint32_t key = mix32(seed + (uint32_t)ctrl->cur3 * 0x9e3779b9u);
+  const long n8 = (n + 7) / 8;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
+    if (8 * i + 8 <= n) {
+      float v[8];
+      unpack8(reinterpret_cast<const uint4*>(x)[i], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t h = mix32(mix32((uint32_t)(8 * i + e) ^ key) + key);
+        v[e] = h >= thr ? v[e] * scale : 0.f;
+      }
+      reinterpret_cast<uint4*>(y)[i] = pack8(v);
+    } else {
+      for (long j = 8 * i; j < n; ++j) {
+        const uint32_t h = mix32(mix32((uint32_t)j ^ key) + key);
+        y[j] = f2bf(h >= thr ? bf2f(x[j]) * scale : 0.f);
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(NT) void add_bf16_k(const uint16_t* a, const uint16_t* b, uint16_t* o, long n8) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     float x[8], y[8];
@@ -992,12 +1153,13 @@ __global__ __launch_bounds__(NT) void sgd_step_k(float* __restrict__ P, const fl
 }
 
 __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x, int x_u8, float scale,
-                                                     const int32_t* __restrict__ labels, const Ctrl* __restrict__ ctrl,
+                                                     const int32_t* __restrict__ labels, Ctrl* __restrict__ ctrl,
                                                      int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
                                                      int32_t* __restrict__ yb) {
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctrl->cur3 = ctrl->iterations + 1;  // this step's t (opt_step)
   if (Cp == 4 && Cin == 3 && x_u8 && HW % 4 == 0) {
     // RGB uint8 rows -> packed 4-channel bf16: one thread per 4 pixels of one row, the 12
     // source bytes as three aligned dword loads (byte loads moved 64 B per wave
@@ -1103,13 +1265,83 @@ __global__ __launch_bounds__(NT) void unpad_add_k(const float* src, int R, int C
 
 }  // namespace
 
+// Keras optimizer_v2 update rules on the flat fp32 master buffer (+ bf16 shadow): the
+// native-engine counterpart of keras/optimizers.py apply_flat.  lr from ctrl (a schedule
+// needs no re-capture); Adam's step t = ctrl->cur3, written by gather_batch at the start
+// of the step (no block of this kernel reads a ctrl field this kernel writes).
+__global__ __launch_bounds__(NT) void opt_step_k(float* __restrict__ P, const float* __restrict__ G,
+                                                 float* __restrict__ S0, float* __restrict__ S1,
+                                                 float* __restrict__ S2, uint16_t* __restrict__ Pb, long n,
+                                                 Ctrl* ctrl, const float* tail, OptArgs o) {
+  const float lr = ctrl->lr;
+  const int t = ctrl->cur3;
+  float lr_t = lr;
+  if (o.kind == 1) lr_t = lr * sqrtf(1.f - powf(o.b2, (float)t)) / (1.f - powf(o.b1, (float)t));
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) {
+    const float g = G[i];
+    float w = P[i];
+    if (o.kind == 1) {  // Adam (S0 m, S1 v, S2 vhat)
+      const float m = o.b1 * S0[i] + (1.f - o.b1) * g;
+      const float v = o.b2 * S1[i] + (1.f - o.b2) * g * g;
+      S0[i] = m;
+      S1[i] = v;
+      float d = v;
+      if (o.flag) {
+        d = fmaxf(S2[i], v);
+        S2[i] = d;
+      }
+      w -= lr_t * (m / (sqrtf(d) + o.eps));
+    } else if (o.kind == 2) {  // RMSprop (S0 rms, S1 momentum, S2 mg)
+      const float ms = o.rho * S0[i] + (1.f - o.rho) * g * g;
+      S0[i] = ms;
+      float den = ms;
+      if (o.flag) {
+        const float mg = o.rho * S2[i] + (1.f - o.rho) * g;
+        S2[i] = mg;
+        den = ms - mg * mg;
+      }
+      const float upd = g / (sqrtf(den) + o.eps) * lr;
+      if (o.mom != 0.f) {
+        const float mo = o.mom * S1[i] + upd;
+        S1[i] = mo;
+        w -= mo;
+      } else {
+        w -= upd;
+      }
+    } else {  // SGD (S0 momentum)
+      float wn, vn;
+      sgd_update(w, g, o.mom != 0.f ? S0[i] : 0.f, lr, o.mom, o.flag, wn, vn);
+      if (o.mom != 0.f) S0[i] = vn;
+      w = wn;
+    }
+    P[i] = w;
+    Pb[i] = f2bf(w);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctrl->acc_loss += tail[0];
+    ctrl->acc_correct += tail[1];
+    ctrl->acc_count += tail[2];
+    int c = ctrl->cursor + 1;
+    if (ctrl->wrap > 0 && c >= ctrl->wrap) c = 0;
+    ctrl->cursor = c;
+    ctrl->iterations = t;
+  }
+}
+
+hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, uint16_t* Pb, long n, Ctrl* ctrl,
+                    const float* tail, const OptArgs& o, hipStream_t s) {
+  if (o.kind < 0 || o.kind > 2) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(opt_step_k, dim3(grid_for(n, NT, 4096)), dim3(NT), 0, s, P, G, S0, S1, S2, Pb, n, ctrl, tail, o);
+  return hipGetLastError();
+}
+
 hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ctrl* ctrl, const float* tail,
                     hipStream_t s) {
   hipLaunchKernelGGL(sgd_step_k, dim3(grid_for(n, NT, 4096)), dim3(NT), 0, s, P, G, V, Pb, n, ctrl, tail);
   return hipGetLastError();
 }
 
-hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, const Ctrl* ctrl, int per,
+hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
                         int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s) {
   if (Cp % 8 && !(Cp == 4 && Cin <= 4 && HW % 2 == 0)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp / 8)), dim3(NT), 0, s, x, x_u8, scale, labels,
@@ -1257,6 +1489,43 @@ hipError_t gap_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* d
 hipError_t relu_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dz, long n, hipStream_t s) {
   if (n % 8) return hipErrorInvalidValue;
   hipLaunchKernelGGL(relu_bwd_k, dim3(grid_for(n / 8)), dim3(NT), 0, s, dy, y, dz, n / 8);
+  return hipGetLastError();
+}
+
+hipError_t act_fwd(const uint16_t* x, uint16_t* y, long n, int kind, hipStream_t s) {
+  if (kind < 0 || kind > 2 || n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(act_fwd_k, dim3(grid_for((n + 7) / 8)), dim3(NT), 0, s, x, y, n, kind);
+  return hipGetLastError();
+}
+
+hipError_t act_bwd(const uint16_t* dy, const uint16_t* y, uint16_t* dx, long n, int kind, hipStream_t s) {
+  if (kind < 0 || kind > 2 || n <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(act_bwd_k, dim3(grid_for((n + 7) / 8)), dim3(NT), 0, s, dy, y, dx, n, kind);
+  return hipGetLastError();
+}
+
+hipError_t dropout(const uint16_t* x, uint16_t* y, long n, const Ctrl* ctrl, uint32_t seed, float rate,
+                   hipStream_t s) {
+  if (!(rate >= 0.f && rate < 1.f) || n <= 0) return hipErrorInvalidValue;
+  const uint32_t thr = (uint32_t)fmin((double)rate * 4294967296.0, 4294967295.0);
+  hipLaunchKernelGGL(dropout_k, dim3(grid_for((n + 7) / 8)), dim3(NT), 0, s, x, y, n, ctrl, seed, thr,
+                     1.f / (1.f - rate));
+  return hipGetLastError();
+}
+
+hipError_t avgpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
+                       int pad_l, int Ho, int Wo, uint16_t* y, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  hipLaunchKernelGGL(avgpool_fwd_k, dim3(grid_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0, s, x, g, y);
+  return hipGetLastError();
+}
+
+hipError_t avgpool_bwd(const uint16_t* dy, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
+                       int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s) {
+  if (C % 8) return hipErrorInvalidValue;
+  PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
+  hipLaunchKernelGGL(avgpool_bwd_k, dim3(grid_for((long)N * H * W * C / 8)), dim3(NT), 0, s, dy, g, dx);
   return hipGetLastError();
 }
 

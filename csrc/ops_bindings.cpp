@@ -143,6 +143,28 @@ void register_kernel_ops(py::module_& m) {
   m.def("relu_bwd", [](U dy, U y, U dz, long n, U s) {
     check(damd::relu_bwd(P_<const u16>(dy), P_<const u16>(y), P_<u16>(dz), n, P_<ihipStream_t>(s)), "relu_bwd");
   });
+  m.def("act_fwd", [](U x, U y, long n, int kind, U s) {
+    check(damd::act_fwd(P_<const u16>(x), P_<u16>(y), n, kind, P_<ihipStream_t>(s)), "act_fwd");
+  });
+  m.def("act_bwd", [](U dy, U y, U dx, long n, int kind, U s) {
+    check(damd::act_bwd(P_<const u16>(dy), P_<const u16>(y), P_<u16>(dx), n, kind, P_<ihipStream_t>(s)), "act_bwd");
+  });
+  m.def("dropout", [](U x, U y, long n, U ctrl, uint32_t seed, float rate, U s) {
+    check(damd::dropout(P_<const u16>(x), P_<u16>(y), n, P_<const damd::Ctrl>(ctrl), seed, rate, P_<ihipStream_t>(s)),
+          "dropout");
+  });
+  m.def("avgpool_fwd", [](U x, std::vector<int> g, U y, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::avgpool_fwd(P_<const u16>(x), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10],
+                            g[11], P_<u16>(y), P_<ihipStream_t>(s)),
+          "avgpool_fwd");
+  });
+  m.def("avgpool_bwd", [](U dy, std::vector<int> g, U dx, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::avgpool_bwd(P_<const u16>(dy), g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8], g[9], g[10],
+                            g[11], P_<u16>(dx), P_<ihipStream_t>(s)),
+          "avgpool_bwd");
+  });
   m.def("add_bf16", [](U a, U b, U o, long n, U s) {
     check(damd::add_bf16(P_<const u16>(a), P_<const u16>(b), P_<u16>(o), n, P_<ihipStream_t>(s)), "add_bf16");
   });
@@ -165,9 +187,16 @@ void register_kernel_ops(py::module_& m) {
                          P_<const float>(tail), P_<ihipStream_t>(s)),
           "sgd_step");
   });
+  m.def("opt_step", [](U P, U G, U S0, U S1, U S2, U Pb, long n, U ctrl, U tail, int kind, float b1, float b2,
+                       float eps, float rho, float mom, int flag, U s) {
+    damd::OptArgs o{kind, b1, b2, eps, rho, mom, flag};
+    check(damd::opt_step(P_<float>(P), P_<const float>(G), P_<float>(S0), P_<float>(S1), P_<float>(S2), P_<u16>(Pb), n,
+                         P_<damd::Ctrl>(ctrl), P_<const float>(tail), o, P_<ihipStream_t>(s)),
+          "opt_step");
+  });
   m.def("gather_batch", [](U x, int x_u8, float scale, U labels, U ctrl, int per, int HW, int Cin, int Cp, U xb, U yb,
                            U s) {
-    check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<const damd::Ctrl>(ctrl),
+    check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<damd::Ctrl>(ctrl),
                              per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s)),
           "gather_batch");
   });

@@ -27,6 +27,7 @@ Fusion rules (decided on the layer graph, not traced):
 from __future__ import annotations
 
 import contextlib
+import gc
 import math
 import struct
 from dataclasses import dataclass, field
@@ -104,11 +105,28 @@ def _layer_graph(model):
     return seq, 0, keys[id(model._outputs[0])], tuple(model._inputs[0].shape[1:])
 
 
+def _act_name(layer) -> str:
+    act = getattr(layer, "activation", None)
+    return getattr(act, "__name__", "linear") if act is not None else "linear"
+
+
+def _opt_kernel_slots(opt):
+    """(opt_step kind, slot names for S0..S2; '' = unused) of a Keras optimizer."""
+    from ..keras import optimizers
+
+    if isinstance(opt, optimizers.Adam):
+        return 1, ["m", "v", "vhat" if opt.amsgrad else ""]
+    if isinstance(opt, optimizers.RMSprop):
+        return 2, ["rms", "momentum" if opt.momentum else "", "mg" if opt.centered else ""]
+    return 0, ["momentum" if opt.momentum else "", "", ""]
+
+
 class NativeGraphEngine(Engine):
     name = "native_graph"
 
     SUPPORTED = ("Conv2D", "BatchNormalization", "Activation", "ReLU", "Add", "MaxPooling2D",
-                 "GlobalAveragePooling2D", "Flatten", "Dense")
+                 "AveragePooling2D", "GlobalAveragePooling2D", "Flatten", "Dense", "Dropout")
+    ACTIVATIONS = ("linear", "relu", "sigmoid", "tanh")
 
     @staticmethod
     def eligible(model, strategy):
@@ -116,8 +134,8 @@ class NativeGraphEngine(Engine):
 
         if strategy.device.type != "cuda":
             return False, "not on a GPU"
-        if type(model.optimizer) is not optimizers.SGD:
-            return False, "optimizer (SGD only)"
+        if type(model.optimizer) not in (optimizers.SGD, optimizers.Adam, optimizers.RMSprop):
+            return False, f"optimizer {type(model.optimizer).__name__}"
         if not (isinstance(model.loss, losses.SparseCategoricalCrossentropy) and model.loss.from_logits):
             return False, "loss"
         for m in model.compiled_metrics:
@@ -135,7 +153,7 @@ class NativeGraphEngine(Engine):
                 return False, f"layer {k}"
             act = getattr(l, "activation", None)
             an = getattr(act, "__name__", "linear") if act is not None else "linear"
-            if k in ("Conv2D", "Dense", "Activation") and an not in ("relu", "linear"):
+            if k in ("Conv2D", "Dense", "Activation") and an not in NativeGraphEngine.ACTIVATIONS:
                 return False, f"activation {an}"
             if k == "ReLU" and (l.max_value is not None or l.negative_slope or l.threshold):
                 return False, "ReLU options"
@@ -146,10 +164,14 @@ class NativeGraphEngine(Engine):
                     return False, "conv stride/filters"
             if k == "MaxPooling2D" and l.pool_size[0] * l.pool_size[1] > 255:
                 return False, "pool size"
+            if k == "Dropout" and not 0.0 <= l.rate < 1.0:
+                return False, "dropout rate"
             if k == "BatchNormalization" and l.axis not in (-1, 3):
                 return False, "BN axis"
             if k == "Add" and len(ins) != 2:
                 return False, "Add arity"
+            if k == "Dense" and l is not seq[-1][0] and l.units % 8:
+                return False, "hidden Dense units must be a multiple of 8"
         last = seq[-1][0]
         if type(last).__name__ != "Dense" or getattr(last.activation, "__name__", "") != "linear":
             return False, "the model must end in a linear Dense (logits)"
@@ -176,7 +198,13 @@ class NativeGraphEngine(Engine):
         self.P = torch.zeros(n, dtype=torch.float32, device=dev)
         self.Pb = torch.zeros(n, dtype=torch.bfloat16, device=dev)
         self.G = torch.zeros(n + 8, dtype=torch.float32, device=dev)  # + metric tail
-        self.V = torch.zeros(n, dtype=torch.float32, device=dev)
+        # optimizer slots (flat, same padded layout as P): SGD momentum; Adam m, v, vhat;
+        # RMSprop rms, momentum, mean gradient -- S0..S2 of the opt_step kernel
+        kind, names = _opt_kernel_slots(model.optimizer)
+        self.opt_kind, self.slot_kernel_names = kind, names
+        self.S = {nm: torch.zeros(n, dtype=torch.float32, device=dev) for nm in names if nm}
+        self._slot_dummy = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.V = self.S.get("momentum", self._slot_dummy)
         self.views, self.bviews, self.gviews = {}, {}, {}
         self.offsets = offs
         for v, sz, off in zip(self.vars, self.sizes, offs):
@@ -294,7 +322,7 @@ class NativeGraphEngine(Engine):
             ho, _ = H.conv_out(x[1], l.kernel_size[0], l.strides[0], l.padding)
             wo, _ = H.conv_out(x[2], l.kernel_size[1], l.strides[1], l.padding)
             return (B, ho, wo, l.filters)
-        if kind == "MaxPooling2D":
+        if kind in ("MaxPooling2D", "AveragePooling2D"):
             g = H.pool_geo(x, l.pool_size, l.strides, l.padding)
             return (B, g[10], g[11], x[3])
         if kind == "GlobalAveragePooling2D":
@@ -311,11 +339,19 @@ class NativeGraphEngine(Engine):
                 return True
             return nd.kind == "Activation" and getattr(nd.layer.activation, "__name__", "") == "relu"
 
-        for nd in self.nodes:
+        for i, nd in enumerate(self.nodes):
             nd.attrs.setdefault("dead", False)
-            if nd.kind == "Activation" and not relu_node(nd):
+            if nd.kind == "Activation" and _act_name(nd.layer) == "linear":
                 nd.attrs["dead"] = True  # linear activation: identity
                 self._alias(nd.out, nd.inputs[0])
+            if nd.kind == "Dropout":
+                if nd.layer.rate == 0.0:
+                    nd.attrs["dead"] = True
+                    self._alias(nd.out, nd.inputs[0])
+                # per-layer, per-replica mask stream (TF draws independent masks per replica)
+                s0 = nd.layer.seed if getattr(nd.layer, "seed", None) is not None else 0x5EED
+                nd.attrs["seed"] = (int(s0) * 0x9E3779B1 + (i + 1) * 0x85EBCA77
+                                    + getattr(self, "rank", 0) * 0xC2B2AE3D) & 0xFFFFFFFF
             if nd.kind == "Flatten":
                 nd.attrs["dead"] = True  # NHWC flatten is a view
                 self._alias(nd.out, nd.inputs[0])
@@ -431,7 +467,7 @@ class NativeGraphEngine(Engine):
                 ws = max(ws, fplan["ws"], H.conv_dgrad_plan(xshape, wshape, l.strides, l.padding)["ws"])
                 if nd.attrs.get("stats"):
                     nd.attrs["stats_buf"] = torch.zeros(fplan["stats_T"], 2, cout, device=dev)
-                if getattr(l.activation, "__name__", "linear") == "relu":
+                if _act_name(l) != "linear":
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
             elif k == "BatchNormalization":
                 C = nd.out.shape[-1]
@@ -455,7 +491,7 @@ class NativeGraphEngine(Engine):
                     nd.attrs["dw_pad"] = torch.zeros(kin, up, dtype=torch.float32, device=dev)
                     if l.use_bias:
                         nd.attrs["b_pad"] = torch.zeros(up, dtype=torch.float32, device=dev)
-                if getattr(l.activation, "__name__", "linear") == "relu":
+                if _act_name(l) != "linear":
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
         # one scratch bf16 buffer for "second writer" gradient accumulation
         big = max([int(np.prod(t.shape)) for t in self._all_tensors()] + [1])
@@ -572,8 +608,8 @@ class NativeGraphEngine(Engine):
         opt = self.model.optimizer
         c = self.ctrl.cpu()
         c[C_LR] = _f2i(opt.learning_rate)
-        c[C_MOM] = _f2i(opt.momentum)
-        c[C_NEST] = int(opt.nesterov)
+        c[C_MOM] = _f2i(getattr(opt, "momentum", 0.0))
+        c[C_NEST] = int(getattr(opt, "nesterov", False))
         c[C_ROW0] = self.rank * self.per_replica
         c[C_GB] = self.global_batch
         self.ctrl.copy_(c.to(self.device))
@@ -597,12 +633,13 @@ class NativeGraphEngine(Engine):
         # optimizer slots are dense over the unpadded weights (Keras order)
         opt = self.model.optimizer
         tot = int(sum(self.sizes))
-        if opt.momentum and "momentum" in opt.slots and opt.slots["momentum"].numel() == tot:
-            src = opt.slots["momentum"].to(self.device)
-            o = 0
-            for sz, off in zip(self.sizes, self.offsets):
-                self.V[off:off + sz].copy_(src[o:o + sz])
-                o += sz
+        for nm, buf in self.S.items():
+            if nm in opt.slots and opt.slots[nm].numel() == tot:
+                src = opt.slots[nm].to(self.device)
+                o = 0
+                for sz, off in zip(self.sizes, self.offsets):
+                    buf[off:off + sz].copy_(src[o:o + sz])
+                    o += sz
 
     def reload_optimizer_state(self):
         opt = self.model.optimizer
@@ -639,7 +676,8 @@ class NativeGraphEngine(Engine):
         torch.index_select(self.feed.y, 0, perm, out=self.y_ep)
         opt = self.model.optimizer
         self._ctrl_write({C_CUR: 0, C_AL: 0, C_AC: 0, C_AN: 0, C_WRAP: int(wrap_steps),
-                          C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
+                          C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(getattr(opt, "momentum", 0.0)),
+                          C_NEST: int(getattr(opt, "nesterov", False))})
 
     # --- the step ----------------------------------------------------------------------------
     def _mark(self, name):
@@ -679,8 +717,16 @@ class NativeGraphEngine(Engine):
         self._mark("optimizer")
 
     def _optimizer_step(self):
-        self.C.sgd_step(self.P.data_ptr(), self.G.data_ptr(), self.V.data_ptr(), self.Pb.data_ptr(), self.nparam,
-                        self.ctrl.data_ptr(), self.G[self.nparam:].data_ptr(), H.stream_handle())
+        opt = self.model.optimizer
+        ptr = [self.S[nm].data_ptr() if nm else self._slot_dummy.data_ptr() for nm in self.slot_kernel_names]
+        if self.opt_kind == 1:
+            args = (float(opt.beta_1), float(opt.beta_2), float(opt.epsilon), 0.0, 0.0, int(opt.amsgrad))
+        elif self.opt_kind == 2:
+            args = (0.0, 0.0, float(opt.epsilon), float(opt.rho), float(opt.momentum), int(opt.centered))
+        else:
+            args = (0.0, 0.0, 0.0, 0.0, float(opt.momentum), int(opt.nesterov))
+        self.C.opt_step(self.P.data_ptr(), self.G.data_ptr(), ptr[0], ptr[1], ptr[2], self.Pb.data_ptr(), self.nparam,
+                        self.ctrl.data_ptr(), self.G[self.nparam:].data_ptr(), self.opt_kind, *args, H.stream_handle())
 
     # forward ops
     def _w(self, nd, var):
@@ -698,13 +744,22 @@ class NativeGraphEngine(Engine):
             wp[:, :kw, :cin].copy_(self.views[id(l.kernel)])  # zeros elsewhere stay zero
             H.conv_fwd_stem4(x, wp, nd.out.root().buf, kh, l.strides, l.padding, bias=bias, relu=relu,
                              stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
-            return
-        if "w_pad" in nd.attrs:
-            kh, kw, cin, cout = l.kernel.shape
-            H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
-            wb = nd.attrs["w_pad"]
-        H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
-                   stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
+        else:
+            if "w_pad" in nd.attrs:
+                kh, kw, cin, cout = l.kernel.shape
+                H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
+                wb = nd.attrs["w_pad"]
+            H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
+                       stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
+        self._act_epilogue(nd)
+
+    def _act_epilogue(self, nd):
+        """sigmoid / tanh of a Conv2D / Dense: in place over the GEMM's bf16 output (ReLU
+        rides in the GEMM epilogue itself)."""
+        an = _act_name(nd.layer)
+        if an in ("sigmoid", "tanh"):
+            y = nd.out.root().buf
+            H.act_fwd(y, y, an)
 
     def _fwd_BatchNormalization(self, nd):
         l = nd.layer
@@ -731,7 +786,18 @@ class NativeGraphEngine(Engine):
     def _fwd_Activation(self, nd):
         C = nd.out.shape[-1]
         x = nd.inputs[0].root()
-        H.bn_apply(x.buf, self._ident(C), nd.out.root().buf, relu=True)
+        an = _act_name(nd.layer) if nd.kind == "Activation" else "relu"
+        if an == "relu" and C % 8 == 0:
+            H.bn_apply(x.buf, self._ident(C), nd.out.root().buf, relu=True)
+        else:
+            H.act_fwd(x.buf, nd.out.root().buf, an)
+
+    def _fwd_Dropout(self, nd):
+        H.dropout(nd.inputs[0].root().buf, nd.out.root().buf, self.ctrl, nd.attrs["seed"], nd.layer.rate)
+
+    def _fwd_AveragePooling2D(self, nd):
+        l = nd.layer
+        H.avgpool_fwd(nd.inputs[0].root().buf, nd.out.root().buf, l.pool_size, l.strides, l.padding)
 
     _fwd_ReLU = _fwd_Activation
 
@@ -777,6 +843,8 @@ class NativeGraphEngine(Engine):
         relu = getattr(l.activation, "__name__", "linear") == "relu"
         out = self.logits if nd.attrs.get("logits") else nd.out.root().buf
         H.dense_fwd(x2, wb, out, bias=bias, relu=relu, workspace=self.gemm_ws)
+        if not nd.attrs.get("logits"):
+            self._act_epilogue(nd)
 
     # backward ops
     def _dy(self, nd):
@@ -790,7 +858,7 @@ class NativeGraphEngine(Engine):
         y = nd.out.root()
         dy = y.grad
         if "dz" in nd.attrs:
-            H.relu_bwd(dy, y.buf, nd.attrs["dz"])
+            self._act_bwd(nd, dy, y.buf, nd.attrs["dz"])
             dy = nd.attrs["dz"]
         ws_s = self._wgrad_stream
         if ws_s is not None:
@@ -856,12 +924,37 @@ class NativeGraphEngine(Engine):
         self._bn_backward(nd, y.grad, y.buf, bool(nd.attrs.get("relu")),
                           mask_from_x=env.get_bool("DAMD_BN_MASK_FROM_X", True))
 
+    def _act_bwd(self, nd, dy, y, dx):
+        an = _act_name(nd.layer) if nd.kind != "ReLU" else "relu"
+        if an == "relu" and dy.numel() % 8 == 0:
+            H.relu_bwd(dy, y, dx)
+        else:
+            H.act_bwd(dy, y, dx, an)
+
     def _bwd_Activation(self, nd):
         x = nd.inputs[0].root()
         y = nd.out.root()
         dx, fin = self._grad_target(x)
         if dx is not None:
-            H.relu_bwd(y.grad, y.buf, dx)
+            self._act_bwd(nd, y.grad, y.buf, dx)
+            if fin:
+                fin()
+
+    def _bwd_Dropout(self, nd):
+        x = nd.inputs[0].root()
+        dx, fin = self._grad_target(x)
+        if dx is not None:
+            # the same counter-hash mask and scale as the forward (same seed, same step t)
+            H.dropout(nd.out.root().grad, dx, self.ctrl, nd.attrs["seed"], nd.layer.rate)
+            if fin:
+                fin()
+
+    def _bwd_AveragePooling2D(self, nd):
+        l = nd.layer
+        x = nd.inputs[0].root()
+        dx, fin = self._grad_target(x)
+        if dx is not None:
+            H.avgpool_bwd(nd.out.root().grad, dx, l.pool_size, l.strides, l.padding)
             if fin:
                 fin()
 
@@ -938,7 +1031,7 @@ class NativeGraphEngine(Engine):
         dy = self._dy(nd)
         if "dz" in nd.attrs:
             y = nd.out.root()
-            H.relu_bwd(dy, y.buf, nd.attrs["dz"])
+            self._act_bwd(nd, dy, y.buf, nd.attrs["dz"])
             dy = nd.attrs["dz"]
         units = l.units
         if l.use_bias:
@@ -962,15 +1055,6 @@ class NativeGraphEngine(Engine):
             H.dense_dgrad(dy, wb, xt.grad.view(xt.grad.shape[0], -1), accumulate=acc, workspace=self.gemm_ws)
 
     # --- driver ---------------------------------------------------------------------------------
-    def _capture(self):
-        torch.cuda.synchronize(self.device)
-        # warm-up on a side stream (torch's recommended capture prologue); the warm-up
-        # trains one real step, which the caller accounts for
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._step_body()
-        self.graph = g
-
     def run(self, n_steps):
         if self.host_collective:
             for _ in range(n_steps):
@@ -1025,9 +1109,19 @@ class NativeGraphEngine(Engine):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(s):
-            with torch.cuda.graph(g, stream=s):
-                self._step_body()
+        # no garbage collection inside the capture: a finalizer that synchronises or frees
+        # device resources (an old engine's communicator, graph, events) is illegal while a
+        # stream captures and aborts the process (seen on the GPU tier)
+        gc.collect()
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            with torch.cuda.stream(s):
+                with torch.cuda.graph(g, stream=s):
+                    self._step_body()
+        finally:
+            if was:
+                gc.enable()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.graph = g
@@ -1048,13 +1142,14 @@ class NativeGraphEngine(Engine):
     def finish(self):
         torch.cuda.synchronize(self.device)
         opt = self.model.optimizer
-        if opt.momentum:
+        if self.S:
             tot = int(sum(self.sizes))
             opt.ensure_slots(tot, self.device)
-            o = 0
-            for sz, off in zip(self.sizes, self.offsets):
-                opt.slots["momentum"][o:o + sz].copy_(self.V[off:off + sz])
-                o += sz
+            for nm, buf in self.S.items():
+                o = 0
+                for sz, off in zip(self.sizes, self.offsets):
+                    opt.slots[nm][o:o + sz].copy_(buf[off:off + sz])
+                    o += sz
 
     def sync(self):
         torch.cuda.synchronize(self.device)

@@ -410,6 +410,7 @@ class Dropout(Layer):
     def __init__(self, rate, noise_shape=None, seed=None, **kw):
         super().__init__(**kw)
         self.rate = float(rate)
+        self.seed = seed
 
     def call(self, x, training=False):
         if not training or self.rate == 0.0:
@@ -418,7 +419,7 @@ class Dropout(Layer):
 
     def get_config(self):
         c = super().get_config()
-        c.update(rate=self.rate, noise_shape=None, seed=None)
+        c.update(rate=self.rate, noise_shape=None, seed=self.seed)
         return c
 
 

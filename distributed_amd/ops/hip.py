@@ -17,6 +17,7 @@ import math
 import os
 from typing import Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 
 from ..native import require_C
@@ -635,6 +636,55 @@ def gap_bwd(dy, dx):
 
 def relu_bwd(dy, y, dz):
     _C().relu_bwd(_ptr(dy), _ptr(y), _ptr(dz), dy.numel(), stream_handle())
+
+
+ACT_KINDS = {"relu": 0, "sigmoid": 1, "tanh": 2}
+
+
+def act_fwd(x, y, kind: str):
+    """y = act(x) on bf16 tensors (in place allowed); kind relu / sigmoid / tanh."""
+    _C().act_fwd(_ptr(x), _ptr(y), x.numel(), ACT_KINDS[kind], stream_handle())
+
+
+def act_bwd(dy, y, dx, kind: str):
+    """dx = dy * act'(y) from the stored activation output y."""
+    _C().act_bwd(_ptr(dy), _ptr(y), _ptr(dx), dy.numel(), ACT_KINDS[kind], stream_handle())
+
+
+def dropout(x, y, ctrl, seed: int, rate: float):
+    """y = x * keep / (1 - rate); keep from (seed, ctrl step t, element) -- the same call on
+    dy is the backward (see dropout_mask_reference)."""
+    _C().dropout(_ptr(x), _ptr(y), x.numel(), _ptr(ctrl), int(seed) & 0xFFFFFFFF, float(rate), stream_handle())
+
+
+def _mix32(h):
+    h = h.astype(np.uint32)
+    h ^= h >> np.uint32(16)
+    h *= np.uint32(0x85EBCA6B)
+    h ^= h >> np.uint32(13)
+    h *= np.uint32(0xC2B2AE35)
+    h ^= h >> np.uint32(16)
+    return h
+
+
+def dropout_mask_reference(n: int, seed: int, t: int, rate: float) -> np.ndarray:
+    """Host oracle of the dropout kernel's keep mask (bool [n]) at step t."""
+    with np.errstate(over="ignore"):
+        key = _mix32(np.array([(int(seed) + int(t) * 0x9E3779B9) & 0xFFFFFFFF], dtype=np.uint64))[0]
+        j = np.arange(n, dtype=np.uint64).astype(np.uint32)
+        h = _mix32((_mix32(j ^ key).astype(np.uint64) + int(key)) & 0xFFFFFFFF)
+    thr = min(int(rate * 4294967296.0), 4294967295)
+    return h >= np.uint32(thr)
+
+
+def avgpool_fwd(x, y, pool, strides, padding):
+    g = pool_geo(x.shape, pool, strides, padding)
+    _C().avgpool_fwd(_ptr(x), g, _ptr(y), stream_handle())
+
+
+def avgpool_bwd(dy, dx, pool, strides, padding):
+    g = pool_geo(dx.shape, pool, strides, padding)
+    _C().avgpool_bwd(_ptr(dy), g, _ptr(dx), stream_handle())
 
 
 def add_bf16(a, b, out):

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Full GPU check of the tree as the driver runs it: GPU tests, smoke(), the headline
-# bench with the driver's flags and with defaults, the ResNet-18 bench, and a rocprofv3
-# kernel-stats pass over the headline bench.  Every GPU step has its own time limit and
-# the script stops at the first failure.
+# bench with the driver's flags and with defaults, the ResNet-18 bench, phase splits of
+# both steps, and a rocprofv3 kernel-stats pass over the headline bench.  Every GPU step
+# has its own time limit and the script stops at the first failure.
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -18,8 +18,8 @@ tail -3 gpurun_out/pytest_gpu.log
 step smoke 300 python -u __graft_entry__.py smoke
 step bench_driver 300 python -u bench.py --gpus 1 --steps 20 --warmup 5
 tail -1 gpurun_out/bench_driver.log
-step bench_default 300 python -u bench.py
+step bench_default 300 python -u bench.py --phases 50
 tail -1 gpurun_out/bench_default.log
-step bench_resnet 300 python -u bench.py --model resnet18 --steps 20 --warmup 5
+step bench_resnet 300 python -u bench.py --model resnet18 --steps 20 --warmup 5 --phases 5
 tail -1 gpurun_out/bench_resnet.log
 step prof_mnist 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mnist -o bench -- python3 bench.py --gpus 1 --steps 500 --warmup 50

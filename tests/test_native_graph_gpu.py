@@ -31,7 +31,7 @@ def _mnist():
 
 
 def _train(build, x, y, init, batch, steps, native, lr=0.1, momentum=0.0, graph=True, device=None, extra_env=None,
-           fused=False):
+           fused=False, optimizer=None):
     env = {"DAMD_NATIVE_GRAPH": "1" if native else "0", "DAMD_FUSED": "1" if fused else "0",
            "DAMD_GRAPH": "1" if graph else "0"}
     env.update(extra_env or {})
@@ -46,10 +46,13 @@ def _train(build, x, y, init, batch, steps, native, lr=0.1, momentum=0.0, graph=
         tf.keras.backend.clear_session()
         m = build()
         m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
-                  optimizer=tf.keras.optimizers.SGD(learning_rate=lr, momentum=momentum), metrics=["accuracy"])
+                  optimizer=optimizer() if optimizer else tf.keras.optimizers.SGD(learning_rate=lr, momentum=momentum),
+                  metrics=["accuracy"])
         m.set_weights(init)
         h = m.fit(x, y, batch_size=batch, epochs=1, steps_per_epoch=steps, shuffle=False, verbose=0)
         eng = m._engine.name
+        if optimizer:
+            return m.get_weights(), h.history, eng, m.optimizer
         return m.get_weights(), h.history, eng
     finally:
         for k, v in old.items():

@@ -67,3 +67,52 @@ def test_gradient_buckets_tile_the_flat_buffer():
     # every trainable variable has exactly one writer node in the backward plan
     written = [i for vs in pl._writes.values() for i in vs]
     assert sorted(written) == sorted(id(v) for v in pl.vars)
+
+
+class _FakeGPUStrategy:
+    import torch as _t
+
+    device = _t.device("cuda")
+
+
+def _compiled(model, opt):
+    model.compile(loss=keras.losses.SparseCategoricalCrossentropy(from_logits=True), optimizer=opt,
+                  metrics=["accuracy"])
+    return model
+
+
+def test_round3_layers_and_optimizers_are_native_eligible():
+    """Dropout, AveragePooling2D, sigmoid / tanh and Adam / RMSprop lower to the native
+    engine (VERDICT r2 #6); what still falls back says why."""
+    L = keras.layers
+    keras.backend.clear_session()
+
+    def net(units=40, act="tanh"):
+        return keras.Sequential([
+            L.Conv2D(16, 3, activation=act, input_shape=(16, 16, 3)),
+            L.AveragePooling2D(pool_size=3, strides=2, padding="same"),
+            L.Dropout(0.25),
+            L.Conv2D(16, 3, activation="sigmoid"),
+            L.Activation("tanh"),
+            L.Flatten(),
+            L.Dense(units, activation="sigmoid"),
+            L.Dropout(0.0),
+            L.Dense(10),
+        ])
+
+    for opt in (keras.optimizers.Adam(), keras.optimizers.RMSprop(momentum=0.9, centered=True),
+                keras.optimizers.SGD(0.1, momentum=0.9)):
+        ok, why = NativeGraphEngine.eligible(_compiled(net(), opt), _FakeGPUStrategy())
+        assert ok, why
+    ok, why = NativeGraphEngine.eligible(_compiled(net(units=36), "adam"), _FakeGPUStrategy())
+    assert not ok and "multiple of 8" in why
+    ok, why = NativeGraphEngine.eligible(_compiled(net(act="softplus"), "adam"), _FakeGPUStrategy())
+    assert not ok and "softplus" in why
+    pl = NativeGraphEngine.plan_only(net(), 8)
+    kinds = {nd.layer.name: (nd.kind, nd.attrs.get("dead")) for nd in pl.nodes}
+    drops = [nd for nd in pl.nodes if nd.kind == "Dropout"]
+    assert [d.attrs["dead"] for d in drops] == [False, True]  # rate 0 is planned away
+    assert drops[0].attrs["seed"] != 0
+    assert ("Activation", False) in kinds.values()  # tanh is a real node (not an identity)
+    pools = [nd for nd in pl.nodes if nd.kind == "AveragePooling2D"]
+    assert pools[0].out.shape == (8, 7, 7, 16)
