@@ -65,6 +65,12 @@ hipError_t avgpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, in
                        int pad_l, int Ho, int Wo, uint16_t* y, hipStream_t s);
 hipError_t avgpool_bwd(const uint16_t* dy, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
                        int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s);
+// Inference: BN st rows from the moving statistics; this step's logits rows -> out at the
+// device cursor; fold the metric tail into ctrl (tail cleared) and advance the cursor
+hipError_t bn_infer_st(const float* rmean, const float* rvar, const float* gamma, const float* beta, float eps, int C,
+                       float* st, hipStream_t s);
+hipError_t logits_store(const float* logits, int ld, int K, int B, const Ctrl* ctrl, float* out, hipStream_t s);
+hipError_t step_fold(Ctrl* ctrl, float* tail, hipStream_t s);
 // out = a + b (bf16)
 hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n, hipStream_t s);
 // fp32 -> bf16

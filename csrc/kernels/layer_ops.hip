@@ -1116,6 +1116,50 @@ __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ l
   }
 }
 
+// ---- inference (predict / evaluate through the native forward plan) ----------------------
+// BatchNorm with the moving statistics: the same st rows bn_finalize writes from batch
+// statistics (mean, 1/sqrt(var + eps), scale, shift), so every BN apply / fused residual /
+// stem-pool kernel runs unchanged in inference mode.
+__global__ __launch_bounds__(NT) void bn_infer_st_k(const float* __restrict__ rmean, const float* __restrict__ rvar,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    float eps, int C, float* __restrict__ st) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  const float m = rmean[c], inv = rsqrtf(rvar[c] + eps);
+  const float sc = (gamma ? gamma[c] : 1.f) * inv;
+  st[c] = m;
+  st[C + c] = inv;
+  st[2 * C + c] = sc;
+  st[3 * C + c] = (beta ? beta[c] : 0.f) - m * sc;
+}
+
+// logits rows of this step -> out[global row][K] (rows past the end of the data dropped);
+// the row base comes from the device cursor, so a captured graph replays across batches
+__global__ __launch_bounds__(NT) void logits_store_k(const float* __restrict__ logits, int ld, int K, int B,
+                                                     const Ctrl* __restrict__ ctrl, float* __restrict__ out) {
+  const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
+  const long n = ctrl->nsamples;
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < (long)B * K; i += (long)gridDim.x * NT) {
+    const int r = (int)(i / K), k = (int)(i % K);
+    if (base + r < n) out[(base + r) * K + k] = logits[(long)r * ld + k];
+  }
+}
+
+// end of an inference step: fold the metric tail into the epoch accumulators (and clear
+// it for the next step), advance the cursor
+__global__ void step_fold_k(Ctrl* ctrl, float* tail) {
+  if (threadIdx.x != 0) return;
+  if (tail) {
+    ctrl->acc_loss += tail[0];
+    ctrl->acc_correct += tail[1];
+    ctrl->acc_count += tail[2];
+    tail[0] = tail[1] = tail[2] = 0.f;
+  }
+  int c = ctrl->cursor + 1;
+  if (ctrl->wrap > 0 && c >= ctrl->wrap) c = 0;
+  ctrl->cursor = c;
+}
+
 // ---- optimizer ------------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void sgd_flat_k(float* __restrict__ P, const float* __restrict__ G,
                                                  float* __restrict__ V, uint16_t* __restrict__ Pb, long n, float lr,
@@ -1332,6 +1376,23 @@ hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, u
                     const float* tail, const OptArgs& o, hipStream_t s) {
   if (o.kind < 0 || o.kind > 2) return hipErrorInvalidValue;
   hipLaunchKernelGGL(opt_step_k, dim3(grid_for(n, NT, 4096)), dim3(NT), 0, s, P, G, S0, S1, S2, Pb, n, ctrl, tail, o);
+  return hipGetLastError();
+}
+
+hipError_t bn_infer_st(const float* rmean, const float* rvar, const float* gamma, const float* beta, float eps, int C,
+                       float* st, hipStream_t s) {
+  hipLaunchKernelGGL(bn_infer_st_k, dim3((C + NT - 1) / NT), dim3(NT), 0, s, rmean, rvar, gamma, beta, eps, C, st);
+  return hipGetLastError();
+}
+
+hipError_t logits_store(const float* logits, int ld, int K, int B, const Ctrl* ctrl, float* out, hipStream_t s) {
+  if (K > ld) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(logits_store_k, dim3(grid_for((long)B * K)), dim3(NT), 0, s, logits, ld, K, B, ctrl, out);
+  return hipGetLastError();
+}
+
+hipError_t step_fold(Ctrl* ctrl, float* tail, hipStream_t s) {
+  hipLaunchKernelGGL(step_fold_k, dim3(1), dim3(64), 0, s, ctrl, tail);
   return hipGetLastError();
 }
 

@@ -165,6 +165,19 @@ void register_kernel_ops(py::module_& m) {
                             g[11], P_<u16>(dx), P_<ihipStream_t>(s)),
           "avgpool_bwd");
   });
+  m.def("bn_infer_st", [](U rmean, U rvar, U gamma, U beta, float eps, int C, U st, U s) {
+    check(damd::bn_infer_st(P_<const float>(rmean), P_<const float>(rvar), P_<const float>(gamma),
+                            P_<const float>(beta), eps, C, P_<float>(st), P_<ihipStream_t>(s)),
+          "bn_infer_st");
+  });
+  m.def("logits_store", [](U logits, int ld, int K, int B, U ctrl, U out, U s) {
+    check(damd::logits_store(P_<const float>(logits), ld, K, B, P_<const damd::Ctrl>(ctrl), P_<float>(out),
+                             P_<ihipStream_t>(s)),
+          "logits_store");
+  });
+  m.def("step_fold", [](U ctrl, U tail, U s) {
+    check(damd::step_fold(P_<damd::Ctrl>(ctrl), P_<float>(tail), P_<ihipStream_t>(s)), "step_fold");
+  });
   m.def("add_bf16", [](U a, U b, U o, long n, U s) {
     check(damd::add_bf16(P_<const u16>(a), P_<const u16>(b), P_<u16>(o), n, P_<ihipStream_t>(s)), "add_bf16");
   });

@@ -127,6 +127,7 @@ class NativeGraphEngine(Engine):
     SUPPORTED = ("Conv2D", "BatchNormalization", "Activation", "ReLU", "Add", "MaxPooling2D",
                  "AveragePooling2D", "GlobalAveragePooling2D", "Flatten", "Dense", "Dropout")
     ACTIVATIONS = ("linear", "relu", "sigmoid", "tanh")
+    _weights_static = False  # True for an inference plan: padded weight copies made once per call
 
     @staticmethod
     def eligible(model, strategy):
@@ -141,6 +142,12 @@ class NativeGraphEngine(Engine):
         for m in model.compiled_metrics:
             if m.name not in ("accuracy", "acc", "sparse_categorical_accuracy"):
                 return False, f"metric {m.name}"
+        return NativeGraphEngine.layers_eligible(model)
+
+    @staticmethod
+    def layers_eligible(model):
+        """(ok, reason): every layer of ``model`` has a native forward + backward kernel
+        and the model ends in a linear Dense (the logits)."""
         try:
             seq, _, out_key, in_shape = _layer_graph(model)
         except Exception as e:  # pragma: no cover
@@ -738,20 +745,37 @@ class NativeGraphEngine(Engine):
         wb = self._w(nd, l.kernel)
         bias = self.views[id(l.bias)] if l.use_bias else None
         relu = getattr(l.activation, "__name__", "linear") == "relu"
+        if not self._weights_static:
+            self._pad_weights(nd)
         if nd.attrs.get("stem4"):
-            kh, kw, cin, cout = l.kernel.shape
+            kh = l.kernel.shape[0]
             wp = nd.attrs["w_pad"]
-            wp[:, :kw, :cin].copy_(self.views[id(l.kernel)])  # zeros elsewhere stay zero
             H.conv_fwd_stem4(x, wp, nd.out.root().buf, kh, l.strides, l.padding, bias=bias, relu=relu,
                              stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
         else:
             if "w_pad" in nd.attrs:
-                kh, kw, cin, cout = l.kernel.shape
-                H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
                 wb = nd.attrs["w_pad"]
             H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
                        stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
         self._act_epilogue(nd)
+
+    def _pad_weights(self, nd):
+        """Refresh a layer's padded bf16 weight copy from the fp32 masters (every training
+        step; once per call for an inference plan, whose weights do not move)."""
+        l = nd.layer
+        if "w_pad" not in nd.attrs:
+            return
+        if nd.kind == "Conv2D":
+            kh, kw, cin, cout = l.kernel.shape
+            if nd.attrs.get("stem4"):
+                nd.attrs["w_pad"][:, :kw, :cin].copy_(self.views[id(l.kernel)])  # zeros elsewhere stay zero
+            else:
+                H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
+        elif nd.kind == "Dense":
+            kin, units = l.kernel.shape
+            H.pad_cast(self.views[id(l.kernel)], 1, kin, units, kin, nd.attrs["w_pad"].shape[1], nd.attrs["w_pad"])
+            if l.use_bias:
+                nd.attrs["b_pad"][:units].copy_(self.views[id(l.bias)])
 
     def _act_epilogue(self, nd):
         """sigmoid / tanh of a Conv2D / Dense: in place over the GEMM's bf16 output (ReLU
@@ -833,12 +857,11 @@ class NativeGraphEngine(Engine):
         x2 = x.view(x.shape[0], -1)
         wb = self._w(nd, l.kernel)
         bias = self.views[id(l.bias)] if l.use_bias else None
+        if not self._weights_static:
+            self._pad_weights(nd)
         if "w_pad" in nd.attrs:
-            kin, units = l.kernel.shape
-            H.pad_cast(self.views[id(l.kernel)], 1, kin, units, kin, nd.attrs["w_pad"].shape[1], nd.attrs["w_pad"])
             wb = nd.attrs["w_pad"]
             if bias is not None:
-                nd.attrs["b_pad"][:units].copy_(bias)
                 bias = nd.attrs["b_pad"]
         relu = getattr(l.activation, "__name__", "linear") == "relu"
         out = self.logits if nd.attrs.get("logits") else nd.out.root().buf

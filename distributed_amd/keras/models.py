@@ -325,11 +325,30 @@ class Model(L.Layer):
         return {k: float(v) for k, v in d.items() if not k.startswith("_")}
 
     # --- evaluate / predict ------------------------------------------------------------
+    def _native_infer(self, batch, evaluate=False):
+        """The native forward plan for predict / evaluate on a GPU (engine/native_infer.py),
+        or None (CPU, DAMD_NATIVE_INFER=0, or a layer / loss / metric it does not cover --
+        logged as a warning, an error under DAMD_STRICT_NATIVE=1)."""
+        dev = self._strategy.device
+        if dev.type != "cuda" or not env.get_bool("DAMD_NATIVE_INFER", True):
+            return None
+        from ..engine import native_infer
+
+        plan = native_infer.plan_for(self, batch, dev, evaluate=evaluate)
+        if plan is None and env.get_bool("DAMD_STRICT_NATIVE", False):
+            raise RuntimeError("DAMD_STRICT_NATIVE=1: this model has no native inference plan")
+        return plan
+
     @torch.no_grad()
     def predict(self, x, batch_size=None, verbose=0, steps=None):
         self._sync_engine()
-        x = np.asarray(x, dtype=np.float32)
         bs = int(batch_size or 32)
+        if steps is not None:
+            x = x[: int(steps) * bs]
+        plan = self._native_infer(bs)
+        if plan is not None:
+            return plan.predict(x)
+        x = np.asarray(x, dtype=np.float32)
         dev = self._strategy.device
         outs = []
         for i in range(0, len(x), bs):
@@ -343,7 +362,9 @@ class Model(L.Layer):
         evaluates a disjoint shard and the sums are all-reduced."""
         self._sync_engine()
         st = self._strategy
-        x = np.asarray(x, dtype=np.float32)
+        x = np.asarray(x)
+        if x.dtype != np.uint8:
+            x = x.astype(np.float32, copy=False)
         y = np.asarray(y)
         world, rank = st.num_replicas_in_sync, st.rank
         bs = int(batch_size or 32)
@@ -351,9 +372,16 @@ class Model(L.Layer):
         dev = st.device
         sums = torch.zeros(2 + len(self.compiled_metrics), dtype=torch.float64)
         lo, hi = (n * rank) // world, (n * (rank + 1)) // world
-        for i in range(lo, hi, bs):
+        plan = self._native_infer(bs, evaluate=True)
+        if plan is not None:
+            # one upload, a graph replay per batch, one host sync for the whole shard
+            loss_sum, cnt_, correct = plan.evaluate_sums(x[lo:hi], y[lo:hi])
+            sums[0], sums[1] = loss_sum, cnt_
+            for k in range(len(self.compiled_metrics)):
+                sums[2 + k] = correct
+        for i in (range(lo, hi, bs) if plan is None else ()):
             j = min(i + bs, hi)
-            xb = torch.from_numpy(np.ascontiguousarray(x[i:j])).to(dev)
+            xb = torch.from_numpy(np.ascontiguousarray(x[i:j])).to(dev).float()
             yb = torch.from_numpy(np.ascontiguousarray(y[i:j])).to(dev)
             out = self(xb, training=False)
             sums[0] += float(self.loss.per_sample(yb, out).double().sum())
