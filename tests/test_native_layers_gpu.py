@@ -127,21 +127,26 @@ def test_opt_step_kernel_matches_apply_flat(name):
     assert torch.equal(Pb, P.bfloat16())
 
 
-def _opt_cases():
+def _opt_cases(eps=1e-7):
     O = tf.keras.optimizers
     return {
-        "adam": lambda: O.Adam(learning_rate=1e-3),
-        "adam_amsgrad": lambda: O.Adam(learning_rate=1e-3, amsgrad=True),
-        "rmsprop": lambda: O.RMSprop(learning_rate=1e-3),
-        "rmsprop_momentum": lambda: O.RMSprop(learning_rate=5e-4, momentum=0.9),
-        "rmsprop_centered_momentum": lambda: O.RMSprop(learning_rate=5e-4, momentum=0.9, centered=True),
+        "adam": lambda: O.Adam(learning_rate=1e-3, epsilon=eps),
+        "adam_amsgrad": lambda: O.Adam(learning_rate=1e-3, amsgrad=True, epsilon=eps),
+        "rmsprop": lambda: O.RMSprop(learning_rate=1e-3, epsilon=eps),
+        "rmsprop_momentum": lambda: O.RMSprop(learning_rate=5e-4, momentum=0.9, epsilon=eps),
+        "rmsprop_centered_momentum": lambda: O.RMSprop(learning_rate=5e-4, momentum=0.9, centered=True, epsilon=eps),
         "sgd_nesterov": lambda: O.SGD(learning_rate=0.05, momentum=0.9, nesterov=True),
     }
 
 
 @pytest.mark.parametrize("name", list(_opt_cases()))
 def test_native_optimizers_track_reference(name):
-    opt = _opt_cases()[name]
+    # This checks the engine's wiring (slots, step t, hyper-parameters, write-back); the
+    # update rules themselves are pinned at the default epsilon by the kernel oracle
+    # above.  epsilon 1e-2, not 1e-7: with a tiny epsilon Adam / RMSprop move every weight
+    # by ~lr * sign(g), so weights whose gradient is ~0 follow the sign of the bf16 vs fp32
+    # rounding noise (measured cos 0.885 at 1e-7, 0.926 at 1e-3 after 10 steps)
+    opt = _opt_cases(eps=1e-2)[name]
     x, y = _data(640, (28, 28, 1), 10, seed=3)
     tf.keras.backend.clear_session()
     torch.manual_seed(11)
@@ -152,19 +157,13 @@ def test_native_optimizers_track_reference(name):
     assert en == "native_graph" and er == "generic"
     assert on.iterations == orf.iterations == 10
     np.testing.assert_allclose(hn["loss"], hr["loss"], rtol=2e-2)
-    # The update rules themselves are pinned exactly by the kernel test above; here the
-    # native run's bf16 gradients meet the fp32 reference's.  Adam / RMSprop normalise the
-    # step per element (~lr * g / |g| early on), so near-zero gradients whose bf16 rounding
-    # differs move their weights by a full step: measured cos >= 0.948, rel <= 0.33.
-    cos_min, rel_max = (0.95, 0.3) if name.startswith("sgd") else (0.9, 0.5)
+    cos_min, rel_max = 0.93, 0.4
     _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=cos_min, rel_max=rel_max)
-    # the slots come back to the Keras optimizer in its dense (unpadded) layout; over the
-    # whole flat vector the many near-zero first-layer gradients dominate (measured cos
-    # 0.848 for the RMSprop momentum slot), so this checks the layout, not the arithmetic
+    # the slots come back to the Keras optimizer in its dense (unpadded) layout
     for s in orf.slot_names():
         a, b = on.slots[s].cpu().double(), orf.slots[s].cpu().double()
         assert a.shape == b.shape
-        assert float(a @ b / (a.norm() * b.norm() + 1e-30)) > 0.75, s
+        assert float(a @ b / (a.norm() * b.norm() + 1e-30)) > 0.9, s
 
 
 def _act_pool_model():
