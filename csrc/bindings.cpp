@@ -50,6 +50,7 @@ class ConvNetTrainer : public StepExecutor {
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
     b_.fuse_head = bufs.contains("fuse_head") ? (int)g("fuse_head") : 0;
     b_.kernels = bufs.contains("kernels") ? (int)g("kernels") : 2;
+    b_.eager_w1 = bufs.contains("eager_w1") ? (int)g("eager_w1") : 0;
     if (b_.kernels != 2 && b_.kernels != 3) throw std::invalid_argument("kernels must be 2 or 3");
     b_.hacc = bufs.contains("hacc") ? P_<long long>(g("hacc")) : nullptr;
     b_.hconv = bufs.contains("hconv") ? P_<long long>(g("hconv")) : nullptr;

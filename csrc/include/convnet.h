@@ -20,6 +20,11 @@ struct ConvNetBuffers {
   long long* hconv;  // [2][320] conv weight/bias gradient x 2^40, by step parity (both all-reduced)
   float* calt;       // [2][320] alternate conv parameters / velocity (double buffer by parity)
   int kernels;       // 2 (default) or 3 (convnet_fused.hip)
+  // 2-launch step, no gradient all-reduce (world 1): bwd applies the W1 update as soon as
+  // its block has the slice's gradient (fp32 master + velocity in place, bf16 copy); fwd
+  // then reads only the bf16 copy.  0: the update is deferred into the next fwd (after
+  // the all-reduce of G)
+  int eager_w1;
 };
 constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;

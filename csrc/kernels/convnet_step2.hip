@@ -55,13 +55,15 @@ constexpr int HEAD_BYTES = HEAD_FLOATS * 4;
 // fwd: grid (NS slices, IG image groups of IB = 2^lg images)
 // =================================================================================
 template <bool U8>
-__global__ __launch_bounds__(512) void fwd(const void* __restrict__ X, float* __restrict__ P,
-                                           const float* __restrict__ G, float* __restrict__ V,
-                                           float* __restrict__ W1alt, float* __restrict__ V1alt,
-                                           uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
+// (ctrl and X lead the argument list: with kernarg preloading they arrive in SGPRs, so
+// the first dependent loads -- the ctrl block, then the batch rows -- start at once)
+__global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* __restrict__ X,
+                                           float* __restrict__ P, const float* __restrict__ G,
+                                           float* __restrict__ V, float* __restrict__ W1alt,
+                                           float* __restrict__ V1alt, uint16_t* __restrict__ w1bf,
                                            uint16_t* __restrict__ pooled, uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv,
-                                           float* __restrict__ calt, int B, int PP, int lg,
+                                           float* __restrict__ calt, int B, int PP, int lg, int eager,
                                            unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -94,6 +96,7 @@ __global__ __launch_bounds__(512) void fwd(const void* __restrict__ X, float* __
   x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
   const int n4 = K * HID / 4;  // <= 2048
   float4 wv[4], gv[4], vv[4];
+  uint4 bq[2];  // eager: the bf16 W1 slice (bwd already applied the update)
   const float* Wcur = c.wpar ? W1alt : P + OFF_W1;
   const float* Vcur = c.wpar ? V1alt : V + OFF_W1;
   float* Wnext = c.wpar ? P + OFF_W1 : W1alt;
@@ -105,12 +108,18 @@ __global__ __launch_bounds__(512) void fwd(const void* __restrict__ X, float* __
   float4* Wn4 = reinterpret_cast<float4*>(Wnext + p0 * 32 * HID);
   float4* Vn4 = reinterpret_cast<float4*>(Vnext + p0 * 32 * HID);
   uint2* Wb = reinterpret_cast<uint2*>(w1bf + p0 * 32 * HID);
+  if (eager) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int ic = min(tid + u * 512, n4 - 1);
-    wv[u] = P4[ic];
-    gv[u] = G4[ic];
-    vv[u] = V4[ic];
+    for (int u = 0; u < 2; ++u)
+      bq[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n4 / 2 - 1)];
+  } else {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int ic = min(tid + u * 512, n4 - 1);
+      wv[u] = P4[ic];
+      gv[u] = G4[ic];
+      vv[u] = V4[ic];
+    }
   }
   // conv parameters: current buffer by parity; their gradient is the previous step's
   // (bwd added it into hconv[par ^ 1])
@@ -127,10 +136,25 @@ __global__ __launch_bounds__(512) void fwd(const void* __restrict__ X, float* __
   lds_barrier();  // the table is read by x_store (the loads above stay in flight)
 
   // ---- pending SGD updates ----
+  if (eager) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + u * 512;  // 8 consecutive n of row kr
+      if (i < n4 / 2) {
+        const int e = i * 8, kr = e >> 6, n = e & 63;
+        const uint32_t w[4] = {bq[u].x, bq[u].y, bq[u].z, bq[u].w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          w1t[(n + 2 * q) * KP + kr] = (uint16_t)(w[q] & 0xffffu);
+          w1t[(n + 2 * q + 1) * KP + kr] = (uint16_t)(w[q] >> 16);
+        }
+      }
+    }
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = tid + u * 512;
-    if (i < n4) {
+    if (!eager && i < n4) {
       float4 wn, vn;
       sgd_or_keep(pend, wv[u].x, gv[u].x, vv[u].x, c, wn.x, vn.x);
       sgd_or_keep(pend, wv[u].y, gv[u].y, vv[u].y, c, wn.y, vn.y);
@@ -235,12 +259,13 @@ __global__ __launch_bounds__(512) void fwd(const void* __restrict__ X, float* __
 // aux element e (parameter order at G + OFF_B1): [0,64) db1, [64,704) dW2
 // (k = (e-64)/10, c = (e-64)%10), [704,714) db2, then 714 loss, 715 correct, 716 count.
 template <bool U8, bool ONE>  // ONE: B <= 64, a single chunk (no loop-carried prefetch registers)
-__global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int* __restrict__ labels,
-                                           const float* __restrict__ P, float* __restrict__ G,
-                                           const uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
+__global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* __restrict__ X,
+                                           const int* __restrict__ labels, const float* P,
+                                           float* __restrict__ G, const uint16_t* w1bf,
                                            const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
-                                           int PP, unsigned long long* st) {
+                                           int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
+                                           unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Stamps sts;
   stamp(sts, st, 0);
@@ -363,6 +388,8 @@ __global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int
   lds_barrier();  // lut visible to x_store
 
   const int dn = wave & 3, dm0 = wave >> 2;
+  const bool mom = c.momentum != 0.f;
+  float ew[ONE ? MAXPP : 1][4], ev[ONE ? MAXPP : 1][4];  // eager (single chunk only)
   f32x4 accw[MAXPP];
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) accw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -380,6 +407,21 @@ __global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int
     store_chunk(chunk);
     lds_barrier();
     stamp(sts, st, 1);
+    // eager: the slice's fp32 masters / velocities for the update right after the dW1
+    // MFMAs, issued once the staged operands have landed (in flight through the head)
+    if (ONE && eager) {
+#pragma unroll
+      for (int i = 0; i < MAXPP; ++i) {
+        if (i >= np) break;
+        const int mt = dm0 + 2 * i;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long e = OFF_W1 + (long)(p0 * 32 + 16 * mt + 4 * (lane >> 4) + j) * HID + 16 * dn + lr16;
+          ew[i][j] = Pw[e];
+          ev[i][j] = mom ? Vw[e] : 0.f;
+        }
+      }
+    }
     // ---- head (every block, redundantly): h = relu(hacc / 2^32 + b1) ----
     {
       const int r = tid >> 3, q = tid & 7;
@@ -510,6 +552,25 @@ __global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int
         accw[i] = mfma16(a, bl, accw[i]);
       }
     }
+    // eager: the slice's SGD update now, its stores overlapping dP and the conv gradient
+    // (fp32 master and velocity in place, bf16 copy for the next fwd; this block read its
+    // old bf16 slice in the prologue and nobody else touches the slice in this launch)
+    if (ONE && eager) {
+#pragma unroll
+      for (int i = 0; i < MAXPP; ++i) {
+        if (i >= np) break;
+        const int mt = dm0 + 2 * i;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long e = OFF_W1 + (long)(p0 * 32 + 16 * mt + 4 * (lane >> 4) + j) * HID + 16 * dn + lr16;
+          float wn, vn;
+          sgd_update(ew[i][j], accw[i][j], ev[i][j], c.lr, c.momentum, c.nesterov, wn, vn);
+          Pw[e] = wn;
+          if (mom) Vw[e] = vn;
+          w1bf_out[e - OFF_W1] = f2bf(wn);
+        }
+      }
+    }
     // dP[b][k] = sum_n (dh_hi + dh_lo)[b][n] W1[k][n]
     {
       const int pm = wave & 3;
@@ -553,10 +614,11 @@ __global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int
     }
   }
   stamp(sts, st, 4);
-  // ---- dW1 straight into the flat gradient buffer (this block owns these rows) ----
+  // ---- dW1 straight into the flat gradient buffer (this block owns these rows), unless
+  // the update was applied eagerly above ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
-    if (i >= np) break;
+    if (i >= np || (ONE && eager)) break;
     const int mt = dm0 + 2 * i;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -610,21 +672,24 @@ __global__ __launch_bounds__(512) void bwd(const void* __restrict__ X, const int
 __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
                                              const float* __restrict__ W1alt, const float* __restrict__ V1alt,
                                              long long* __restrict__ hconv, const float* __restrict__ calt,
-                                             long long* __restrict__ hacc, int B, Ctrl* __restrict__ ctrl) {
+                                             long long* __restrict__ hacc, int B, int eager,
+                                             uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl) {
   const Ctrl c = *ctrl;
   const bool mom = c.momentum != 0.f, pend = c.pending != 0;
   // after a step's bwd: current W1 / conv parameters live in the alternates when wpar is
   // set; the pending conv gradient is in hconv[wpar ^ 1]
   const long long* hg = hconv + (c.wpar ^ 1) * NCONV;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NPARAM; i += gridDim.x * blockDim.x) {
-    const bool alt1 = c.wpar && i >= OFF_W1 && i < OFF_B1, altc = c.wpar && i < NCONV;
+    const bool w1 = i >= OFF_W1 && i < OFF_B1;
+    const bool alt1 = !eager && c.wpar && w1, altc = c.wpar && i < NCONV;
     const float w = alt1 ? W1alt[i - OFF_W1] : (altc ? calt[i] : P[i]);
     const float v = alt1 ? V1alt[i - OFF_W1] : (altc ? calt[NCONV + i] : V[i]);
     const float g = i < NCONV ? from_fix(hg[i], CINV) : G[i];
     float wn, vn;
-    sgd_or_keep(pend, w, g, v, c, wn, vn);
+    sgd_or_keep(pend && !(eager && w1), w, g, v, c, wn, vn);  // eager: W1 is already current
     P[i] = wn;
     if (mom) V[i] = vn;
+    if (w1) w1bf[i - OFF_W1] = f2bf(wn);
     G[i] = 0.f;
   }
   // both parities of the fixed-point accumulators start the next step at zero
@@ -671,14 +736,17 @@ size_t convnet2_bwd_lds(int PP) {
          (size_t)CH * PP * 32 + 16 + 256 * 4;
 }
 
+// eager W1 update: world-1 runs with the single-chunk backward (B <= 64) only
+static int eager2(const ConvNetBuffers& b, int B) { return b.eager_w1 && B <= convnet::CH ? 1 : 0; }
+
 template <bool U8>
 static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
   const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
-  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.X, b.P, b.G, b.V, b.W1alt,
-                     b.V1alt, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, b.stamps);
+  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P, b.G, b.V,
+                     b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, eager2(b, B), b.stamps);
 }
 
 template <bool U8>
@@ -686,13 +754,13 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   using namespace convnet;
   const int NS = convnet_num_slices(PP);
   if (B <= CH)
-    hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.X, b.labels, b.P,
-                       b.G, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+    hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
+                       b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
+                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
   else
-    hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.X, b.labels,
-                       b.P, b.G, b.w1bf, b.ctrl, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+    hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
+                       b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
+                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
@@ -717,7 +785,7 @@ hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStrea
 
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {
   hipLaunchKernelGGL(convnet2::flush, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.hconv, b.calt,
-                     b.hacc, B, b.ctrl);
+                     b.hacc, B, eager2(b, B), b.w1bf, b.ctrl);
   return hipGetLastError();
 }
 

@@ -74,7 +74,12 @@ def _build_C(verbose=False, jobs=None) -> Path:
         o = objdir / (s.name + ".o")
         if _deps_newer(o, [s] + hdrs):
             if s.suffix == ".hip":
-                cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)] + common
+                # kernarg preloading: the first 16 argument dwords arrive in SGPRs, so a
+                # kernel's first dependent load does not wait on a kernarg-segment fetch
+                # (DAMD_KERNARG_PRELOAD=0 turns it off for A/B runs)
+                pre = ["-mllvm", "-amdgpu-kernarg-preload-count=16"] if os.environ.get(
+                    "DAMD_KERNARG_PRELOAD", "1") != "0" else []
+                cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)] + common + pre
             else:
                 cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)] + common + [
                     "-fvisibility=hidden"

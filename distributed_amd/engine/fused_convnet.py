@@ -154,11 +154,21 @@ class FusedConvNetEngine(Engine):
         # 30.0 us/step at B=64: same-address atomic serialisation + a serial tail on the
         # critical path) and not bitwise reproducible, so the separate F2 launch is default.
         bufs["fuse_head"] = 1 if env.get_bool("DAMD_CONVNET_FUSE_HEAD", False) else 0
+        # world 1 (no gradient all-reduce): bwd applies the W1 update itself as soon as it
+        # has the slice's gradient, and fwd reads only the bf16 copy (DAMD_EAGER_W1=0: the
+        # deferred update in fwd, as with an all-reduce between the launches)
+        force_ar = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
+        # (B <= 64: the single-chunk backward; the multi-chunk one has no registers to spare
+        # for the slice's masters)
+        self.eager_w1 = (self.kernels == 2 and self.world == 1 and not force_ar and not self.persist
+                         and B <= 64 and env.get_bool("DAMD_EAGER_W1", True))
+        bufs["eager_w1"] = int(self.eager_w1)
         self.stamps = None
         if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
             self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)
             bufs["stamps"] = self.stamps.data_ptr()
         self.trainer = C.ConvNetTrainer(dev.index or 0, bufs, B, self.PP, 1)
+        self._refresh_w1bf()
         # DAMD_FORCE_ALLREDUCE=1 keeps the (size-1) RCCL all-reduce inside the captured step
         # at world 1: the multi-GPU graph path exercised on a single GPU
         force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
@@ -378,6 +388,15 @@ class FusedConvNetEngine(Engine):
             opt.ensure_slots(NPARAM, self.device)
             opt.slots["momentum"].copy_(self.V[:NPARAM])
         torch.cuda.synchronize(self.device)
+
+    def _refresh_w1bf(self):
+        """bf16 copy of W1 from the fp32 master (the eager step's fwd reads only the copy)."""
+        torch.cuda.synchronize(self.device)
+        self.w1bf.copy_(self.P[NCONV:NCONV + FEAT * HID])
+        torch.cuda.synchronize(self.device)
+
+    def after_external_write(self):
+        self._refresh_w1bf()
 
     def sync(self):
         # host readers (get_weights, checkpoints, callbacks) see the trained values: the

@@ -16,3 +16,7 @@ step stamps2 120 python -u scripts/stamps.py 64
 tail -17 gpurun_out/stamps2.log
 step bench_long 200 python -u bench.py
 tail -1 gpurun_out/bench_long.log | cut -c1-200
+step bench_driver 200 python -u bench.py --gpus 1 --steps 20 --warmup 5
+tail -1 gpurun_out/bench_driver.log | cut -c1-200
+step bench_driver2 200 python -u bench.py --gpus 1 --steps 20 --warmup 5
+tail -1 gpurun_out/bench_driver2.log | cut -c1-200

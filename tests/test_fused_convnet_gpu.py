@@ -103,7 +103,7 @@ def test_one_step_matches_reference(B, pp, monkeypatch):
     g64, _, _ = _ref_step(w0, x[:B], y[:B], B, quant=False)
     e64 = rel_errs(g64)
     print("vs fp64 reference:", {k: f"{v:.2e}" for k, v in e64.items()})
-    assert max(e64.values()) < 1e-1, e64
+    assert max(e64.values()) < 8e-2, e64  # measured <= 6.3e-2 over these shapes (bf16 dense compute)
     assert abs(met["loss"] - lsum / B) < 2e-2
     assert abs(met["accuracy"] - corr / B) < 1.5 / B
 
@@ -354,3 +354,34 @@ def test_phase_times_fused_step():
     print("fused step phases (ms):", ph)
     assert ph["forward"] > 0 and ph["backward"] > 0 and ph["allreduce"] >= 0
     assert int(m.optimizer.iterations) == it0 + 5
+
+
+@pytest.mark.parametrize("nesterov", [False, True])
+def test_eager_w1_update_bitwise_equals_deferred(nesterov, monkeypatch):
+    """World 1: bwd applies the W1 update as soon as it has the slice's gradient and fwd
+    reads only the bf16 copy (DAMD_EAGER_W1, default); the same arithmetic as the deferred
+    update in the next fwd, so the runs agree bitwise -- across graph replays, an epoch
+    flush and a host-side set_weights (which must refresh the bf16 copy)."""
+    _need_gpu()
+    monkeypatch.setenv("DAMD_GRAPH_STEPS", "4")
+    x, y = _data(1024)
+    res = []
+    for eager in ("1", "0"):
+        monkeypatch.setenv("DAMD_EAGER_W1", eager)
+        m = _model(lr=0.05, momentum=0.9, nesterov=nesterov, seed=5)
+        eng = _engine(m, 64)
+        assert eng.eager_w1 == (eager == "1")
+        eng.bind(x, y)
+        eng.start_epoch(0, shuffle=True)
+        eng.run(9)
+        met0 = eng.end_epoch()
+        w = m.get_weights()
+        w[2] = w[2] * 0.5  # host write of W1 between epochs
+        m.set_weights(w)
+        eng.start_epoch(1, shuffle=True)
+        eng.run(7)
+        met1 = eng.end_epoch()
+        eng.finish()
+        res.append((np.concatenate([v.ravel() for v in m.get_weights()]), met0, met1))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
