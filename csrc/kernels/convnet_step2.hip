@@ -679,7 +679,11 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
   // after a step's bwd: current W1 / conv parameters live in the alternates when wpar is
   // set; the pending conv gradient is in hconv[wpar ^ 1]
   const long long* hg = hconv + (c.wpar ^ 1) * NCONV;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NPARAM; i += gridDim.x * blockDim.x) {
+  // eager: W1 is current and its gradient was never stored -- only the conv and
+  // b1/W2/b2 parameters are visited
+  const int nvisit = eager ? NPARAM - (OFF_B1 - OFF_W1) : NPARAM;
+  for (int iv = blockIdx.x * blockDim.x + threadIdx.x; iv < nvisit; iv += gridDim.x * blockDim.x) {
+    const int i = eager && iv >= OFF_W1 ? iv + (OFF_B1 - OFF_W1) : iv;
     const bool w1 = i >= OFF_W1 && i < OFF_B1;
     const bool alt1 = !eager && c.wpar && w1, altc = c.wpar && i < NCONV;
     const float w = alt1 ? W1alt[i - OFF_W1] : (altc ? calt[i] : P[i]);
@@ -784,7 +788,7 @@ hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStrea
 }
 
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {
-  hipLaunchKernelGGL(convnet2::flush, dim3(340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.hconv, b.calt,
+  hipLaunchKernelGGL(convnet2::flush, dim3(eager2(b, B) ? 36 : 340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.hconv, b.calt,
                      b.hacc, B, eager2(b, B), b.w1bf, b.ctrl);
   return hipGetLastError();
 }
