@@ -349,7 +349,9 @@ class FusedConvNetEngine(Engine):
         bwd = sum(r[1] for r in rows) / n
         ar = sum(r[2] for r in rows) / n
         return {"forward": fwd, "backward": bwd, "allreduce": ar, "optimizer": 0.0,
-                "step": fwd + bwd + ar, "note": "SGD update fused into the forward kernel",
+                "step": fwd + bwd + ar,
+                "note": ("W1 SGD update in the backward kernel, conv / b1 / W2 / b2 updates in the forward kernel"
+                         if self.eager_w1 else "SGD update fused into the forward kernel"),
                 "allreduce_kind": self.allreduce_kind}
 
     def prepare(self, n_steps):
