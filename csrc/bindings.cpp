@@ -83,7 +83,8 @@ class ConvNetTrainer : public StepExecutor {
       HIP_CHECK(convnet2_launch_bwd(b_, B_, PP_, stream_));
       HIP_CHECK(hipEventRecord(ev[2], stream_));
       if (grad_allreduce_) {
-        if (peer_) peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, b_.hconv, 2 * kConvNetNConv);
+        if (peer_ && fold_) peer_->allreduce_staged((long)convnet_grad_count(PP_), 2 * kConvNetNConv, stream_);
+        else if (peer_) peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, b_.hconv, 2 * kConvNetNConv);
         else if (comm_) comm_->allreduce_f32_i64(b_.G, convnet_grad_count(PP_), b_.hconv, 2 * kConvNetNConv, stream_);
       }
       HIP_CHECK(hipEventRecord(ev[3], stream_));
@@ -108,6 +109,36 @@ class ConvNetTrainer : public StepExecutor {
     b_.X = P_<const void>(X); b_.labels = P_<const int>(labels); b_.x_u8 = x_u8;
     invalidate_graphs();
   }
+  // Fold the per-step peer all-reduce into the step kernels: bwd writes its gradient
+  // straight into the all-reduce's `in` staging (no copy-in pass), the next fwd / flush
+  // read the reduced gradient from `out` (no copy-out pass); the peer kernel only
+  // exchanges.  fold = false restores the engine's own buffers (copy-in / copy-out).
+  void set_peer_fold(PeerAllreduce* p, bool fold) {
+    if (!G_own_) { G_own_ = b_.G; hconv_own_ = b_.hconv; }
+    set_peer(p);
+    fold_ = fold && p && p->world() > 1 && b_.kernels == 2;
+    if (fold_) {
+      const long n = (long)convnet_grad_count(PP_), nfp = (n + 3) / 4 * 4;
+      if (PeerAllreduce::message_words(n, 2 * kConvNetNConv) > p->capacity())
+        throw std::invalid_argument("peer all-reduce capacity too small for the folded step");
+      b_.G = p->in_local();
+      b_.hconv = reinterpret_cast<long long*>(p->in_local() + nfp);
+      b_.Gr = p->out_local();
+      b_.hconv_r = reinterpret_cast<long long*>(p->out_local() + nfp);
+    } else {
+      b_.G = G_own_; b_.hconv = hconv_own_; b_.Gr = nullptr; b_.hconv_r = nullptr;
+    }
+    invalidate_graphs();
+  }
+  bool folded() const { return fold_; }
+  // the reduced [loss, correct, count] tail of the last step (host copy, synchronizes)
+  std::vector<float> metric_tail() {
+    std::vector<float> t(3);
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    const float* g = b_.Gr ? b_.Gr : b_.G;
+    HIP_CHECK(hipMemcpy(t.data(), g + kConvNetNParam, 3 * sizeof(float), hipMemcpyDeviceToHost));
+    return t;
+  }
   void flush() {
     if (b_.kernels == 2) HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
     else HIP_CHECK(convnet_launch_flush(b_, PP_, stream_));
@@ -117,6 +148,7 @@ class ConvNetTrainer : public StepExecutor {
   int batch() const { return B_; }
 
  protected:
+  void enqueue_tail() override { flush(); }
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     if (b_.kernels == 2) HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
@@ -126,14 +158,19 @@ class ConvNetTrainer : public StepExecutor {
     // exactly, in the same call as the fp32 gradient + metric buffer
     long long* aux = b_.kernels == 2 ? b_.hconv : nullptr;
     const long n64 = b_.kernels == 2 ? 2 * kConvNetNConv : 0;  // both parities (see convnet_step2.hip)
-    if (peer_)  // native xGMI two-shot all-reduce
+    if (peer_ && fold_)  // the message is already in the peer `in` staging: exchange only
+      peer_->allreduce_staged((long)convnet_grad_count(PP_), n64, stream_);
+    else if (peer_)  // native xGMI two-shot all-reduce
       peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, aux, n64);
     else if (comm_)  // comm set only when a reduction is wanted
       comm_->allreduce_f32_i64(b_.G, convnet_grad_count(PP_), aux, (size_t)n64, stream_);
   }
 
  private:
-  ConvNetBuffers b_;
+  ConvNetBuffers b_{};
+  float* G_own_ = nullptr;         // the engine's gradient buffer (b_.G unless folded)
+  long long* hconv_own_ = nullptr;
+  bool fold_ = false;
   int B_, PP_, grad_allreduce_;
   long long* phacc_ = nullptr;
   long long* phconv_ = nullptr;
@@ -224,10 +261,14 @@ PYBIND11_MODULE(_C, m) {
       .def("set_data", &ConvNetTrainer::set_data, py::arg("x"), py::arg("labels"), py::arg("x_u8") = 0)
       .def("set_comm", [](ConvNetTrainer& t, RcclComm* c) { t.set_comm(c); },
            py::keep_alive<1, 2>())
-      .def("set_peer", [](ConvNetTrainer& t, PeerAllreduce* p) { t.set_peer(p); }, py::keep_alive<1, 2>())
+      .def("set_peer", [](ConvNetTrainer& t, PeerAllreduce* p, bool fold) { t.set_peer_fold(p, fold); },
+           py::arg("peer"), py::arg("fold") = false, py::keep_alive<1, 2>())
+      .def_property_readonly("folded", &ConvNetTrainer::folded)
+      .def("metric_tail", &ConvNetTrainer::metric_tail)
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
-      .def("capture", &ConvNetTrainer::capture)
-      .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
+      .def("capture", &ConvNetTrainer::capture, py::arg("k"), py::arg("tail") = false)
+      .def("launch_graph", &ConvNetTrainer::launch_graph, py::arg("k"), py::arg("tail") = false)
+      .def("run", &ConvNetTrainer::run, py::arg("k"), py::arg("tail") = false, py::call_guard<py::gil_scoped_release>())
       .def("run_persistent", &ConvNetTrainer::run_persistent, py::arg("steps"), py::arg("timeout_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
       .def("phase_times", &ConvNetTrainer::phase_times, py::arg("steps"), py::call_guard<py::gil_scoped_release>())

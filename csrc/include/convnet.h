@@ -25,6 +25,11 @@ struct ConvNetBuffers {
   // then reads only the bf16 copy.  0: the update is deferred into the next fwd (after
   // the all-reduce of G)
   int eager_w1;
+  // read side of the gradient when the peer all-reduce is folded into the step (the
+  // all-reduce's `out` staging; G / hconv are then its `in` staging, written by bwd):
+  // fwd, bwd's metric fold and flush read Gr / hconv_r.  Null: G / hconv.
+  float* Gr;
+  long long* hconv_r;
 };
 constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;

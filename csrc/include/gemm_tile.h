@@ -183,9 +183,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       }
       const int n = n0 + t;
       if (n < a.N) {
-        float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
-        st[n] = s;
-        st[a.N + n] = q;
+        if (a.stats_acc) {
+          unsafeAtomicAdd(a.stats_acc + n, (double)s);
+          unsafeAtomicAdd(a.stats_acc + a.N + n, (double)q);
+        } else {
+          float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
+          st[n] = s;
+          st[a.N + n] = q;
+        }
       }
     }
   }

@@ -8,6 +8,30 @@
 namespace damd {
 
 // BatchNorm (training) ---------------------------------------------------------------
+// Batch statistics without a finalize launch: the producers (conv GEMM epilogue E_STATS
+// with GemmArgs::stats_acc, splitk_finish, bn_bwd_reduce / pool_bn_bwd_reduce with `acc`)
+// add their per-block fp32 partials into acc[2][C] with fp64 atomics (exact for partials
+// within 2^29 of each other: arrival order does not change the sum in practice); the
+// consumer kernel (bn_apply, bn_relu_maxpool_fwd / bn_bwd_apply, pool_bn_bwd_apply)
+// derives the coefficients from acc in its prologue (every block, into LDS); its block 0
+// also writes st / co, the moving statistics and dgamma / dbeta.  The accumulators are
+// zeroed once per step (gather_batch's `zero` range).
+struct BNFin {
+  const double* acc;   // [2][C] sum, sum of squares; null: the kernel reads st as before
+  const float* gamma;  // may be null (1)
+  const float* beta;   // may be null (0)
+  float* st;           // [4][C] out (block 0): mean, invstd, scale, shift
+  float* rmean;        // moving statistics (block 0), may be null
+  float* rvar;
+  float count, eps, mom;
+};
+struct BNBwdFin {
+  const double* acc;   // [2][C] sum dz, sum dz * xhat; null: the kernel reads co as before
+  float* dgamma;       // += (block 0), may be null
+  float* dbeta;
+  float* co;           // [3][C] out (block 0)
+  float count;
+};
 // partials [T][2][C] (column sum, sum of squares; from the conv GEMM epilogue) ->
 // st[4][C] = mean, invstd, scale = gamma*invstd, shift = beta - mean*scale; moving
 // statistics updated Keras-style (m = m*momentum + batch*(1-momentum), biased variance).
@@ -15,13 +39,15 @@ hipError_t bn_finalize(const float* part, int T, int C, float count, const float
                        float eps, float momentum, float* rmean, float* rvar, float* st, hipStream_t s);
 // y = act(x*scale + shift [+ r | + r*scale2 + shift2])   (res_mode 0 / 1 / 2)
 hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const float* st2, int res_mode,
-                    int relu, uint16_t* y, long M, int C, hipStream_t s);
+                    int relu, uint16_t* y, long M, int C, hipStream_t s, const BNFin* f1 = nullptr,
+                    const BNFin* f2 = nullptr);
 // inference: y = act(x*scale + shift) with scale/shift from the moving statistics
 // backward, pass 1: dz = dy * [y > 0] (relu_mask 1; relu_mask 2: y recomputed as
 // bf16(relu(x * sc + sh)) from x and st, bitwise the stored bn_apply output, y unread) ; per-block partial sums of dz and
 // dz * xhat -> part [T][2][C]; optionally writes dz (bf16).  Returns T via *T_out.
 hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
-                         const float* st, uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s);
+                         const float* st, uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s,
+                         double* acc = nullptr);
 int bn_bwd_blocks(long M, int C);
 // pass 2: dgamma/dbeta (accumulated into the gradient sinks, may be null) and the
 // coefficients co[3][C] so that dx = a*dz + b + c*xhat
@@ -29,7 +55,7 @@ hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const f
                            float* dgamma, float* dbeta, float* co, hipStream_t s);
 // pass 3: dx = a*dz + b + c*xhat, dz recomputed from dy and the relu mask (bf16 out)
 hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
-                        const float* co, uint16_t* dx, long M, int C, hipStream_t s);
+                        const float* co, uint16_t* dx, long M, int C, hipStream_t s, const BNBwdFin* bf = nullptr);
 
 // Pooling ----------------------------------------------------------------------------------
 hipError_t maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
@@ -38,14 +64,15 @@ hipError_t maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int
                        int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* dx, hipStream_t s);
 // stem fusion (BatchNorm(st) -> ReLU -> MaxPool): the pool reads the conv output x
 hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H, int W, int C, int ph, int pw, int sh,
-                               int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s);
+                               int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s,
+                               const BNFin* f = nullptr);
 // its backward: BN-backward partials / apply with the pool routing + ReLU mask recomputed
 hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                               int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                              float* part, int T, hipStream_t s);
+                              float* part, int T, hipStream_t s, double* acc = nullptr);
 hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                              int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                             const float* co, uint16_t* dx, hipStream_t s);
+                             const float* co, uint16_t* dx, hipStream_t s, const BNBwdFin* bf = nullptr);
 // global average pool over H*W: x [N][HW][C] bf16 -> y [N][C] (bf16 or fp32)
 hipError_t gap_fwd(const uint16_t* x, int N, int HW, int C, void* y, int y_f32, hipStream_t s);
 hipError_t gap_bwd(const void* dy, int dy_f32, int N, int HW, int C, uint16_t* dx, hipStream_t s);
@@ -116,9 +143,11 @@ hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, u
 // the step's rows of the (epoch-permuted) dataset: row = (cursor*global_batch + row0 + i)
 // mod nsamples (cursor from ctrl); x fp32 or uint8 (k / scale, i.e. exactly float32(k/255)
 // for scale 255) [n][HW][Cin] -> bf16
-// [per][HW][Cp] zero-padded channels; labels int32.
+// [per][HW][Cp] zero-padded channels; labels int32.  `zero` (optional): nzero doubles
+// cleared in the same launch (the step's BatchNorm statistics accumulators, BNFin).
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
-                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s);
+                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, double* zero = nullptr,
+                        long nzero = 0);
 // fp32 [R][C1][C2] -> bf16 [R][C1p][C2p] (zero padding)
 hipError_t pad_cast(const float* src, int R, int C1, int C2, int C1p, int C2p, uint16_t* dst, hipStream_t s);
 // dst fp32 [R][C1][C2] += src fp32 [R][C1p][C2p] (the un-padded part)

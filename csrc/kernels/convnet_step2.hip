@@ -64,7 +64,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
                                            uint16_t* __restrict__ pooled, uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv,
                                            float* __restrict__ calt, int B, int PP, int lg, int eager,
-                                           unsigned long long* st) {
+                                           unsigned long long* st, const long long* __restrict__ hconv_r) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nblk = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + s;
@@ -80,6 +80,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
   float* lut = cw + NCONV + IB * PP * 32 / 4;                              // [256] k / 255
   const Ctrl c = *ctrl;
+  if (c.pad[2]) return;  // dry replay (graph warm-up): no work, no writes
   const int par = c.wpar;
   if (lin == 0 && tid == 0) {
     ctrl->cur2 = c.cursor;
@@ -125,7 +126,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // (bwd added it into hconv[par ^ 1])
   const int tcl = min(tid, NCONV - 1);
   const float cp = (par ? calt : P)[tcl], cv = (par ? calt + NCONV : V)[tcl];
-  const long long cq = hconv[(par ^ 1) * NCONV + tcl];
+  const long long cq = hconv_r[(par ^ 1) * NCONV + tcl];
   // b1/W2/b2: the grid's last two blocks own their pending update (nobody else in this
   // launch reads them; bwd reads the updated values)
   const int si = (lin - (nblk - 2)) * 512 + tid;
@@ -265,7 +266,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
-                                           unsigned long long* st) {
+                                           unsigned long long* st, const float* __restrict__ Gr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   Stamps sts;
   stamp(sts, st, 0);
@@ -292,6 +293,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   int* ylds = reinterpret_cast<int*>(db1p + 16 * HID);  // [CH] label of the row, -1 if invalid
   float* lut = reinterpret_cast<float*>(cs + CH * KC + 16);  // [256] k / 255 (after the codes)
   const Ctrl c = *ctrl;
+  if (c.pad[2]) return;
   const int cur = c.cur2, par = c.par2;
   const long long* hcur = hacc + (long)par * B * HID;
   if (s == 0 && tid == 0) {
@@ -316,7 +318,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   const int ae = s * chunk_aux + ae_local;
   const bool aux_on = ae_local < chunk_aux && ae < NAUX2;
   const int aec = min(ae, NAUX2 - 1);
-  const float ag_old = G[OFF_LOSS + max(0, min(aec - NSMALL, 2))];  // previous step's reduced metric
+  const float ag_old = Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];  // previous step's reduced metric
   float arsum = 0.f;
 
   // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
@@ -669,12 +671,16 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 // flush: apply the pending (deferred) update to every parameter, zero the gradient
 // buffers, fold the pending metrics into the epoch accumulators, clear `pending`.
 // =================================================================================
+// G / hconv: the reduced gradient (the peer all-reduce's `out` when it is folded into the
+// step, see ConvNetBuffers::Gr); hconv_w: the buffer bwd adds into (both parities cleared)
 __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
                                              const float* __restrict__ W1alt, const float* __restrict__ V1alt,
                                              long long* __restrict__ hconv, const float* __restrict__ calt,
                                              long long* __restrict__ hacc, int B, int eager,
-                                             uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl) {
+                                             uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
+                                             long long* __restrict__ hconv_w) {
   const Ctrl c = *ctrl;
+  if (c.pad[2]) return;
   const bool mom = c.momentum != 0.f, pend = c.pending != 0;
   // after a step's bwd: current W1 / conv parameters live in the alternates when wpar is
   // set; the pending conv gradient is in hconv[wpar ^ 1]
@@ -698,7 +704,10 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
   }
   // both parities of the fixed-point accumulators start the next step at zero
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * NCONV + 2 * B * HID; i += gridDim.x * blockDim.x) {
-    if (i < 2 * NCONV) hconv[i] = 0;
+    if (i < 2 * NCONV) {
+      hconv[i] = 0;
+      hconv_w[i] = 0;
+    }
     else hacc[i - 2 * NCONV] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -749,8 +758,10 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
   const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
-  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P, b.G, b.V,
-                     b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, eager2(b, B), b.stamps);
+  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P,
+                     b.Gr ? b.Gr : b.G, b.V,
+                     b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, eager2(b, B), b.stamps,
+                     b.hconv_r ? b.hconv_r : b.hconv);
 }
 
 template <bool U8>
@@ -760,11 +771,11 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G);
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr);
+                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
@@ -788,8 +799,9 @@ hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStrea
 }
 
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {
-  hipLaunchKernelGGL(convnet2::flush, dim3(eager2(b, B) ? 36 : 340), dim3(256), 0, st, b.P, b.G, b.V, b.W1alt, b.V1alt, b.hconv, b.calt,
-                     b.hacc, B, eager2(b, B), b.w1bf, b.ctrl);
+  hipLaunchKernelGGL(convnet2::flush, dim3(eager2(b, B) ? 36 : 340), dim3(256), 0, st, b.P, b.Gr ? b.Gr : b.G, b.V,
+                     b.W1alt, b.V1alt, b.hconv_r ? b.hconv_r : b.hconv, b.calt, b.hacc, B, eager2(b, B), b.w1bf, b.ctrl,
+                     b.hconv);
   return hipGetLastError();
 }
 

@@ -531,7 +531,8 @@ __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__
 // (BatchNorm batch statistics: stats[blk][2][N]).  Thread = 8 columns of one row.
 __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ slab, int S, int M, int N,
                                                       const float* __restrict__ bias, const uint16_t* R, int relu,
-                                                      float* __restrict__ stats, int rb, uint16_t* out, int ldc) {
+                                                      float* __restrict__ stats, int rb, uint16_t* out, int ldc,
+                                                      double* __restrict__ stats_acc) {
   __shared__ float red[2][NT * 8];
   // blockIdx.y: band of up to NT x 8 columns (wide layers: N > 2048)
   const int c0 = blockIdx.y * NT * 8, Nb = min(N - c0, NT * 8);
@@ -585,7 +586,7 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
       *reinterpret_cast<uint4*>(out + (size_t)m * ldc + n) = uint4{pk[0], pk[1], pk[2], pk[3]};
     }
   }
-  if (!stats) return;
+  if (!stats && !stats_acc) return;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     red[0][t * 8 + e] = r0 < rp ? cs[e] : 0.f;
@@ -599,8 +600,13 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
       a += red[0][(q * cg + gg) * 8 + e];
       b += red[1][(q * cg + gg) * 8 + e];
     }
-    stats[(size_t)blockIdx.x * 2 * N + c0 + c] = a;
-    stats[(size_t)blockIdx.x * 2 * N + N + c0 + c] = b;
+    if (stats_acc) {
+      unsafeAtomicAdd(stats_acc + c0 + c, (double)a);
+      unsafeAtomicAdd(stats_acc + N + c0 + c, (double)b);
+    } else {
+      stats[(size_t)blockIdx.x * 2 * N + c0 + c] = a;
+      stats[(size_t)blockIdx.x * 2 * N + N + c0 + c] = b;
+    }
   }
 }
 
@@ -677,12 +683,12 @@ hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipS
 }
 
 hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
-                         float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s) {
+                         float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s, double* stats_acc) {
   if (splits < 1 || N % 8 || ldc % 8 || rows_per_block < 1) return hipErrorInvalidValue;
   const int grid = (M + rows_per_block - 1) / rows_per_block;
   const int bands = (N / 8 + NT - 1) / NT;
   hipLaunchKernelGGL(splitk_finish_k, dim3(grid, bands), dim3(NT), 0, s, slab, splits, M, N, bias, R, relu, stats,
-                     rows_per_block, out, ldc);
+                     rows_per_block, out, ldc, stats_acc);
   return hipGetLastError();
 }
 

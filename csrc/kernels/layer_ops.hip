@@ -94,6 +94,71 @@ __device__ __forceinline__ void reduce_partials8(const float* __restrict__ part,
   __syncthreads();
 }
 
+// ---- in-consumer finalize (BNFin / BNBwdFin, layer_ops.h) ----------------------------
+// Every block derives the per-channel coefficients of all C channels from the fp64
+// accumulators into LDS (s: [4][C] for the forward, [3][C] for the backward); block 0 also
+// publishes them (st / co), updates the moving statistics and adds dgamma / dbeta.  The
+// returned pointer replaces st / co in the kernel body (global when acc is null).
+__device__ __forceinline__ const float* bn_fin_prologue(const BNFin& f, int C, float* s, const float* st) {
+  if (f.acc == nullptr) return st;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const double mean = f.acc[c] / (double)f.count;
+    double var = f.acc[C + c] / (double)f.count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float m = (float)mean, v = (float)var;
+    const float inv = rsqrtf(v + f.eps);
+    const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
+    const float sc = g * inv, sh = b - m * sc;
+    s[c] = m;
+    s[C + c] = inv;
+    s[2 * C + c] = sc;
+    s[3 * C + c] = sh;
+    if (blockIdx.x == 0) {
+      f.st[c] = m;
+      f.st[C + c] = inv;
+      f.st[2 * C + c] = sc;
+      f.st[3 * C + c] = sh;
+      if (f.rmean) {
+        f.rmean[c] = f.rmean[c] * f.mom + m * (1.f - f.mom);
+        f.rvar[c] = f.rvar[c] * f.mom + v * (1.f - f.mom);
+      }
+    }
+  }
+  __syncthreads();
+  return s;
+}
+__device__ __forceinline__ const float* bn_bwd_fin_prologue(const BNBwdFin& f, int C, const float* st, float* s,
+                                                            const float* co) {
+  if (f.acc == nullptr) return co;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float db = (float)f.acc[c], dg = (float)f.acc[C + c];
+    const float a = st[2 * C + c];
+    s[c] = a;
+    s[C + c] = -a * db / f.count;
+    s[2 * C + c] = -a * dg / f.count;
+    if (blockIdx.x == 0) {
+      if (f.dbeta) f.dbeta[c] += db;
+      if (f.dgamma) f.dgamma[c] += dg;
+      f.co[c] = s[c];
+      f.co[C + c] = s[C + c];
+      f.co[2 * C + c] = s[2 * C + c];
+    }
+  }
+  __syncthreads();
+  return s;
+}
+// per-block (fp32, fixed order) partial of channel ch -> the fp64 accumulator or the
+// partials row of this block
+__device__ __forceinline__ void put_partial(float* part, double* acc, int C, int ch, float a, float b) {
+  if (acc) {
+    unsafeAtomicAdd(acc + ch, (double)a);
+    unsafeAtomicAdd(acc + C + ch, (double)b);
+  } else {
+    part[(size_t)blockIdx.x * 2 * C + ch] = a;
+    part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
+  }
+}
+
 __global__ __launch_bounds__(FT) void bn_finalize_k(const float* part, int T, int C, float count,
                                                     const float* gamma, const float* beta, float eps, float mom,
                                                     float* rmean, float* rvar, float* st) {
@@ -119,9 +184,13 @@ __global__ __launch_bounds__(FT) void bn_finalize_k(const float* part, int T, in
   }
 }
 
-__global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x, const float* __restrict__ st,
-                                                 const uint16_t* __restrict__ r, const float* __restrict__ st2,
-                                                 int res_mode, int relu, uint16_t* __restrict__ y, long n8, int C) {
+__global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x, const float* st_in,
+                                                 const uint16_t* __restrict__ r, const float* st2_in,
+                                                 int res_mode, int relu, uint16_t* __restrict__ y, long n8, int C,
+                                                 BNFin f1, BNFin f2) {
+  extern __shared__ float sfin[];  // [4][C] (f1), then [4][C] (f2)
+  const float* st = bn_fin_prologue(f1, C, sfin, st_in);
+  const float* st2 = res_mode == 2 ? bn_fin_prologue(f2, C, sfin + 4 * C, st2_in) : st2_in;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     const int c = (int)((i * 8) % C);
     float xv[8], sc[8], sh[8];
@@ -155,7 +224,8 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x,
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                       int relu_mask, const uint16_t* __restrict__ x,
                                                       const float* __restrict__ st, uint16_t* __restrict__ dz_out,
-                                                      float* __restrict__ part, long M, int C, long rows_per_block) {
+                                                      float* __restrict__ part, long M, int C, long rows_per_block,
+                                                      double* __restrict__ acc) {
   __shared__ float red[2][NT * 8];
   const int cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;  // rows per iteration
@@ -208,8 +278,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
       a += red[0][(q * cg + gg) * 8 + e];
       b += red[1][(q * cg + gg) * 8 + e];
     }
-    part[(size_t)blockIdx.x * 2 * C + ch] = a;
-    part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
+    put_partial(part, acc, C, ch, a, b);
   }
 }
 
@@ -231,8 +300,10 @@ __global__ __launch_bounds__(FT) void bn_bwd_finalize_k(const float* part, int T
 
 __global__ __launch_bounds__(NT) void bn_bwd_apply_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                      int relu_mask, const uint16_t* __restrict__ x,
-                                                     const float* __restrict__ st, const float* __restrict__ co,
-                                                     uint16_t* __restrict__ dx, long n8, int C) {
+                                                     const float* __restrict__ st, const float* co_in,
+                                                     uint16_t* __restrict__ dx, long n8, int C, BNBwdFin bf) {
+  extern __shared__ float sfin[];  // [3][C]
+  const float* co = bn_bwd_fin_prologue(bf, C, st, sfin, co_in);
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     const int c = (int)((i * 8) % C);
     float d[8], xv[8], mean[8], inv[8], a[8], b[8], cc[8];
@@ -426,8 +497,11 @@ __global__ __launch_bounds__(NT) void avgpool_bwd_k(const uint16_t* __restrict__
 // passes, so neither the 4x larger un-pooled gradient nor the ReLU output is stored.
 
 __global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_k(const uint16_t* __restrict__ x,
-                                                            const float* __restrict__ st, PoolGeo g,
-                                                            uint16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+                                                            const float* st_in, PoolGeo g,
+                                                            uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                            BNFin f) {
+  extern __shared__ float sfin[];
+  const float* st = bn_fin_prologue(f, g.C, sfin, st_in);
   const int cg = g.C / 8;
   const long total = (long)g.N * g.Ho * g.Wo * cg;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < total; i += (long)gridDim.x * NT) {
@@ -474,8 +548,11 @@ __global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_k(const uint16_t* __re
 // loads and normalisations per 4 outputs instead of 36.
 template <int PT, int PL>
 __global__ __launch_bounds__(NT) void bn_relu_maxpool_fwd_q_k(const uint16_t* __restrict__ x,
-                                                              const float* __restrict__ st, PoolGeo g,
-                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+                                                              const float* st_in, PoolGeo g,
+                                                              uint16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                              BNFin f) {
+  extern __shared__ float sfin[];
+  const float* st = bn_fin_prologue(f, g.C, sfin, st_in);
   const int cg = g.C / 8;
   const int Ho2 = g.Ho / 2, Wo2 = g.Wo / 2;
   const long total = (long)g.N * Ho2 * Wo2 * cg;
@@ -590,7 +667,8 @@ __device__ __forceinline__ void stem_dy8(const uint16_t* __restrict__ dpool, con
 __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_k(const uint16_t* __restrict__ dpool,
                                                            const uint8_t* __restrict__ arg, PoolGeo g,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ st,
-                                                           float* __restrict__ part, long M, long rows_per_block) {
+                                                           float* __restrict__ part, long M, long rows_per_block,
+                                                           double* __restrict__ acc) {
   __shared__ float red[2][NT * 8];
   const int C = g.C, cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;
@@ -629,16 +707,17 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_k(const uint16_t* __res
       a += red[0][(q * cg + gg) * 8 + e];
       b += red[1][(q * cg + gg) * 8 + e];
     }
-    part[(size_t)blockIdx.x * 2 * C + ch] = a;
-    part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
+    put_partial(part, acc, C, ch, a, b);
   }
 }
 
 __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_k(const uint16_t* __restrict__ dpool,
                                                           const uint8_t* __restrict__ arg, PoolGeo g,
                                                           const uint16_t* __restrict__ x, const float* __restrict__ st,
-                                                          const float* __restrict__ co, uint16_t* __restrict__ dx,
-                                                          long n8) {
+                                                          const float* co_in, uint16_t* __restrict__ dx,
+                                                          long n8, BNBwdFin bf) {
+  extern __shared__ float sfin[];
+  const float* co = bn_bwd_fin_prologue(bf, g.C, st, sfin, co_in);
   const int C = g.C, cg = C / 8;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
     const int c8 = (int)(i % cg), c = c8 * 8;
@@ -726,7 +805,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_q_k(const uint16_t* __r
                                                              const uint8_t* __restrict__ arg, PoolGeo g,
                                                              const uint16_t* __restrict__ x,
                                                              const float* __restrict__ st, float* __restrict__ part,
-                                                             long nquad, long quads_per_block) {
+                                                             long nquad, long quads_per_block, double* __restrict__ acc) {
   __shared__ float red[2][NT * 8];
   const int C = g.C, cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;
@@ -779,8 +858,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_q_k(const uint16_t* __r
       sa += red[0][(q * cg + gg) * 8 + e];
       sb += red[1][(q * cg + gg) * 8 + e];
     }
-    part[(size_t)blockIdx.x * 2 * C + ch] = sa;
-    part[(size_t)blockIdx.x * 2 * C + C + ch] = sb;
+    put_partial(part, acc, C, ch, sa, sb);
   }
 }
 
@@ -789,8 +867,10 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_apply_q_k(const uint16_t* __re
                                                             const uint8_t* __restrict__ arg, PoolGeo g,
                                                             const uint16_t* __restrict__ x,
                                                             const float* __restrict__ st,
-                                                            const float* __restrict__ co, uint16_t* __restrict__ dx,
-                                                            long nq8) {
+                                                            const float* co_in, uint16_t* __restrict__ dx,
+                                                            long nq8, BNBwdFin bf) {
+  extern __shared__ float sfin[];
+  const float* co = bn_bwd_fin_prologue(bf, g.C, st, sfin, co_in);
   const int C = g.C, cg = C / 8;
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nq8; i += (long)gridDim.x * NT) {
     const int c8 = (int)(i % cg), c = c8 * 8;
@@ -1199,7 +1279,8 @@ __global__ __launch_bounds__(NT) void sgd_step_k(float* __restrict__ P, const fl
 __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x, int x_u8, float scale,
                                                      const int32_t* __restrict__ labels, Ctrl* __restrict__ ctrl,
                                                      int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
-                                                     int32_t* __restrict__ yb) {
+                                                     int32_t* __restrict__ yb, double* __restrict__ zero, long nzero) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nzero; i += (long)gridDim.x * NT) zero[i] = 0.0;
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
@@ -1403,10 +1484,11 @@ hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ct
 }
 
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
-                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s) {
+                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, double* zero, long nzero) {
   if (Cp % 8 && !(Cp == 4 && Cin <= 4 && HW % 2 == 0)) return hipErrorInvalidValue;
+  if (nzero < 0 || (nzero > 0 && zero == nullptr)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp / 8)), dim3(NT), 0, s, x, x_u8, scale, labels,
-                     ctrl, per, HW, Cin, Cp, xb, yb);
+                     ctrl, per, HW, Cin, Cp, xb, yb, zero, nzero);
   return hipGetLastError();
 }
 
@@ -1428,10 +1510,23 @@ hipError_t bn_finalize(const float* part, int T, int C, float count, const float
   return hipGetLastError();
 }
 
+// blocks of a consumer that finalizes in its prologue: every block pays one pass over the
+// C channels, so the grid-stride kernels run at most 8 blocks per CU
+constexpr int FIN_GRID_CAP = 2048;
+constexpr int FIN_MAX_C = 4096;
+static const BNFin kNoFin{};
+static const BNBwdFin kNoBwdFin{};
+
 hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const float* st2, int res_mode, int relu,
-                    uint16_t* y, long M, int C, hipStream_t s) {
+                    uint16_t* y, long M, int C, hipStream_t s, const BNFin* f1, const BNFin* f2) {
   const long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, x, st, r, st2, res_mode, relu, y, n8, C);
+  const BNFin a = f1 ? *f1 : kNoFin, b = (f2 && res_mode == 2) ? *f2 : kNoFin;
+  if ((a.acc && !a.st) || (b.acc && !b.st) || ((a.acc || b.acc) && C > FIN_MAX_C)) return hipErrorInvalidValue;
+  const size_t lds = (a.acc ? 4 * C * sizeof(float) : 0) + (b.acc ? 4 * C * sizeof(float) : 0);
+  // (the f2 region starts at 4C: allocate it whenever f2 finalizes)
+  const size_t lds2 = b.acc ? 8 * C * sizeof(float) : lds;
+  hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(n8, NT, (a.acc || b.acc) ? FIN_GRID_CAP : 8192)), dim3(NT), lds2, s,
+                     x, st, r, st2, res_mode, relu, y, n8, C, a, b);
   return hipGetLastError();
 }
 
@@ -1443,10 +1538,11 @@ int bn_bwd_blocks(long M, int C) {
 }
 
 hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
-                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s) {
-  if (C % 8 || C / 8 > NT) return hipErrorInvalidValue;
+                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s, double* acc) {
+  if (C % 8 || C / 8 > NT || (!part && !acc)) return hipErrorInvalidValue;
   const long rows = (M + T - 1) / T;
-  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows);
+  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows,
+                     acc);
   return hipGetLastError();
 }
 
@@ -1460,9 +1556,12 @@ hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const f
 }
 
 hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
-                        const float* co, uint16_t* dx, long M, int C, hipStream_t s) {
+                        const float* co, uint16_t* dx, long M, int C, hipStream_t s, const BNBwdFin* bf) {
   const long n8 = M * C / 8;
-  hipLaunchKernelGGL(bn_bwd_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, dy, y, relu_mask, x, st, co, dx, n8, C);
+  const BNBwdFin f = bf ? *bf : kNoBwdFin;
+  if (f.acc && (!f.co || C > FIN_MAX_C)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_apply_k, dim3(grid_for(n8, NT, f.acc ? FIN_GRID_CAP : 8192)), dim3(NT),
+                     f.acc ? 3 * C * sizeof(float) : 0, s, dy, y, relu_mask, x, st, co, dx, n8, C, f);
   return hipGetLastError();
 }
 
@@ -1483,51 +1582,61 @@ hipError_t maxpool_bwd(const uint16_t* dy, const uint8_t* arg, int N, int H, int
 }
 
 hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H, int W, int C, int ph, int pw, int sh,
-                               int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s) {
+                               int sw, int pad_t, int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s,
+                               const BNFin* fp) {
   if (C % 8 || ph * pw > 255) return hipErrorInvalidValue;
+  const BNFin f = fp ? *fp : kNoFin;
+  if (f.acc && (!f.st || C > FIN_MAX_C)) return hipErrorInvalidValue;
+  const int cap = f.acc ? FIN_GRID_CAP : 8192;
+  const size_t lds = f.acc ? 4 * C * sizeof(float) : 0;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   if (quad_pool_geo(g) && Ho % 2 == 0 && Wo % 2 == 0) {
     auto k = g.pt ? (g.pl ? bn_relu_maxpool_fwd_q_k<1, 1> : bn_relu_maxpool_fwd_q_k<1, 0>)
                   : (g.pl ? bn_relu_maxpool_fwd_q_k<0, 1> : bn_relu_maxpool_fwd_q_k<0, 0>);
-    hipLaunchKernelGGL(k, dim3(grid_for((long)N * Ho * Wo * C / 32)), dim3(NT), 0, s, x, st, g, y, arg);
+    hipLaunchKernelGGL(k, dim3(grid_for((long)N * Ho * Wo * C / 32, NT, cap)), dim3(NT), lds, s, x, st, g, y, arg, f);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(bn_relu_maxpool_fwd_k, dim3(grid_for((long)N * Ho * Wo * C / 8)), dim3(NT), 0, s, x, st, g, y,
-                     arg);
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_k, dim3(grid_for((long)N * Ho * Wo * C / 8, NT, cap)), dim3(NT), lds, s, x,
+                     st, g, y, arg, f);
   return hipGetLastError();
 }
 
 hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                               int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                              float* part, int T, hipStream_t s) {
-  if (C % 8 || C / 8 > NT) return hipErrorInvalidValue;
+                              float* part, int T, hipStream_t s, double* acc) {
+  if (C % 8 || C / 8 > NT || (!part && !acc)) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   const long M = (long)N * H * W, rows = (M + T - 1) / T;
   if (quad_pool_geo(g)) {
     const long nq = (long)N * Ho * Wo, qpb = (nq + T - 1) / T;
     auto k = g.pt ? (g.pl ? pool_bn_bwd_reduce_q_k<1, 1> : pool_bn_bwd_reduce_q_k<1, 0>)
                   : (g.pl ? pool_bn_bwd_reduce_q_k<0, 1> : pool_bn_bwd_reduce_q_k<0, 0>);
-    hipLaunchKernelGGL(k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, nq, qpb);
+    hipLaunchKernelGGL(k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, nq, qpb, acc);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(pool_bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, M, rows);
+  hipLaunchKernelGGL(pool_bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, M, rows, acc);
   return hipGetLastError();
 }
 
 hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                              int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                             const float* co, uint16_t* dx, hipStream_t s) {
+                             const float* co, uint16_t* dx, hipStream_t s, const BNBwdFin* bfp) {
   if (C % 8) return hipErrorInvalidValue;
+  const BNBwdFin f = bfp ? *bfp : kNoBwdFin;
+  if (f.acc && (!f.co || C > FIN_MAX_C)) return hipErrorInvalidValue;
+  const int cap = f.acc ? FIN_GRID_CAP : 8192;
+  const size_t lds = f.acc ? 3 * C * sizeof(float) : 0;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   const long n8 = (long)N * H * W * C / 8;
   if (quad_pool_geo(g)) {
     const long nq8 = (long)N * Ho * Wo * C / 8;
     auto k = g.pt ? (g.pl ? pool_bn_bwd_apply_q_k<1, 1> : pool_bn_bwd_apply_q_k<1, 0>)
                   : (g.pl ? pool_bn_bwd_apply_q_k<0, 1> : pool_bn_bwd_apply_q_k<0, 0>);
-    hipLaunchKernelGGL(k, dim3(grid_for(nq8)), dim3(NT), 0, s, dpool, arg, g, x, st, co, dx, nq8);
+    hipLaunchKernelGGL(k, dim3(grid_for(nq8, NT, cap)), dim3(NT), lds, s, dpool, arg, g, x, st, co, dx, nq8, f);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(pool_bn_bwd_apply_k, dim3(grid_for(n8)), dim3(NT), 0, s, dpool, arg, g, x, st, co, dx, n8);
+  hipLaunchKernelGGL(pool_bn_bwd_apply_k, dim3(grid_for(n8, NT, cap)), dim3(NT), lds, s, dpool, arg, g, x, st, co, dx,
+                     n8, f);
   return hipGetLastError();
 }
 

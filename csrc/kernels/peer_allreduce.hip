@@ -103,8 +103,11 @@ __device__ __forceinline__ float4 msg_add(float4 a, float4 b, bool i64) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
+// staged: the caller already wrote the message into own `in` and reads the result from own
+// `out` (the fused trainer's folded step): phases A and D are skipped, the flags alone
+// order the exchange (stream order covers the local side, see peer_comm.h)
 __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __restrict__ data, long n,
-                                                       long long* __restrict__ aux, long n64) {
+                                                       long long* __restrict__ aux, long n64, int staged) {
   const int b = blockIdx.x, t = threadIdx.x, W = a.world;
   const long chunk = a.chunk, shard = chunk * a.nblk;
   const unsigned e = a.epoch[b] + 1;
@@ -113,9 +116,11 @@ __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __rest
 
   // A: local message -> own `in` (chunk set b), zero beyond the message
   float4* in_own = reinterpret_cast<float4*>(a.in[a.rank]);
-  for (int s = 0; s < W; ++s) {
-    const long base = s * shard + (long)b * chunk;
-    for (long i = t; i < c4; i += NT) in_own[base / 4 + i] = msg_load(data, n, aux, n64, nfp, base + 4 * i);
+  if (!staged) {
+    for (int s = 0; s < W; ++s) {
+      const long base = s * shard + (long)b * chunk;
+      for (long i = t; i < c4; i += NT) in_own[base / 4 + i] = msg_load(data, n, aux, n64, nfp, base + 4 * i);
+    }
   }
   signal_all(a, 0, e);
   wait_all(a, 0, e);
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __rest
 
   // D: own `out` (chunk set b) -> local gradient
   const float4* out_own = reinterpret_cast<const float4*>(a.out[a.rank]);
-  for (int s = 0; s < W; ++s) {
+  for (int s = 0; s < W && !staged; ++s) {
     const long base = s * shard + (long)b * chunk;
     for (long i = t; i < c4; i += NT) msg_store(data, n, aux, n64, nfp, base + 4 * i, out_own[base / 4 + i]);
   }
@@ -157,7 +162,15 @@ hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, long lo
     return hipErrorInvalidValue;
   if ((long)a.world * a.nblk * a.chunk < (n + 3) / 4 * 4 + 2 * n64) return hipErrorInvalidValue;
   if (reinterpret_cast<uintptr_t>(data) % 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, data, n, aux64, n64);
+  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, data, n, aux64, n64, 0);
+  return hipGetLastError();
+}
+
+hipError_t peer_allreduce_staged_launch(const PeerArgs& a, long n, long n64, hipStream_t st) {
+  if (a.world < 1 || a.world > kPeerMaxRanks || a.nblk < 1 || a.nblk > kPeerMaxBlocks || a.chunk % 4)
+    return hipErrorInvalidValue;
+  if ((long)a.world * a.nblk * a.chunk < (n + 3) / 4 * 4 + 2 * n64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, nullptr, n, nullptr, n64, 1);
   return hipGetLastError();
 }
 

@@ -29,8 +29,9 @@ void register_kernel_ops(py::module_& m) {
       "gemm",
       [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,
          uintptr_t stats, uintptr_t R, int M, int N, int K, int lda, int ldb, int ldc, std::vector<int> geo, int kc,
-         int k_per_split, uintptr_t stream, int kstep) {
+         int k_per_split, uintptr_t stream, int kstep, uintptr_t stats_acc) {
         damd::GemmArgs a{};
+        a.stats_acc = P_<double>(stats_acc);
         a.A = P_<const void>(A);
         a.B = P_<const void>(B);
         a.C = P_<void>(C);
@@ -53,15 +54,17 @@ void register_kernel_ops(py::module_& m) {
       py::arg("amode"), py::arg("bmode"), py::arg("epi"), py::arg("splits"), py::arg("tile"), py::arg("A"),
       py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("stats"), py::arg("R"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
-      py::arg("stream"), py::arg("kstep") = 0);
+      py::arg("stream"), py::arg("kstep") = 0, py::arg("stats_acc") = 0);
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
   m.def("conv_gemm_kstep", &damd::conv_gemm_kstep);
   m.def("splitk_finish", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, uintptr_t R, int relu,
-                            uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream) {
+                            uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream, uintptr_t stats_acc) {
     check(damd::splitk_finish(P_<const float>(slab), splits, M, N, P_<const float>(bias), P_<const uint16_t>(R), relu,
-                              P_<float>(stats), rb, P_<uint16_t>(out), ldc, P_<ihipStream_t>(stream)),
+                              P_<float>(stats), rb, P_<uint16_t>(out), ldc, P_<ihipStream_t>(stream),
+                              P_<double>(stats_acc)),
           "splitk_finish");
-  });
+  }, py::arg("slab"), py::arg("splits"), py::arg("M"), py::arg("N"), py::arg("bias"), py::arg("R"), py::arg("relu"),
+     py::arg("stats"), py::arg("rb"), py::arg("out"), py::arg("ldc"), py::arg("stream"), py::arg("stats_acc") = 0);
   m.def("splitk_finish_f32", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, int relu, uintptr_t out,
                                 int ldc, uintptr_t stream) {
     check(damd::splitk_finish_f32(P_<const float>(slab), splits, M, N, P_<const float>(bias), relu, P_<float>(out),
@@ -101,6 +104,68 @@ void register_kernel_ops(py::module_& m) {
     check(damd::bn_bwd_apply(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
                              P_<const float>(co), P_<u16>(dx), M, C, P_<ihipStream_t>(s)),
           "bn_bwd_apply");
+  });
+  // ---- BatchNorm with the finalize in the consumer (layer_ops.h BNFin / BNBwdFin) ----
+  // fin = [acc, gamma, beta, st, rmean, rvar] pointers + [count, eps, momentum]
+  // bfin = [acc, dgamma, dbeta, co] pointers + count
+  auto mkfin = [](const std::vector<U>& p, const std::vector<float>& v) {
+    damd::BNFin f{};
+    if (p.empty()) return f;
+    if (p.size() != 6 || v.size() != 3) throw std::invalid_argument("fin: 6 pointers + [count, eps, momentum]");
+    f.acc = P_<const double>(p[0]); f.gamma = P_<const float>(p[1]); f.beta = P_<const float>(p[2]);
+    f.st = P_<float>(p[3]); f.rmean = P_<float>(p[4]); f.rvar = P_<float>(p[5]);
+    f.count = v[0]; f.eps = v[1]; f.mom = v[2];
+    return f;
+  };
+  auto mkbfin = [](const std::vector<U>& p, float count) {
+    damd::BNBwdFin f{};
+    if (p.size() != 4) throw std::invalid_argument("bfin: [acc, dgamma, dbeta, co]");
+    f.acc = P_<const double>(p[0]); f.dgamma = P_<float>(p[1]); f.dbeta = P_<float>(p[2]); f.co = P_<float>(p[3]);
+    f.count = count;
+    return f;
+  };
+  m.def("bn_apply_fin", [mkfin](U x, U r, int res_mode, int relu, U y, long M, int C, std::vector<U> p1,
+                                std::vector<float> v1, std::vector<U> p2, std::vector<float> v2, U s) {
+    const damd::BNFin a = mkfin(p1, v1), b = mkfin(p2, v2);
+    check(damd::bn_apply(P_<const u16>(x), a.st, P_<const u16>(r), b.st, res_mode, relu, P_<u16>(y), M, C,
+                         P_<ihipStream_t>(s), &a, &b),
+          "bn_apply_fin");
+  });
+  m.def("bn_bwd_reduce_acc", [](U dy, U y, int relu_mask, U x, U st, U dz, U acc, int T, long M, int C, U s) {
+    check(damd::bn_bwd_reduce(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
+                              P_<u16>(dz), nullptr, T, M, C, P_<ihipStream_t>(s), P_<double>(acc)),
+          "bn_bwd_reduce_acc");
+  });
+  m.def("bn_bwd_apply_fin", [mkbfin](U dy, U y, int relu_mask, U x, U st, U dx, long M, int C, std::vector<U> bp,
+                                     float count, U s) {
+    const damd::BNBwdFin f = mkbfin(bp, count);
+    check(damd::bn_bwd_apply(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
+                             f.co, P_<u16>(dx), M, C, P_<ihipStream_t>(s), &f),
+          "bn_bwd_apply_fin");
+  });
+  m.def("bn_relu_maxpool_fwd_fin", [mkfin](U x, std::vector<int> g, U y, U arg, std::vector<U> p, std::vector<float> v,
+                                           U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    const damd::BNFin f = mkfin(p, v);
+    check(damd::bn_relu_maxpool_fwd(P_<const u16>(x), f.st, g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8],
+                                    g[9], g[10], g[11], P_<u16>(y), P_<uint8_t>(arg), P_<ihipStream_t>(s), &f),
+          "bn_relu_maxpool_fwd_fin");
+  });
+  m.def("pool_bn_bwd_reduce_acc", [](U dpool, U arg, std::vector<int> g, U x, U st, U acc, int T, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    check(damd::pool_bn_bwd_reduce(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
+                                   g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st),
+                                   nullptr, T, P_<ihipStream_t>(s), P_<double>(acc)),
+          "pool_bn_bwd_reduce_acc");
+  });
+  m.def("pool_bn_bwd_apply_fin", [mkbfin](U dpool, U arg, std::vector<int> g, U x, U st, U dx, std::vector<U> bp,
+                                          float count, U s) {
+    if (g.size() != 12) throw std::invalid_argument("pool geometry");
+    const damd::BNBwdFin f = mkbfin(bp, count);
+    check(damd::pool_bn_bwd_apply(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
+                                  g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st), f.co,
+                                  P_<u16>(dx), P_<ihipStream_t>(s), &f),
+          "pool_bn_bwd_apply_fin");
   });
   m.def("maxpool_fwd", [](U x, std::vector<int> g, U y, U arg, U s) {
     if (g.size() != 12) throw std::invalid_argument("pool geometry");
@@ -208,11 +273,14 @@ void register_kernel_ops(py::module_& m) {
           "opt_step");
   });
   m.def("gather_batch", [](U x, int x_u8, float scale, U labels, U ctrl, int per, int HW, int Cin, int Cp, U xb, U yb,
-                           U s) {
+                           U s, U zero, long nzero) {
     check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<damd::Ctrl>(ctrl),
-                             per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s)),
+                             per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s), P_<double>(zero),
+                             nzero),
           "gather_batch");
-  });
+  }, py::arg("x"), py::arg("x_u8"), py::arg("scale"), py::arg("labels"), py::arg("ctrl"), py::arg("per"),
+     py::arg("HW"), py::arg("Cin"), py::arg("Cp"), py::arg("xb"), py::arg("yb"), py::arg("s"), py::arg("zero") = 0,
+     py::arg("nzero") = 0);
   m.def("pad_cast", [](U src, int R, int C1, int C2, int C1p, int C2p, U dst, U s) {
     check(damd::pad_cast(P_<const float>(src), R, C1, C2, C1p, C2p, P_<u16>(dst), P_<ihipStream_t>(s)), "pad_cast");
   });

@@ -116,6 +116,16 @@ void PeerAllreduce::allreduce(float* data, long n, hipStream_t st, long long* au
   HIP_CHECK(peer_allreduce_launch(a_, data, n, aux64, n64, st));
 }
 
+void PeerAllreduce::allreduce_staged(long n, long n64, hipStream_t st) {
+  if (!opened_) throw std::runtime_error("peer all-reduce: open() the peers' handles first");
+  if (n64 < 0 || message_words(n, n64) > cap_) throw std::invalid_argument("peer all-reduce: bad staged message");
+  if (a_.world == 1) {  // the result is the input
+    HIP_CHECK(hipMemcpyAsync(out_, in_, (size_t)message_words(n, n64) * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  HIP_CHECK(peer_allreduce_staged_launch(a_, n, n64, st));
+}
+
 unsigned PeerAllreduce::status() const {
   unsigned s = 0;
   HIP_CHECK(hipMemcpy(&s, a_.status, sizeof(s), hipMemcpyDeviceToHost));

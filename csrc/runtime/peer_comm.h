@@ -54,6 +54,8 @@ struct PeerArgs {
 // `aux64` (fixed-point accumulators, summed exactly as integers) starting at the next
 // 16-byte word boundary; every rank ends with the same bits.
 hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, long long* aux64, long n64, hipStream_t st);
+// staged: the message is already in `in` of this rank, the result stays in `out`
+hipError_t peer_allreduce_staged_launch(const PeerArgs& a, long n, long n64, hipStream_t st);
 
 class PeerAllreduce {
  public:
@@ -73,6 +75,14 @@ class PeerAllreduce {
   // in-place SUM all-reduce of n fp32 values at `data` (and n64 int64 values at `aux64`)
   // on `st` (capturable)
   void allreduce(float* data, long n, hipStream_t st, long long* aux64 = nullptr, long n64 = 0);
+  // the same exchange for a message the caller has already written into this rank's `in`
+  // staging (n fp32 words, then the int64 segment at the next 16-byte word); the result is
+  // left in `out` (same layout) -- no copy-in / copy-out passes.  The caller writes `in`
+  // only after this call's previous instance completed on its stream and reads `out` only
+  // after this one did (stream order), which is what keeps the buffer reuse safe.
+  void allreduce_staged(long n, long n64, hipStream_t st);
+  float* in_local() const { return in_; }
+  float* out_local() const { return out_; }
   // message words (fp32 slots) of a call with n floats and n64 int64 values
   static long message_words(long n, long n64) { return (n + 3) / 4 * 4 + 2 * n64; }
   // 0 = every wait so far completed; otherwise a wait timed out (peer missing / wedged)

@@ -128,6 +128,12 @@ class NativeGraphEngine(Engine):
                  "AveragePooling2D", "GlobalAveragePooling2D", "Flatten", "Dense", "Dropout")
     ACTIVATIONS = ("linear", "relu", "sigmoid", "tanh")
     _weights_static = False  # True for an inference plan: padded weight copies made once per call
+    # DAMD_BN_FIN=1: BatchNorm statistics through fp64 accumulators finalized inside the
+    # consumer kernels (ops/hip.py BNFin): 40 fewer launches per ResNet-18 step, but every
+    # producer block adds into the same 2C addresses, and those same-address fp64 atomics
+    # serialise at the memory side (bn_bwd_reduce 8 -> 27 us): measured 3.13 vs 2.80
+    # ms/step, so the per-block partials + finalize kernels stay the default
+    _bn_fin = True
 
     @staticmethod
     def eligible(model, strategy):
@@ -500,6 +506,7 @@ class NativeGraphEngine(Engine):
                         nd.attrs["b_pad"] = torch.zeros(up, dtype=torch.float32, device=dev)
                 if _act_name(l) != "linear":
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
+        self._plan_bn_fin()
         # one scratch bf16 buffer for "second writer" gradient accumulation
         big = max([int(np.prod(t.shape)) for t in self._all_tensors()] + [1])
         self.scratch = torch.zeros(big, dtype=torch.bfloat16, device=dev)
@@ -508,6 +515,35 @@ class NativeGraphEngine(Engine):
         self.gemm_ws = torch.zeros(max(ws, 4), dtype=torch.float32, device=dev)
         nbytes += self.gemm_ws.numel() * 4
         self.act_bytes = nbytes
+
+    def _plan_bn_fin(self):
+        """fp64 statistics accumulators of every BatchNorm ([2][C] forward sums, [2][C]
+        backward sums) in one buffer, cleared by the step's gather_batch launch; the conv
+        producing a BN input accumulates into it from its epilogue."""
+        bns = [nd for nd in self.nodes if nd.kind == "BatchNormalization" and not nd.attrs.get("dead")]
+        use = (self._bn_fin and env.get_bool("DAMD_BN_FIN", False)
+               and all(nd.out.shape[-1] <= H.FIN_MAX_C for nd in bns))
+        self.bn_acc = None
+        if not use or not bns:
+            return
+        tot = sum(4 * nd.out.shape[-1] for nd in bns)
+        self.bn_acc = torch.zeros(tot, dtype=torch.float64, device=self.device)
+        o = 0
+        for nd in bns:
+            C = nd.out.shape[-1]
+            nd.attrs["acc_f"] = self.bn_acc[o:o + 2 * C]
+            nd.attrs["acc_b"] = self.bn_acc[o + 2 * C:o + 4 * C]
+            o += 4 * C
+            if nd.attrs.get("stats_from_conv"):
+                self._producer(nd.inputs[0]).attrs["stats_buf"] = nd.attrs["acc_f"]
+            l = nd.layer
+            M = int(np.prod(nd.inputs[0].shape[:-1]))
+            nd.attrs["fin"] = H.BNFin(nd.attrs["acc_f"], self._view_or_none(l.gamma), self._view_or_none(l.beta),
+                                      nd.attrs["st"], l.moving_mean.value, l.moving_variance.value, M, l.epsilon,
+                                      l.momentum)
+
+    def _view_or_none(self, var):
+        return self.views[id(var)] if var is not None else None
 
     # --- gradient buckets (all-reduce overlapped with the rest of backward) ------------------
     def _plan_buckets(self, bucket_mb: float):
@@ -700,8 +736,10 @@ class NativeGraphEngine(Engine):
         self._mark("start")
         h, w, c = self.in_shape
         self.G.zero_()
+        acc = self.bn_acc
         C.gather_batch(self.x_ep.data_ptr(), int(self.feed.x_u8), 255.0, self.y_ep.data_ptr(), self.ctrl.data_ptr(),
-                       B, h * w, c, self.cin_pad, self.x0.buf.data_ptr(), self.labels.data_ptr(), s)
+                       B, h * w, c, self.cin_pad, self.x0.buf.data_ptr(), self.labels.data_ptr(), s,
+                       zero=acc.data_ptr() if acc is not None else 0, nzero=acc.numel() if acc is not None else 0)
         live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
         for nd in live:
             getattr(self, "_fwd_" + nd.kind)(nd)
@@ -793,6 +831,15 @@ class NativeGraphEngine(Engine):
         st = nd.attrs["st"]
         gamma = self.views[id(l.gamma)] if l.gamma is not None else None
         beta = self.views[id(l.beta)] if l.beta is not None else None
+        fin = nd.attrs.get("fin")
+        if fin is not None:
+            if not nd.attrs.get("stats_from_conv"):  # sum / sum of squares of x into acc_f
+                self.C.bn_bwd_reduce_acc(x.buf.data_ptr(), 0, 0, x.buf.data_ptr(), self._ident(C).data_ptr(), 0,
+                                         nd.attrs["acc_f"].data_ptr(), nd.attrs["T"], M, C, H.stream_handle())
+            if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None:
+                return  # finalized and applied by the fused Add / MaxPool that consumes it
+            H.bn_apply_fin(x.buf, nd.out.root().buf, fin, relu=nd.attrs.get("relu", False))
+            return
         if nd.attrs.get("stats_from_conv"):
             part = self._producer(x).attrs["stats_buf"]
             Tn = part.shape[0]
@@ -837,11 +884,19 @@ class NativeGraphEngine(Engine):
             r, st2 = other.root().buf, None
         else:
             r, st2 = other.inputs[0].root().buf, other.attrs["st"]
+        if main.attrs.get("fin") is not None:
+            H.bn_apply_fin(x.buf, nd.out.root().buf, main.attrs["fin"], relu=nd.attrs.get("relu", False), r=r,
+                           fin2=other.attrs["fin"] if mode == "bn" else None)
+            return
         H.bn_apply(x.buf, main.attrs["st"], nd.out.root().buf, relu=nd.attrs.get("relu", False), r=r, st2=st2)
 
     def _fwd_MaxPooling2D(self, nd):
         l = nd.layer
         bn = nd.attrs.get("bn")
+        if bn is not None and bn.attrs.get("fin") is not None:
+            H.bn_relu_maxpool_fwd_fin(bn.inputs[0].root().buf, nd.out.root().buf, nd.attrs["arg"], l.pool_size,
+                                      l.strides, l.padding, bn.attrs["fin"])
+            return
         if bn is not None:  # stem fusion: pool(relu(BN(x))) straight from the conv output
             H.bn_relu_maxpool_fwd(bn.inputs[0].root().buf, bn.attrs["st"], nd.out.root().buf, nd.attrs["arg"],
                                   l.pool_size, l.strides, l.padding)
@@ -928,12 +983,20 @@ class NativeGraphEngine(Engine):
         st, part, co, Tn = bn.attrs["st"], bn.attrs["part"], bn.attrs["co"], bn.attrs["T"]
         ym = ymask.data_ptr() if relu else 0
         mode = (2 if mask_from_x else 1) if relu else 0
+        dx, fin = self._grad_target(x)
+        if bn.attrs.get("fin") is not None and dx is not None:
+            H.bn_bwd_fin(dy, ymask if relu else None, mode, x.buf, st, bn.attrs["acc_b"], co, dx,
+                         dgamma=self.gviews[id(l.gamma)] if l.gamma is not None else None,
+                         dbeta=self.gviews[id(l.beta)] if l.beta is not None else None,
+                         dz_out=dz_out if relu else None)
+            if fin:
+                fin()
+            return
         C_.bn_bwd_reduce(dy.data_ptr(), ym, mode, x.buf.data_ptr(), st.data_ptr(),
                          dz_out.data_ptr() if (dz_out is not None and relu) else 0, part.data_ptr(), Tn, M, C, s)
         C_.bn_bwd_finalize(part.data_ptr(), Tn, C, float(M), st.data_ptr(), 0,
                            self.gviews[id(l.gamma)].data_ptr() if l.gamma is not None else 0,
                            self.gviews[id(l.beta)].data_ptr() if l.beta is not None else 0, co.data_ptr(), s)
-        dx, fin = self._grad_target(x)
         if dx is not None:
             C_.bn_bwd_apply(dy.data_ptr(), ym, mode, x.buf.data_ptr(), st.data_ptr(), co.data_ptr(),
                             dx.data_ptr(), M, C, s)
@@ -1011,12 +1074,9 @@ class NativeGraphEngine(Engine):
             if fin:
                 fin()
         else:
-            g = dy
-            if relu:
-                g = self.scratch2[: M * C].view(out.shape)
-                H.relu_bwd(dy, out.buf, g)
-            self._bn_backward(main, g, out.buf, False)
-            self._bn_backward(other, g, out.buf, False)
+            # both BN backwards mask dy by [out > 0] themselves (no separate ReLU-backward pass)
+            self._bn_backward(main, dy, out.buf, relu)
+            self._bn_backward(other, dy, out.buf, relu)
 
     def _bwd_MaxPooling2D(self, nd):
         l = nd.layer
@@ -1025,6 +1085,14 @@ class NativeGraphEngine(Engine):
             x = bn.inputs[0].root()
             bl = bn.layer
             dx, fin = self._grad_target(x)
+            if bn.attrs.get("fin") is not None and dx is not None:
+                H.pool_bn_bwd_fin(nd.out.root().grad, nd.attrs["arg"], x.buf, bn.attrs["st"], bn.attrs["acc_b"],
+                                  bn.attrs["co"], dx, l.pool_size, l.strides, l.padding,
+                                  dgamma=self.gviews[id(bl.gamma)] if bl.gamma is not None else None,
+                                  dbeta=self.gviews[id(bl.beta)] if bl.beta is not None else None)
+                if fin:
+                    fin()
+                return
             H.pool_bn_bwd(nd.out.root().grad, nd.attrs["arg"], x.buf, bn.attrs["st"], bn.attrs["part"],
                           bn.attrs["co"], dx, l.pool_size, l.strides, l.padding,
                           dgamma=self.gviews[id(bl.gamma)] if bl.gamma is not None else None,

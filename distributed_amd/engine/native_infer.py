@@ -34,6 +34,7 @@ from .native_graph import C_AL, C_AC, C_AN, C_CUR, C_GB, C_NS, C_ROW0, C_WRAP, N
 class NativeInference(NativeGraphEngine):
     name = "native_infer"
     _weights_static = True
+    _bn_fin = False  # BN runs from the moving statistics (bn_infer_st)
 
     @staticmethod
     def eligible(model, device, evaluate: bool = False) -> Tuple[bool, str]:

@@ -245,12 +245,24 @@ def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
     _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle())
 
 
+def _stats_ptrs(stats):
+    """(partials pointer, fp64 accumulator pointer) of a stats argument: an fp32 [T][2][N]
+    partials tensor, or an fp64 [2][N] accumulator (BNFin: producers add, the consumer
+    finalizes)."""
+    if stats is None:
+        return 0, 0
+    if stats.dtype == torch.float64:
+        return 0, _ptr(stats)
+    return _ptr(stats), 0
+
+
 def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
          geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0):
     t = pick_tile(N) if tile is None else tile
     kps = k_per_split if k_per_split is not None else -(-K // BK) * BK
-    _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), _ptr(stats), _ptr(R), M, N, K,
-              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep)
+    sp, sa = _stats_ptrs(stats)
+    _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), sp, _ptr(R), M, N, K,
+              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep, stats_acc=sa)
 
 
 # ---- dense -------------------------------------------------------------------------------
@@ -386,8 +398,7 @@ def conv_fwd_stem4(x, w8, out, kernel_size, strides=(2, 2), padding="same", bias
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, wshape, strides, padding)
     assert tuple(out.shape) == (n, ho, wo, cout)
     plan = conv_fwd_plan(x.shape, wshape, strides, padding)
-    if stats is not None and stats.shape[0] != plan["stats_T"]:
-        raise ValueError(f"conv_fwd_stem4: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
+    _check_stats(stats, plan, cout, "conv_fwd_stem4")
     M, K = plan["M"], plan["K"]
     geo = (h, wd, 4, ho, wo, kh, 8, s, pad)
     if plan["splits"] == 1:
@@ -399,8 +410,19 @@ def conv_fwd_stem4(x, w8, out, kernel_size, strides=(2, 2), padding="same", bias
     ws = _workspace(workspace, plan["ws"], x.device)
     gemm(x, w8, ws, amode=A_CONV64, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=32)
-    _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), _ptr(stats), FINISH_RB,
-                       _ptr(out), cout, stream_handle())
+    sp, sa = _stats_ptrs(stats)
+    _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), sp, FINISH_RB,
+                       _ptr(out), cout, stream_handle(), stats_acc=sa)
+
+
+def _check_stats(stats, plan, cout, who):
+    if stats is None:
+        return
+    if stats.dtype == torch.float64:
+        if stats.numel() != 2 * cout:
+            raise ValueError(f"{who}: an fp64 statistics accumulator has 2 x {cout} elements, got {stats.numel()}")
+    elif stats.shape[0] != plan["stats_T"]:
+        raise ValueError(f"{who}: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
 
 
 def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
@@ -463,8 +485,7 @@ def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, 
     assert tuple(out.shape) == (n, ho, wo, cout)
     plan = conv_fwd_plan(x.shape, w.shape, strides, padding)
     M, K = plan["M"], plan["K"]
-    if stats is not None and stats.shape[0] != plan["stats_T"]:
-        raise ValueError(f"conv_fwd: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
+    _check_stats(stats, plan, cout, "conv_fwd")
     geo = (h, wd, cin, ho, wo, kh, kw, s, pad)
     if plan["splits"] == 1:
         epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | \
@@ -475,8 +496,9 @@ def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, 
     ws = _workspace(workspace, plan["ws"], x.device)
     gemm(x, w, ws, amode=plan["amode"], bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo)
-    _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), _ptr(stats), FINISH_RB,
-                       _ptr(out), cout, stream_handle())
+    sp, sa = _stats_ptrs(stats)
+    _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), sp, FINISH_RB,
+                       _ptr(out), cout, stream_handle(), stats_acc=sa)
 
 
 def _workspace(ws, need, device):
@@ -622,6 +644,73 @@ def pool_bn_bwd(dpool, arg, x, st, part, co, dx, pool, strides, padding, dgamma=
     _C().bn_bwd_finalize(_ptr(part), T, C, float(M), _ptr(st), 0, _ptr(dgamma), _ptr(dbeta), _ptr(co), s)
     if dx is not None:
         _C().pool_bn_bwd_apply(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(co), _ptr(dx), s)
+
+
+# ---- BatchNorm with the finalize folded into the consumer kernel (layer_ops.h BNFin) ------
+# The producers (conv / dense GEMM epilogue with an fp64 `stats` tensor, split-K finish,
+# bn_bwd_reduce with `acc`) add their per-block partials into an fp64 [2][C] accumulator;
+# the consumer derives the coefficients in its prologue, so neither bn_finalize nor
+# bn_bwd_finalize is launched.  The accumulators must be zero before the producers run
+# (the native graph engine clears them all in the step's gather_batch launch).
+FIN_MAX_C = 4096
+
+
+class BNFin:
+    """Forward finalize parameters of one BatchNorm: fp64 accumulator acc [2][C] (sum,
+    sum of squares of the BN input), gamma / beta (None: 1 / 0), st [4][C] written by the
+    consumer's block 0 (mean, invstd, scale, shift), moving statistics (None: not
+    updated), the element count per channel, epsilon and the moving-average momentum."""
+
+    def __init__(self, acc, gamma, beta, st, rmean, rvar, count, eps, momentum):
+        self.acc, self.st = acc, st
+        self._p = [_ptr(acc), _ptr(gamma), _ptr(beta), _ptr(st), _ptr(rmean), _ptr(rvar)]
+        self._v = [float(count), float(eps), float(momentum)]
+
+    def args(self):
+        return self._p, self._v
+
+
+_NOFIN = ([], [])
+
+
+def bn_apply_fin(x, y, fin: BNFin, relu=False, r=None, fin2: Optional[BNFin] = None):
+    """bn_apply with its statistics finalized in the kernel: y = act(BN(x) [+ r | + BN2(r)])."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    mode = 0 if r is None else (1 if fin2 is None else 2)
+    p1, v1 = fin.args()
+    p2, v2 = fin2.args() if fin2 is not None else _NOFIN
+    _C().bn_apply_fin(_ptr(x), _ptr(r), mode, int(relu), _ptr(y), M, C, p1, v1, p2, v2, stream_handle())
+
+
+def bn_bwd_fin(dy, y, relu_mask, x, st, acc, co, dx, dgamma=None, dbeta=None, dz_out=None):
+    """BN backward in two launches: bn_bwd_reduce adds sum(dz), sum(dz * xhat) into the fp64
+    accumulator acc [2][C]; bn_bwd_apply derives co, adds dgamma / dbeta (block 0) and
+    writes dx."""
+    C = x.shape[-1]
+    M = x.numel() // C
+    T = _C().bn_bwd_blocks(M, C)
+    s = stream_handle()
+    _C().bn_bwd_reduce_acc(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dz_out), _ptr(acc), T, M, C, s)
+    _C().bn_bwd_apply_fin(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dx), M, C,
+                          [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s)
+
+
+def bn_relu_maxpool_fwd_fin(x, y, arg, pool, strides, padding, fin: BNFin):
+    g = pool_geo(x.shape, pool, strides, padding)
+    p, v = fin.args()
+    _C().bn_relu_maxpool_fwd_fin(_ptr(x), g, _ptr(y), _ptr(arg), p, v, stream_handle())
+
+
+def pool_bn_bwd_fin(dpool, arg, x, st, acc, co, dx, pool, strides, padding, dgamma=None, dbeta=None):
+    g = pool_geo(x.shape, pool, strides, padding)
+    C = x.shape[-1]
+    M = x.numel() // C
+    T = _C().bn_bwd_blocks(M, C)
+    s = stream_handle()
+    _C().pool_bn_bwd_reduce_acc(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(acc), T, s)
+    _C().pool_bn_bwd_apply_fin(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(dx),
+                               [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s)
 
 
 def gap_fwd(x, y):

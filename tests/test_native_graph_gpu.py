@@ -344,6 +344,24 @@ def test_stem_fusion_matches_unfused():
     np.testing.assert_allclose(hf["loss"], hu["loss"], rtol=1e-6)
 
 
+def test_bn_fin_matches_partials_finalize():
+    """BatchNorm statistics through fp64 accumulators finalized in the consumer kernels
+    (DAMD_BN_FIN=1: no bn_finalize / bn_bwd_finalize launches) == per-block partials +
+    the finalize kernels (default): two momentum steps, every weight incl. the moving
+    statistics, and the loss."""
+    x, y = _data(128, (32, 32, 3), 10, seed=8)
+    tf.keras.backend.clear_session()
+    init = _small_resnet().get_weights()
+    wa, ha, ea = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9,
+                        extra_env={"DAMD_BN_FIN": "1"})
+    wb, hb, eb = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9,
+                        extra_env={"DAMD_BN_FIN": "0"})
+    assert ea == eb == "native_graph"
+    for a, b in zip(wa, wb):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-5)
+
+
 def test_resnet18_full_size_trains():
     x, y = _data(64, (224, 224, 3), 1000, seed=3)
     tf.keras.backend.clear_session()
