@@ -104,12 +104,11 @@ def main():
     if args.graph_steps:
         os.environ["DAMD_GRAPH_STEPS"] = str(args.graph_steps)
     elif "DAMD_GRAPH_STEPS" not in os.environ and args.steps > 0:
-        # replayed graph length: every replay boundary costs ~4.5 us (scripts/probe_overhead.py:
-        # 23.97 us/step with 5-step graphs, 23.07 with 20-step graphs at k = 2000), so a short
-        # timed run is ONE replay of a graph of all its steps (the warmup runs its steps
-        # eagerly); long runs replay a common divisor of the warmup and timed counts
+        # replayed graph length: a common divisor of the warmup and timed step counts, so the
+        # warmup already replays the very graph the timed loop replays (its first launch
+        # pays one-time costs) -- e.g. 5 for --steps 20 --warmup 5
         g = math.gcd(args.steps, args.warmup)
-        os.environ["DAMD_GRAPH_STEPS"] = str(args.steps if args.steps <= 200 else (g if g >= 20 else 200))
+        os.environ["DAMD_GRAPH_STEPS"] = str(g if g >= 5 else min(args.steps, 20))
 
     import numpy as np
     import torch
@@ -169,14 +168,8 @@ def main():
     fail_at = runtime.fault_injection_step()  # DAMD_FAIL_AT=rank:step (launcher / gang tests)
     if fail_at is not None and fail_at <= args.warmup:
         raise RuntimeError(f"injected failure on rank {rt.rank} at step {fail_at} (DAMD_FAIL_AT)")
-    # build the replayed HIP graph(s) first: capture is setup, not part of a timed step.
-    # The fused engine's timed run ends in the flush of the last deferred SGD update: its
-    # last replay is a graph captured with that flush as its tail (one launch less)
-    fused = engine.name == "fused_convnet"
-    if fused:
-        engine.prepare(max(args.steps, args.warmup), flush=True)
-    else:
-        engine.prepare(max(args.steps, args.warmup))
+    # build the replayed HIP graph(s) first: capture is setup, not part of a timed step
+    engine.prepare(max(args.steps, args.warmup))
     run(args.warmup)
     engine.sync()
     comm = strategy.communicator
@@ -193,10 +186,9 @@ def main():
     barrier()
     device_sync()
     t0 = time.perf_counter()
-    if fused:
-        engine.run(args.steps, flush=True)  # the last deferred SGD update is part of the timed work
-    else:
-        run(args.steps)
+    run(args.steps)
+    if engine.name == "fused_convnet":
+        engine._flush()  # the last deferred SGD update is part of the timed work
     if not on_gpu:
         engine.sync()
     # on the GPU the device-wide synchronize waits for every stream, the engines' own

@@ -148,7 +148,6 @@ class ConvNetTrainer : public StepExecutor {
   int batch() const { return B_; }
 
  protected:
-  void enqueue_tail() override { flush(); }
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     if (b_.kernels == 2) HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
@@ -266,9 +265,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("folded", &ConvNetTrainer::folded)
       .def("metric_tail", &ConvNetTrainer::metric_tail)
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
-      .def("capture", &ConvNetTrainer::capture, py::arg("k"), py::arg("tail") = false)
-      .def("launch_graph", &ConvNetTrainer::launch_graph, py::arg("k"), py::arg("tail") = false)
-      .def("run", &ConvNetTrainer::run, py::arg("k"), py::arg("tail") = false, py::call_guard<py::gil_scoped_release>())
+      .def("capture", &ConvNetTrainer::capture)
+      .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
       .def("run_persistent", &ConvNetTrainer::run_persistent, py::arg("steps"), py::arg("timeout_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
       .def("phase_times", &ConvNetTrainer::phase_times, py::arg("steps"), py::call_guard<py::gil_scoped_release>())

@@ -61,9 +61,7 @@ struct Ctrl {
                             //    cleared by flush: the first step after a flush applies none)
   int   par2;               // 19 step parity as seen by the 2nd kernel of a 2-launch step (set by the 1st)
   int   pad[12];              // 20 pad[0]: persistent kernel's global step (buffer rotation / barrier
-                              //    targets); 21 pad[1]: its error word (a grid wait timed out);
-                              // 22 pad[2]: dry replay -- the 2-launch step's kernels return at
-                              //    once (a captured graph's first replay warmed without a step)
+                              //    targets); 21 pad[1]: its error word (a grid wait timed out)
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

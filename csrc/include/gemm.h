@@ -11,7 +11,9 @@ enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4,
                  // weight gradient over "virtual rows" (conv_gemm.hip): K = virtual rows
                  A_WGRAD64 = 7,
                  // conv_wgrad3.hip: direct 3x3/s1/p1 weight gradient (all taps per block)
-                 A_WGRAD3 = 8 };
+                 A_WGRAD3 = 8,
+                 // conv3x3.hip: direct 3x3/s1/p1 forward / backprop-input (input halo in LDS)
+                 A_CONV3 = 9, A_DGRAD3 = 10 };
 enum GemmBMode { B_NC = 0, B_KC = 1 };
 // E_SLAB: split-K partial of split z stored (plain fp32 stores) to C + z * M * ldc; a
 // deterministic splitk_reduce then adds the slabs into the destination in fixed order.
@@ -46,6 +48,10 @@ int wgrad64_rows(int N, int Ho, int Wo, int kstep);
 // A_WGRAD3: K = wgrad3_rows (q space), k_per_split a multiple of 32, tiles 64x64 x 9 taps
 hipError_t wgrad3_launch(const GemmArgs& a, int epi, int splits, hipStream_t s);
 int wgrad3_rows(int N, int H, int W);
+// A_CONV3 / A_DGRAD3: tile 1 -> BN 64 (256 x 64), 0 -> BN 128 (128 x 128); output rows per
+// block for an H x W image (0: not supported); stats partials = Nimg * ceil(H / rows)
+hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream_t s);
+int conv3_rows(int H, int W, int bn);
 int wgrad64_rows_per_step(int Wo, int kstep);
 // k-step depth of those kernels (32 or 64, env DAMD_CONV_KB): the gathered channel count
 // must be a multiple of it for A_CONV64 / A_DGRAD64

@@ -1,0 +1,255 @@
+// Direct 3x3 / stride-1 / pad-1 convolution on MFMA with the input halo resident in LDS
+// (gfx950 / MI355X): the ResNet-18 layer-1 / layer-2 convolutions,
+// forward and backprop-input.
+//
+//   forward:         y[n][oh][ow][co] = sum_{kh,kw,ci} x[n][oh+kh-1][ow+kw-1][ci] W[kh][kw][ci][co]
+//   backprop-input:  dx[n][ih][iw][ci] = sum_{kh,kw,co} dy[n][ih+1-kh][iw+1-kw][co] W[kh][kw][ci][co]
+//                    (the same convolution of dy with the flipped taps)
+//
+// Why (rocprofv3 PMC, scripts/pmc_l2.sh): the implicit-GEMM conv kernels (conv_gemm.hip)
+// stage one filter tap per k-step, so every input pixel crosses L2 -> LDS nine times:
+// ~300 MB of L2 -> LDS traffic for a 25 MB layer-1 activation, 86-90 % L2 hits, ~10 TB/s
+// achieved -- the kernels are bound by the LDS fill rate, not by the MFMAs (16-22 % of
+// peak).  Here a block owns R whole output rows of one image and stages the (R+2) x (W+2)
+// input halo of a 64-channel chunk ONCE; the nine taps read shifted windows of it, and only
+// the weights stream through the LDS ring (one 64 x BN tile per tap and chunk).  A-side
+// traffic drops ~9x (layer 1: BN = 64 tile, 256 output pixels per block).
+//
+// LDS images (all filled by LDS-DMA, swizzle applied to the source address, rule 21):
+//   halo [pixel q][64 ch] bf16, 128 B per pixel; 16-byte chunk c of pixel q at slot
+//     c ^ (q & 7): the 16 lanes of a fragment read (16 consecutive output pixels = 16
+//     consecutive halo pixels at any tap) hit 8 distinct 16-B bank groups per 8 lanes;
+//   weights: forward [64 k][BN] (mn-contiguous, tile::frag_mc transpose reads), backprop-
+//     input [BN rows][64 k] (k-contiguous, as conv_gemm.hip's DGRAD operand).
+// Tile: 256 threads = 4 waves, BN = 64 -> 256 x 64 (4 x 1 waves), BN = 128 -> 128 x 128
+// (2 x 2), each wave 64 x 64 as 4 x 4 v_mfma_f32_16x16x32_bf16.  Rows of the tile beyond
+// the block's R x W pixels read a clamped halo pixel and are masked in the epilogue.
+// Epilogue: tile::epilogue (bias / residual add / BN statistics per tile / ReLU / bf16).
+#include "damd_common.h"
+#include "gemm.h"
+#include "gemm_tile.h"
+
+namespace damd {
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __attribute__((aligned(64))) uint4 g_zero16_c3[4];
+
+using tile::glds16;
+
+// k-contiguous [rows][64] image swizzle (conv_gemm.hip kc_swz<64>)
+__device__ __forceinline__ int kc64_swz(int r) { return r & 7; }
+
+template <int STAGES, int NQ, class Issue, class Compute>
+__device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute) {
+  constexpr int NK = 9;
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s) issue(s, s);
+  for (int kt = 0; kt < NK; ++kt) {
+    const int ahead = min(NK - 1 - kt, STAGES - 2);
+    if constexpr (STAGES >= 4) {
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQ) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (STAGES == 3) {
+      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + STAGES - 1 < NK) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
+    compute(kt % STAGES, kt);
+  }
+}
+
+// GemmArgs: A = gathered tensor (x, or dy for DGRAD) [Nimg][H][W][Cin] bf16, B = weights
+// [3][3][.][.] bf16, C = output [Nimg][H][W][N]; M = Nimg*H*W; Cin = gathered channels
+// (% 64), N = output channels (% BN); H, W the (shared) image size.  R output rows per
+// block, tpi = ceil(H / R) row blocks per image; grid (N / BN, Nimg * tpi).
+template <int BN, bool DGRAD, int EPI, int STAGES>
+__global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi) {
+  constexpr int WN = BN / 64, WM = 4 / WN, BM = WM * 64;
+  constexpr int B_ST = BN * 64 * 2;
+  constexpr int NB = B_ST / 4096;  // weight DMA instructions per wave per stage
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int H = a.H, W = a.W, SC = a.Cin, N = a.N;
+  const int HW = W + 2;
+  const int hpix = (R + 2) * HW;
+  const int halo_bytes = (hpix * 128 + 1023) & ~1023;
+  char* halo = smem;
+  char* ring = smem + halo_bytes;
+
+  const int tn = blockIdx.x, tm = blockIdx.y;
+  const int img = tm / tpi, oh0 = (tm - img * tpi) * R;
+  const int reff = min(R, H - oh0);
+  const int npx = reff * W;  // valid output pixels of this block
+  const int n0 = tn * BN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const uint16_t* src = (const uint16_t*)a.A;
+  const uint16_t* wsrc = (const uint16_t*)a.B;
+  const void* zero = tile::pinned_addr(g_zero16_c3);
+
+  // halo pixel of output pixel p (row-major over the block's R x W) at tap offset 0
+  int hbase[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = min(wm * 64 + i * 16 + (lane & 15), npx - 1);
+    const int r = p / W, c = p - r * W;
+    hbase[i] = r * HW + c;
+  }
+  // weight DMA: forward rows k of BN*2 bytes (CPR chunks, RPI k-rows per 1-KB instruction);
+  // backprop-input rows n of 64 k (8 chunks, 8 rows per instruction)
+  constexpr int CPR = BN / 8, RPI = 64 / CPR;
+  const int ca = (lane & 7) ^ kc64_swz(lane >> 3);
+  const uint16_t* brow[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int q = wave + 4 * j;
+    if constexpr (DGRAD) {
+      const int n = n0 + 8 * q + (lane >> 3);  // row of the [BN][64] image
+      brow[j] = wsrc + (long)n * a.kc + 8 * ca;
+    } else {
+      const int kr = q * RPI + lane / CPR;
+      const int ch = (lane % CPR) ^ tile::mc_swz<BN>(kr);
+      brow[j] = wsrc + (long)kr * N + n0 + 8 * ch;
+    }
+  }
+  // halo DMA: instruction j covers halo pixels 8j .. 8j+7 (lane / 8), slot lane & 7
+  const int nhi = halo_bytes / 1024;
+  const uint16_t* img_base = src + (long)img * H * W * SC;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = SC / 64;
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    const int c0 = chunk * 64;
+    if (chunk) {  // every wave is done with the previous halo and weight stages
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    for (int j = wave; j < nhi; j += 4) {
+      const int q = 8 * j + (lane >> 3);
+      const int hr = q / HW, hc = q - hr * HW;
+      const int ih = oh0 - 1 + hr, iw = hc - 1;
+      const bool ok = q < hpix && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      const int cs = (lane & 7) ^ (q & 7);
+      glds16(ok ? (const void*)(img_base + ((long)ih * W + iw) * SC + c0 + 8 * cs) : zero, halo + j * 1024);
+    }
+    auto issue = [&](int stage, int tap) __attribute__((always_inline)) {
+      char* sb = ring + stage * B_ST;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const void* p;
+        if constexpr (DGRAD) p = brow[j] + (long)tap * N * a.kc + c0;  // W[tap][n][co0 ..]
+        else p = brow[j] + (long)(tap * SC + c0) * N;                    // W[tap][c0 + k][n0 ..]
+        glds16(p, sb + (wave + 4 * j) * 1024);
+      }
+    };
+    auto compute = [&](int stage, int tap) __attribute__((always_inline)) {
+      const char* ib = ring + stage * B_ST;
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const int toff = DGRAD ? (2 - kh) * HW + (2 - kw) : kh * HW + kw;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = hbase[i] + toff, c = 4 * kk + (lane >> 4);
+          af[i] = *reinterpret_cast<const bf16x8*>(halo + q * 128 + 16 * (c ^ (q & 7)));
+          if constexpr (DGRAD) {
+            const int r = wn * 64 + i * 16 + (lane & 15);
+            bfr[i] = *reinterpret_cast<const bf16x8*>(ib + r * 128 + 16 * (c ^ kc64_swz(r)));
+          } else {
+            bfr[i] = tile::frag_mc<BN>(ib + kk * 32 * BN * 2, wn * 64 + i * 16, lane);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      }
+    };
+    tap_loop<STAGES, NB>(issue, compute);
+  }
+  __syncthreads();  // `red` of the epilogue aliases the halo
+  GemmArgs e = a;
+  const int m0 = (img * H + oh0) * W;
+  e.M = m0 + npx;  // rows past the block's pixels are masked
+  tile::epilogue<BM, BN, EPI>(e, acc, m0, n0, tm, wm, wn, wave, lane, reinterpret_cast<float*>(smem));
+}
+
+template <int BN>
+constexpr int conv3_stages() { return BN == 64 ? 4 : 3; }
+
+int halo_bytes_of(int R, int W) { return (((R + 2) * (W + 2)) * 128 + 1023) & ~1023; }
+
+template <int BN, bool DG, int EPI>
+hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
+  constexpr int ST = conv3_stages<BN>();
+  const int tpi = (a.H + R - 1) / R;
+  const size_t lds = (size_t)halo_bytes_of(R, a.W) + (size_t)ST * BN * 64 * 2;
+  auto k = conv3_kernel<BN, DG, EPI, ST>;
+  static bool attr = false;  // once per instantiation (host-side, before any capture)
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nimg = a.M / (a.H * a.W);
+  hipLaunchKernelGGL(k, dim3(a.N / BN, nimg * tpi), dim3(NT), lds, s, a, R, tpi);
+  return hipGetLastError();
+}
+
+template <int BN, bool DG>
+hipError_t launch3_epi(const GemmArgs& a, int epi, int R, hipStream_t s) {
+  switch (epi) {
+    case E_BF16: return launch3<BN, DG, E_BF16>(a, R, s);
+    case E_BIAS | E_BF16: return launch3<BN, DG, E_BIAS | E_BF16>(a, R, s);
+    case E_BIAS | E_RELU | E_BF16: return launch3<BN, DG, E_BIAS | E_RELU | E_BF16>(a, R, s);
+    case E_RELU | E_BF16: return launch3<BN, DG, E_RELU | E_BF16>(a, R, s);
+    case E_BF16 | E_STATS: return launch3<BN, DG, E_BF16 | E_STATS>(a, R, s);
+    case E_BIAS | E_BF16 | E_STATS: return launch3<BN, DG, E_BIAS | E_BF16 | E_STATS>(a, R, s);
+    case E_BF16 | E_ADD: return launch3<BN, DG, E_BF16 | E_ADD>(a, R, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+// Output rows per block of the direct 3x3 kernel for an image of width W and tile width bn
+// (0: the shape is not taken): the block's pixels R x W fill its BM = 64 * 4 / (bn / 64)
+// MFMA rows, R <= H, and the halo + weight ring fit 80 KiB (two blocks per CU).
+int conv3_rows(int H, int W, int bn) {
+  if (bn != 64 && bn != 128) return 0;
+  const int bm = bn == 64 ? 256 : 128;
+  int R = bm / W;
+  if (R < 1) return 0;
+  if (R > H) R = H;
+  const int st = bn == 64 ? conv3_stages<64>() : conv3_stages<128>();
+  if (halo_bytes_of(R, W) + st * bn * 64 * 2 > 80 * 1024) return 0;
+  return R;
+}
+
+// a.kc: the backprop-input weight row length (= the gathered channel count Cout), as for
+// A_DGRAD64; geometry in a.H / a.W (input = output size), a.Cin = gathered channels
+hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream_t s) {
+  const int R = conv3_rows(a.H, a.W, bn);
+  if (R == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || a.Cin % 64 || a.N % bn || a.M % (a.H * a.W))
+    return hipErrorInvalidValue;
+  if (dgrad && a.kc != a.Cin) return hipErrorInvalidValue;
+  if (epi & (E_SLAB | E_ATOMIC)) return hipErrorInvalidValue;
+  if (bn == 64) return dgrad ? launch3_epi<64, true>(a, epi, R, s) : launch3_epi<64, false>(a, epi, R, s);
+  return dgrad ? launch3_epi<128, true>(a, epi, R, s) : launch3_epi<128, false>(a, epi, R, s);
+}
+
+}  // namespace damd

@@ -80,7 +80,6 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
   float* lut = cw + NCONV + IB * PP * 32 / 4;                              // [256] k / 255
   const Ctrl c = *ctrl;
-  if (c.pad[2]) return;  // dry replay (graph warm-up): no work, no writes
   const int par = c.wpar;
   if (lin == 0 && tid == 0) {
     ctrl->cur2 = c.cursor;
@@ -293,7 +292,6 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   int* ylds = reinterpret_cast<int*>(db1p + 16 * HID);  // [CH] label of the row, -1 if invalid
   float* lut = reinterpret_cast<float*>(cs + CH * KC + 16);  // [256] k / 255 (after the codes)
   const Ctrl c = *ctrl;
-  if (c.pad[2]) return;
   const int cur = c.cur2, par = c.par2;
   const long long* hcur = hacc + (long)par * B * HID;
   if (s == 0 && tid == 0) {
@@ -680,7 +678,6 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
                                              uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
                                              long long* __restrict__ hconv_w) {
   const Ctrl c = *ctrl;
-  if (c.pad[2]) return;
   const bool mom = c.momentum != 0.f, pend = c.pending != 0;
   // after a step's bwd: current W1 / conv parameters live in the alternates when wpar is
   // set; the pending conv gradient is in hconv[wpar ^ 1]

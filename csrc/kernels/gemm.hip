@@ -698,6 +698,10 @@ hipError_t gemm_launch(const GemmArgs& a, int amode, int bmode, int epi, int spl
   if (splits < 1) return hipErrorInvalidValue;
   if ((epi & E_ATOMIC) && (epi & ~E_ATOMIC)) return hipErrorInvalidValue;
   if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
+  if (amode == A_CONV3 || amode == A_DGRAD3) {
+    if (bmode != (amode == A_DGRAD3 ? B_KC : B_NC) || splits != 1) return hipErrorInvalidValue;
+    return conv3_launch(a, amode == A_DGRAD3, epi, tile == 1 ? 64 : 128, s);
+  }
   if (amode == A_WGRAD3) {
     if (bmode != B_NC) return hipErrorInvalidValue;
     return wgrad3_launch(a, epi, splits, s);

@@ -28,23 +28,19 @@ StepExecutor::~StepExecutor() {
 
 void StepExecutor::invalidate_graphs() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
-  for (auto& kv : tail_graphs_) hipGraphExecDestroy(kv.second);
   graphs_.clear();
-  tail_graphs_.clear();
 }
 
 void StepExecutor::step(int k) {
   for (int i = 0; i < k; ++i) enqueue_one_step();
 }
 
-void StepExecutor::capture(int k, bool tail) {
-  auto& cache = tail ? tail_graphs_ : graphs_;
-  if (k <= 0 || cache.count(k)) return;
+void StepExecutor::capture(int k) {
+  if (k <= 0 || graphs_.count(k)) return;
   hipGraph_t g = nullptr;
   HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
     for (int i = 0; i < k; ++i) enqueue_one_step();
-    if (tail) enqueue_tail();
   } catch (...) {
     hipStreamEndCapture(stream_, &g);
     if (g) hipGraphDestroy(g);
@@ -58,19 +54,10 @@ void StepExecutor::capture(int k, bool tail) {
   // upload now, so the first replay inside a timed loop does not pay for it
   HIP_CHECK(hipGraphUpload(ge, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
-  cache[k] = ge;
+  graphs_[k] = ge;
 }
 
-void StepExecutor::run(int k, bool tail) {
-  hipGraphExec_t last = nullptr;
-  if (tail) {
-    auto it = tail_graphs_.upper_bound(k);  // the largest tail graph <= k ends the run
-    if (it != tail_graphs_.begin()) {
-      --it;
-      last = it->second;
-      k -= it->first;
-    }
-  }
+void StepExecutor::run(int k) {
   while (k > 0) {
     auto it = graphs_.upper_bound(k);  // first key > k
     if (it == graphs_.begin()) break;  // no graph <= k
@@ -79,16 +66,6 @@ void StepExecutor::run(int k, bool tail) {
     k -= it->first;
   }
   step(k);
-  if (last) HIP_CHECK(hipGraphLaunch(last, stream_));
-  else if (tail) enqueue_tail();
-}
-
-bool StepExecutor::launch_graph(int k, bool tail) {
-  auto& cache = tail ? tail_graphs_ : graphs_;
-  auto it = cache.find(k);
-  if (it == cache.end()) return false;
-  HIP_CHECK(hipGraphLaunch(it->second, stream_));
-  return true;
 }
 
 bool StepExecutor::sync(double timeout_s) { return stream_wait_with_deadline(stream_, timeout_s, comm_); }

@@ -31,17 +31,10 @@ class StepExecutor {
 
   // Enqueue k steps eagerly (one host launch per kernel).
   void step(int k);
-  // Capture k steps into a graph (cached by k); tail: the graph ends with the executor's
-  // tail work (enqueue_tail, e.g. the fused trainer's flush of the deferred update), so a
-  // run that ends in a flush is one replay.
-  void capture(int k, bool tail = false);
+  // Capture k steps into a graph (cached by k).
+  void capture(int k);
   // Run k steps: greedily replay the largest captured graph <= remaining, eager tail.
-  // tail: finish with enqueue_tail(), inside the last replay when a tail graph of <= k
-  // steps has been captured.
-  void run(int k, bool tail = false);
-  // replay the captured graph of exactly k steps (tail: the tail variant) once; false if
-  // there is none (graph warm-up: the caller makes the replay a no-op)
-  bool launch_graph(int k, bool tail = false);
+  void run(int k);
   // Block until the stream drains; false on watchdog timeout (comm aborted).
   bool sync(double timeout_s);
   void invalidate_graphs();
@@ -49,14 +42,13 @@ class StepExecutor {
 
  protected:
   virtual void enqueue_one_step() = 0;
-  virtual void enqueue_tail() {}
   hipStream_t stream_ = nullptr;
   RcclComm* comm_ = nullptr;
   PeerAllreduce* peer_ = nullptr;
   int device_;
 
  private:
-  std::map<int, hipGraphExec_t> graphs_, tail_graphs_;
+  std::map<int, hipGraphExec_t> graphs_;
 };
 
 }  // namespace damd

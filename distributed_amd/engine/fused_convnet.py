@@ -29,7 +29,7 @@ HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 REC = 716
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
 (C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
- C_FLUSHT, C_PEND, C_PAR2, C_PSTEP, C_PERR, C_DRY) = range(23)
+ C_FLUSHT, C_PEND, C_PAR2, C_PSTEP, C_PERR) = range(22)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -310,14 +310,7 @@ class FusedConvNetEngine(Engine):
         self._ctrl_write({C_CUR: 0, C_AL: 0, C_AC: 0, C_AN: 0, C_WRAP: int(wrap_steps),
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
 
-    def run(self, n_steps, flush: bool = False):
-        """n_steps training steps; flush: also apply the last step's deferred update -- with
-        graphs, inside the last replay (a graph captured with the flush as its tail)."""
-        self._run(n_steps, flush)
-        if flush:
-            self._flush()
-
-    def _run(self, n_steps, flush):
+    def run(self, n_steps):
         if self.persist and n_steps > 0:
             # the deferred update of a previous 2-launch step is applied first; the persistent
             # kernel applies every update of its own steps before it returns
@@ -338,13 +331,11 @@ class FusedConvNetEngine(Engine):
             return
         if self.use_graph and n_steps >= self.graph_steps:
             self.trainer.capture(self.graph_steps)
-            if flush:
-                self.trainer.capture(self.graph_steps, tail=True)
         if self.use_graph:
-            self.trainer.run(n_steps, tail=flush)
+            self.trainer.run(n_steps)
         else:
             self.trainer.step(n_steps)
-        self._pending = not (flush and self.use_graph)
+        self._pending = True
         self.steps_done += n_steps
 
     def phase_times(self, n_steps: int) -> dict:
@@ -366,31 +357,11 @@ class FusedConvNetEngine(Engine):
                          if self.eager_w1 else "SGD update fused into the forward kernel"),
                 "allreduce_kind": self.allreduce_kind}
 
-    def prepare(self, n_steps, flush: bool = False):
+    def prepare(self, n_steps):
         if self.persist:
             return
         if self.use_graph and not self.host_collective and n_steps >= self.graph_steps:
             self.trainer.capture(self.graph_steps)
-            if flush:
-                self.trainer.capture(self.graph_steps, tail=True)
-            self._warm_graphs(flush)
-
-    def _warm_graphs(self, tail: bool):
-        """One dry replay of each captured graph (ctrl's dry word set: every kernel returns at
-        once, nothing is written): a graph's first replay costs ~1.5 us per kernel node more
-        than later ones (measured: a fresh 20-step graph ran 28.2 us/step over 20 steps vs
-        ~23.7 warm), and that cost belongs to setup.  Only without a collective in the graph
-        (the all-reduce kernels do not read ctrl)."""
-        if self.kernels != 2 or self.world > 1 or self.allreduce_kind != "none":
-            return
-        self._flush()
-        self._ctrl_write({C_DRY: 1})
-        try:
-            for t in ((False, True) if tail else (False,)):
-                self.trainer.launch_graph(self.graph_steps, t)
-            self.trainer.sync(0.0)
-        finally:
-            self._ctrl_write({C_DRY: 0})
 
     def _flush(self):
         if self._pending:

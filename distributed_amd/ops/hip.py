@@ -22,7 +22,7 @@ import torch
 
 from ..native import require_C
 
-A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64, A_WGRAD64, A_WGRAD3 = range(9)
+A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64, A_WGRAD64, A_WGRAD3, A_CONV3, A_DGRAD3 = range(11)
 B_NC, B_KC = 0, 1
 E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB = 1, 2, 4, 8, 16, 32, 64
 BK = 32
@@ -451,6 +451,40 @@ def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
     _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw8), stream_handle())
 
 
+# ---- direct 3x3 / stride-1 / pad-1 convolution (csrc/kernels/conv3x3.hip) ---------------
+
+
+def conv3_rows(h: int, w: int, bn: int) -> int:
+    """Output rows per block of the direct 3x3 kernel (mirror of conv3x3.hip conv3_rows):
+    the block's R x W pixels fill its 256 (BN 64) / 128 (BN 128) MFMA rows and the input
+    halo + weight ring fit 80 KiB (two blocks per CU); 0 = shape not taken."""
+    bm = 256 if bn == 64 else 128
+    r = min(bm // w, h)
+    if r < 1:
+        return 0
+    halo = (((r + 2) * (w + 2)) * 128 + 1023) & ~1023
+    return r if halo + (4 if bn == 64 else 3) * bn * 128 <= 80 * 1024 else 0
+
+
+def conv3_tile(n: int, h: int, w: int, gathered: int, out_ch: int):
+    """(tile, rows, row blocks per image) when the direct kernel takes a 3x3/s1/p1 conv of
+    ``gathered`` input channels into ``out_ch`` on n x h x w images, else None: channels %
+    64, the block's pixels fill >= 3/4 of its MFMA rows, and the grid has >= CONV3_MIN_WG
+    blocks (DAMD_CONV3_MIN_WG, default 384; smaller grids keep the split-K implicit GEMM)."""
+    if os.environ.get("DAMD_CONV3", "1") == "0" or os.environ.get("DAMD_CONV_GLDS", "1") == "0":
+        return None
+    if gathered % 64 or out_ch % 64:
+        return None
+    bn = 64 if out_ch % 128 else 128
+    r = conv3_rows(h, w, bn)
+    if r == 0 or r * w < 0.75 * (256 if bn == 64 else 128):
+        return None
+    tpi = -(-h // r)
+    if (out_ch // bn) * n * tpi < int(os.environ.get("DAMD_CONV3_MIN_WG", 384)):
+        return None
+    return (1 if bn == 64 else 0), r, tpi
+
+
 def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     """Launch plan of conv_fwd: tile, split-K, number of BN-statistics partials and the
     fp32 workspace it needs (0 when not split)."""
@@ -464,6 +498,10 @@ def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
                 "kstep": 32, "stats_T": -(-M // (FINISH_RB if splits > 1 else tile_rows(t))),
                 "ws": splits * M * N if splits > 1 else 0}
     M, N, K = n * ho * wo, cout, kh * kw * cin
+    c3 = conv3_tile(n, h, wd, cin, cout) if (kh == kw == 3 and s == 1 and pad == 1 and ho == h) else None
+    if c3 is not None:
+        return {"M": M, "N": N, "K": K, "tile": c3[0], "splits": 1, "kps": K, "amode": A_CONV3,
+                "stats_T": n * c3[2], "ws": 0}
     t = pick_tile(N)
     glds = use_glds(cin)
     splits, kps = split_plan(M, N, K, t, conv_kstep() if glds else BK)
@@ -514,6 +552,9 @@ def _workspace(ws, need, device):
 def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx_shape, w_shape, strides, padding)
     M, N, K = n * h * wd, cin, kh * kw * cout
+    c3 = conv3_tile(n, h, wd, cout, cin) if (kh == kw == 3 and s == 1 and pad == 1 and ho == h) else None
+    if c3 is not None:
+        return {"M": M, "N": N, "K": K, "tile": c3[0], "splits": 1, "kps": K, "amode": A_DGRAD3, "ws": 0}
     t = pick_tile(N)
     if (s == 2 and use_glds(cout) and h % 2 == 0 and wd % 2 == 0 and pad == 0
             and os.environ.get("DAMD_DGRAD_SUBPIX", "1") != "0"):

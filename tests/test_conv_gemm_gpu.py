@@ -378,3 +378,59 @@ def test_bn_bwd_relu_mask_from_x(H, M, c):
         out.append((part, dg, db, dx))
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+CONV3_CASES = [
+    # n, h, cin, cout: tile BN 64 (256 x 64) / 128 (128 x 128), R output rows per block
+    (2, 56, 64, 64),     # ResNet layer 1: BN 64, R 4 (224 of 256 rows)
+    (2, 28, 128, 128),   # layer 2: BN 128, R 4
+    (2, 14, 256, 256),   # BN 128, R 9: row blocks of 9 + 5 rows (ragged last block)
+    (3, 20, 64, 128),    # R 6 over 20 rows (6, 6, 6, 2)
+    (2, 30, 128, 64),    # BN 64, R 8 over 30 rows; 2 ci-chunks
+]
+
+
+@pytest.mark.parametrize("n,h,cin,cout", CONV3_CASES)
+def test_direct_conv3(H, monkeypatch, n, h, cin, cout):
+    """The direct 3x3/s1/p1 kernel (csrc/kernels/conv3x3.hip: input halo resident in LDS,
+    weights streamed per tap) against the fp32 conv and the implicit-GEMM kernel, forward
+    with bias + ReLU and with the BN-statistics epilogue, backprop-input plain and
+    accumulating."""
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    x = rb(rnd(n, h, h, cin, seed=11)).requires_grad_(True)
+    w = rb(rnd(3, 3, cin, cout, scale=0.05, seed=12)).requires_grad_(True)
+    bias = rnd(cout, scale=0.1, seed=13)
+    y = ref.conv2d(x, w, None, (1, 1), "same")
+    dy = rb(rnd(*y.shape, seed=14))
+    gx, = torch.autograd.grad(y, (x,), dy)
+    xb, wb, dyb = x.detach().bfloat16(), w.detach().bfloat16(), dy.bfloat16()
+    fplan = H.conv_fwd_plan(x.shape, w.shape, (1, 1), "same")
+    dplan = H.conv_dgrad_plan(x.shape, w.shape, (1, 1), "same")
+    assert fplan["amode"] == H.A_CONV3 and dplan["amode"] == H.A_DGRAD3
+    # forward, bias + ReLU epilogue
+    out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_fwd(xb, wb, out, (1, 1), "same", bias=bias, relu=True)
+    close(out, torch.relu(y.detach() + bias), 1e-2, 4e-3)
+    # forward with BN statistics: per-tile partials summing to the stored values' moments
+    st = torch.zeros(fplan["stats_T"], 2, cout, device=dev)
+    out2 = torch.empty_like(out)
+    H.conv_fwd(xb, wb, out2, (1, 1), "same", stats=st)
+    close(out2, y.detach(), 1e-2, 4e-3)
+    y32 = out2.float().reshape(-1, cout)
+    close(st[:, 0].sum(0), y32.sum(0), 1e-3, 1e-4)
+    close(st[:, 1].sum(0), (y32 * y32).sum(0), 1e-3, 1e-4)
+    # the implicit-GEMM kernel: same products, another summation order
+    monkeypatch.setenv("DAMD_CONV3", "0")
+    assert H.conv_fwd_plan(x.shape, w.shape, (1, 1), "same")["amode"] != H.A_CONV3
+    out0 = torch.empty_like(out)
+    H.conv_fwd(xb, wb, out0, (1, 1), "same")
+    close(out2, out0, 1e-2, 2e-3)
+    monkeypatch.setenv("DAMD_CONV3", "1")
+    # backprop-input, then accumulating onto it
+    dx = torch.empty(x.shape, device=dev, dtype=torch.bfloat16)
+    H.conv_dgrad(dyb, wb, dx, (1, 1), "same")
+    close(dx, gx, 1e-2, 4e-3)
+    base = rb(rnd(*x.shape, seed=15))
+    dx2 = base.bfloat16().contiguous()
+    H.conv_dgrad(dyb, wb, dx2, (1, 1), "same", accumulate=True)
+    close(dx2, gx + base, 1e-2, 4e-3)
