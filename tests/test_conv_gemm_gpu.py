@@ -387,16 +387,20 @@ CONV3_CASES = [
     (2, 14, 256, 256),   # BN 128, R 9: row blocks of 9 + 5 rows (ragged last block)
     (3, 20, 64, 128),    # R 6 over 20 rows (6, 6, 6, 2)
     (2, 30, 128, 64),    # BN 64, R 8 over 30 rows; 2 ci-chunks
+    (3, 28, 64, 64),     # 64 -> 64 at R 9 (28 = 9 + 9 + 9 + 1 rows)
 ]
 
 
+@pytest.mark.parametrize("stationary", ["1", "0"])
 @pytest.mark.parametrize("n,h,cin,cout", CONV3_CASES)
-def test_direct_conv3(H, monkeypatch, n, h, cin, cout):
+def test_direct_conv3(H, monkeypatch, n, h, cin, cout, stationary):
     """The direct 3x3/s1/p1 kernel (csrc/kernels/conv3x3.hip: input halo resident in LDS,
     weights streamed per tap) against the fp32 conv and the implicit-GEMM kernel, forward
     with bias + ReLU and with the BN-statistics epilogue, backprop-input plain and
-    accumulating."""
+    accumulating.  64 -> 64 shapes also through the weight-stationary persistent kernel
+    (DAMD_CONV3W=1)."""
     monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    monkeypatch.setenv("DAMD_CONV3W", stationary)
     x = rb(rnd(n, h, h, cin, seed=11)).requires_grad_(True)
     w = rb(rnd(3, 3, cin, cout, scale=0.05, seed=12)).requires_grad_(True)
     bias = rnd(cout, scale=0.1, seed=13)
