@@ -52,6 +52,8 @@ int wgrad3_rows(int N, int H, int W);
 // block for an H x W image (0: not supported); stats partials = Nimg * ceil(H / rows)
 hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream_t s);
 int conv3_rows(int H, int W, int bn);
+hipError_t conv3_stamps_enable(int on);                              // diagnostics
+hipError_t conv3_stamps_read(unsigned long long* host, int blocks);  // [blocks][4]
 int wgrad64_rows_per_step(int Wo, int kstep);
 // k-step depth of those kernels (32 or 64, env DAMD_CONV_KB): the gathered channel count
 // must be a multiple of it for A_CONV64 / A_DGRAD64

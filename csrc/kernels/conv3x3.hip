@@ -38,6 +38,12 @@ constexpr int NT = 256;
 
 __device__ __attribute__((aligned(64))) uint4 g_zero16_c3[4];
 
+// Diagnostics (conv3_stamps_enable): per block s_memrealtime at kernel start, after the
+// first tap's operands landed, after the taps, after the epilogue -> g_c3_st[block][4]
+constexpr int kC3StampBlocks = 4096;
+__device__ int g_c3_on;
+__device__ unsigned long long g_c3_st[kC3StampBlocks][4];
+
 using tile::glds16;
 
 // k-contiguous [rows][64] image swizzle (conv_gemm.hip kc_swz<64>)
@@ -73,6 +79,8 @@ __device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute) {
 // block, tpi = ceil(H / R) row blocks per image; grid (N / BN, Nimg * tpi).
 template <int BN, bool DGRAD, int EPI, int STAGES>
 __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi) {
+  const bool stamps = g_c3_on != 0;
+  unsigned long long st0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, st1 = 0ull, st2 = 0ull;
   constexpr int WN = BN / 64, WM = 4 / WN, BM = WM * 64;
   constexpr int B_ST = BN * 64 * 2;
   constexpr int NB = B_ST / 4096;  // weight DMA instructions per wave per stage
@@ -158,6 +166,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
       }
     };
     auto compute = [&](int stage, int tap) __attribute__((always_inline)) {
+      if (stamps && chunk == 0 && tap == 0) st1 = __builtin_amdgcn_s_memrealtime();
       const char* ib = ring + stage * B_ST;
       const int kh = tap / 3, kw = tap - kh * 3;
       const int toff = DGRAD ? (2 - kh) * HW + (2 - kw) : kh * HW + kw;
@@ -183,11 +192,21 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
     };
     tap_loop<STAGES, NB>(issue, compute);
   }
+  if (stamps) st2 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();  // `red` of the epilogue aliases the halo
   GemmArgs e = a;
   const int m0 = (img * H + oh0) * W;
   e.M = m0 + npx;  // rows past the block's pixels are masked
   tile::epilogue<BM, BN, EPI>(e, acc, m0, n0, tm, wm, wn, wave, lane, reinterpret_cast<float*>(smem));
+  if (stamps && threadIdx.x == 0) {
+    const int b = blockIdx.y * gridDim.x + blockIdx.x;
+    if (b < kC3StampBlocks) {
+      g_c3_st[b][0] = st0;
+      g_c3_st[b][1] = st1;
+      g_c3_st[b][2] = st2;
+      g_c3_st[b][3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 // ---- weight-stationary persistent variant: 64 -> 64 channels (opt-in, DAMD_CONV3W=1) ----
@@ -375,6 +394,13 @@ hipError_t launch3_epi(const GemmArgs& a, int epi, int R, hipStream_t s) {
 }
 
 }  // namespace
+
+hipError_t conv3_stamps_enable(int on) { return hipMemcpyToSymbol(HIP_SYMBOL(g_c3_on), &on, sizeof(int)); }
+// [blocks][4] stamps of the last conv3_kernel launch (host copy; synchronizes)
+hipError_t conv3_stamps_read(unsigned long long* host, int blocks) {
+  if (blocks > kC3StampBlocks) blocks = kC3StampBlocks;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_c3_st), (size_t)blocks * 4 * sizeof(unsigned long long));
+}
 
 // Output rows per block of the direct 3x3 kernel for an image of width W and tile width bn
 // (0: the shape is not taken): the block's pixels R x W fill its BM = 64 * 4 / (bn / 64)

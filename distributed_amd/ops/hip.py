@@ -470,7 +470,7 @@ def conv3_tile(n: int, h: int, w: int, gathered: int, out_ch: int):
     """(tile, rows, row blocks per image) when the direct kernel takes a 3x3/s1/p1 conv of
     ``gathered`` input channels into ``out_ch`` on n x h x w images, else None: channels %
     64, the block's pixels fill >= 3/4 of its MFMA rows, and the grid has >= CONV3_MIN_WG
-    blocks (DAMD_CONV3_MIN_WG, default 384; smaller grids keep the split-K implicit GEMM)."""
+    blocks (DAMD_CONV3_MIN_WG, default 256: ResNet layers 1-3; smaller grids keep the split-K implicit GEMM)."""
     if os.environ.get("DAMD_CONV3", "1") == "0" or os.environ.get("DAMD_CONV_GLDS", "1") == "0":
         return None
     if gathered % 64 or out_ch % 64:
@@ -480,7 +480,7 @@ def conv3_tile(n: int, h: int, w: int, gathered: int, out_ch: int):
     if r == 0 or r * w < 0.75 * (256 if bn == 64 else 128):
         return None
     tpi = -(-h // r)
-    if (out_ch // bn) * n * tpi < int(os.environ.get("DAMD_CONV3_MIN_WG", 384)):
+    if (out_ch // bn) * n * tpi < int(os.environ.get("DAMD_CONV3_MIN_WG", 256)):
         return None
     return (1 if bn == 64 else 0), r, tpi
 
