@@ -59,8 +59,9 @@ int wgrad64_rows_per_step(int Wo, int kstep);
 // must be a multiple of it for A_CONV64 / A_DGRAD64
 int conv_gemm_kstep();
 int gemm_stats_tile_rows(int tile);
-// dst[i] += sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order)
-hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s);
+// dst[i] (+)= sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order);
+// accumulate = 0 overwrites dst (no zeroing pass before a first writer)
+hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s, int accumulate = 1);
 // bf16 split-K epilogue: out = relu?(sum_s slab[s] + bias + R) (R bf16 [M][ldc], may alias
 // out); stats (optional) = per-column sum / sumsq of the stored pre-ReLU values per block
 // of rows_per_block rows: [ceil(M / rows_per_block)][2][N]

@@ -143,11 +143,12 @@ hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, u
 // the step's rows of the (epoch-permuted) dataset: row = (cursor*global_batch + row0 + i)
 // mod nsamples (cursor from ctrl); x fp32 or uint8 (k / scale, i.e. exactly float32(k/255)
 // for scale 255) [n][HW][Cin] -> bf16
-// [per][HW][Cp] zero-padded channels; labels int32.  `zero` (optional): nzero doubles
-// cleared in the same launch (the step's BatchNorm statistics accumulators, BNFin).
+// [per][HW][Cp] zero-padded channels; labels int32.  zero / zero2 (optional): byte ranges
+// (16-byte aligned, multiples of 16 bytes) cleared in the same launch -- the step's
+// gradient buffer and BatchNorm statistics accumulators, so no memset launch precedes it.
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
-                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, double* zero = nullptr,
-                        long nzero = 0);
+                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, void* zero = nullptr,
+                        long zero_bytes = 0, void* zero2 = nullptr, long zero2_bytes = 0);
 // fp32 [R][C1][C2] -> bf16 [R][C1p][C2p] (zero padding)
 hipError_t pad_cast(const float* src, int R, int C1, int C2, int C1p, int C2p, uint16_t* dst, hipStream_t s);
 // dst fp32 [R][C1][C2] += src fp32 [R][C1p][C2p] (the un-padded part)

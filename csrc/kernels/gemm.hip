@@ -501,7 +501,7 @@ hipError_t launch_tile(const GemmArgs& a, int epi, int splits, int tile, hipStre
 // ~600 blocks streaming the slabs.
 constexpr int RED_E = 16, RED_G = NT / RED_E;
 __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__ slab, int splits, long n4,
-                                                     float4* __restrict__ dst) {
+                                                     float4* __restrict__ dst, int accumulate) {
   __shared__ float4 part[RED_G][RED_E];
   const int e = threadIdx.x % RED_E, g = threadIdx.x / RED_E;
   const long i = blockIdx.x * (long)RED_E + e;
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__
   part[g][e] = acc;
   __syncthreads();
   if (g == 0 && i < n4) {
-    float4 d = dst[i];
+    float4 d = accumulate ? dst[i] : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < RED_G; ++q) {
       d.x += part[q][e].x; d.y += part[q][e].y; d.z += part[q][e].z; d.w += part[q][e].w;
@@ -617,14 +617,14 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
 // splitk_reduce_k would leave 16 - S of every 16 threads idle and run ~n4/16 tiny blocks.
 constexpr int FLAT_MAX_SPLITS = 16;
 __global__ __launch_bounds__(NT) void splitk_reduce_flat_k(const float4* __restrict__ slab, int splits, long n4,
-                                                          float4* __restrict__ dst) {
+                                                          float4* __restrict__ dst, int accumulate) {
   const long i = blockIdx.x * (long)NT + threadIdx.x;
   if (i >= n4) return;
   float4 v[FLAT_MAX_SPLITS];
 #pragma unroll
   for (int sp = 0; sp < FLAT_MAX_SPLITS; ++sp)
     if (sp < splits) v[sp] = slab[(size_t)sp * n4 + i];
-  float4 d = dst[i];
+  float4 d = accumulate ? dst[i] : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int sp = 0; sp < FLAT_MAX_SPLITS; ++sp)
     if (sp < splits) {
@@ -668,17 +668,17 @@ hipError_t splitk_finish_f32(const float* slab, int splits, int M, int N, const 
   return hipGetLastError();
 }
 
-hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s) {
+hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s, int accumulate) {
   if (n % 4 || splits < 1) return hipErrorInvalidValue;
   const long n4 = n / 4;
   if (splits <= FLAT_MAX_SPLITS && n4 >= 32 * NT) {
     hipLaunchKernelGGL(splitk_reduce_flat_k, dim3((unsigned)((n4 + NT - 1) / NT)), dim3(NT), 0, s,
-                       reinterpret_cast<const float4*>(slab), splits, n4, reinterpret_cast<float4*>(dst));
+                       reinterpret_cast<const float4*>(slab), splits, n4, reinterpret_cast<float4*>(dst), accumulate);
     return hipGetLastError();
   }
   const long g = (n4 + RED_E - 1) / RED_E;
   hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab),
-                     splits, n4, reinterpret_cast<float4*>(dst));
+                     splits, n4, reinterpret_cast<float4*>(dst), accumulate);
   return hipGetLastError();
 }
 

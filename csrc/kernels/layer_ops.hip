@@ -1279,8 +1279,10 @@ __global__ __launch_bounds__(NT) void sgd_step_k(float* __restrict__ P, const fl
 __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x, int x_u8, float scale,
                                                      const int32_t* __restrict__ labels, Ctrl* __restrict__ ctrl,
                                                      int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
-                                                     int32_t* __restrict__ yb, double* __restrict__ zero, long nzero) {
-  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nzero; i += (long)gridDim.x * NT) zero[i] = 0.0;
+                                                     int32_t* __restrict__ yb, uint4* __restrict__ zero, long nz16,
+                                                     uint4* __restrict__ zero2, long nz16b) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nz16; i += (long)gridDim.x * NT) zero[i] = uint4{0u, 0u, 0u, 0u};
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nz16b; i += (long)gridDim.x * NT) zero2[i] = uint4{0u, 0u, 0u, 0u};
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
@@ -1484,11 +1486,18 @@ hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ct
 }
 
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
-                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, double* zero, long nzero) {
+                        int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, void* zero, long zero_bytes,
+                        void* zero2, long zero2_bytes) {
   if (Cp % 8 && !(Cp == 4 && Cin <= 4 && HW % 2 == 0)) return hipErrorInvalidValue;
-  if (nzero < 0 || (nzero > 0 && zero == nullptr)) return hipErrorInvalidValue;
+  for (int k = 0; k < 2; ++k) {
+    const void* z = k ? zero2 : zero;
+    const long nb = k ? zero2_bytes : zero_bytes;
+    if (nb < 0 || nb % 16 || (nb > 0 && (z == nullptr || reinterpret_cast<uintptr_t>(z) % 16)))
+      return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp / 8)), dim3(NT), 0, s, x, x_u8, scale, labels,
-                     ctrl, per, HW, Cin, Cp, xb, yb, zero, nzero);
+                     ctrl, per, HW, Cin, Cp, xb, yb, static_cast<uint4*>(zero), zero_bytes / 16,
+                     static_cast<uint4*>(zero2), zero2_bytes / 16);
   return hipGetLastError();
 }
 

@@ -78,10 +78,10 @@ void register_kernel_ops(py::module_& m) {
                                   ldc, P_<ihipStream_t>(stream)),
           "splitk_finish_f32");
   });
-  m.def("splitk_reduce", [](uintptr_t slab, int splits, long n, uintptr_t dst, uintptr_t stream) {
-    check(damd::splitk_reduce(P_<const float>(slab), splits, n, P_<float>(dst), P_<ihipStream_t>(stream)),
+  m.def("splitk_reduce", [](uintptr_t slab, int splits, long n, uintptr_t dst, uintptr_t stream, int accumulate) {
+    check(damd::splitk_reduce(P_<const float>(slab), splits, n, P_<float>(dst), P_<ihipStream_t>(stream), accumulate),
           "splitk_reduce");
-  });
+  }, py::arg("slab"), py::arg("splits"), py::arg("n"), py::arg("dst"), py::arg("stream"), py::arg("accumulate") = 1);
 
   using U = uintptr_t;
   using u16 = uint16_t;
@@ -280,14 +280,14 @@ void register_kernel_ops(py::module_& m) {
           "opt_step");
   });
   m.def("gather_batch", [](U x, int x_u8, float scale, U labels, U ctrl, int per, int HW, int Cin, int Cp, U xb, U yb,
-                           U s, U zero, long nzero) {
+                           U s, U zero, long zero_bytes, U zero2, long zero2_bytes) {
     check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<damd::Ctrl>(ctrl),
-                             per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s), P_<double>(zero),
-                             nzero),
+                             per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s), P_<void>(zero),
+                             zero_bytes, P_<void>(zero2), zero2_bytes),
           "gather_batch");
   }, py::arg("x"), py::arg("x_u8"), py::arg("scale"), py::arg("labels"), py::arg("ctrl"), py::arg("per"),
      py::arg("HW"), py::arg("Cin"), py::arg("Cp"), py::arg("xb"), py::arg("yb"), py::arg("s"), py::arg("zero") = 0,
-     py::arg("nzero") = 0);
+     py::arg("zero_bytes") = 0, py::arg("zero2") = 0, py::arg("zero2_bytes") = 0);
   m.def("pad_cast", [](U src, int R, int C1, int C2, int C1p, int C2p, U dst, U s) {
     check(damd::pad_cast(P_<const float>(src), R, C1, C2, C1p, C2p, P_<u16>(dst), P_<ihipStream_t>(s)), "pad_cast");
   });

@@ -735,11 +735,13 @@ class NativeGraphEngine(Engine):
         s = H.stream_handle()
         self._mark("start")
         h, w, c = self.in_shape
-        self.G.zero_()
+        # the step's first launch also clears the gradient buffer (and the BN statistics
+        # accumulators): no memset launch in the step
         acc = self.bn_acc
         C.gather_batch(self.x_ep.data_ptr(), int(self.feed.x_u8), 255.0, self.y_ep.data_ptr(), self.ctrl.data_ptr(),
                        B, h * w, c, self.cin_pad, self.x0.buf.data_ptr(), self.labels.data_ptr(), s,
-                       zero=acc.data_ptr() if acc is not None else 0, nzero=acc.numel() if acc is not None else 0)
+                       zero=self.G.data_ptr(), zero_bytes=self.G.numel() * 4,
+                       zero2=acc.data_ptr() if acc is not None else 0, zero2_bytes=acc.numel() * 8 if acc is not None else 0)
         live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
         for nd in live:
             getattr(self, "_fwd_" + nd.kind)(nd)
@@ -806,7 +808,8 @@ class NativeGraphEngine(Engine):
         if nd.kind == "Conv2D":
             kh, kw, cin, cout = l.kernel.shape
             if nd.attrs.get("stem4"):
-                nd.attrs["w_pad"][:, :kw, :cin].copy_(self.views[id(l.kernel)])  # zeros elsewhere stay zero
+                # [KH][KW][cin][cout] -> [KH][8][4][cout]: the (cin, cout) rows padded at their tail
+                H.pad_cast(self.views[id(l.kernel)], kh, kw, cin * cout, 8, 4 * cout, nd.attrs["w_pad"])
             else:
                 H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
         elif nd.kind == "Dense":
@@ -951,13 +954,11 @@ class NativeGraphEngine(Engine):
             if nd.attrs.get("stem4"):
                 kh, kw, cin, cout = l.kernel.shape
                 dwp = nd.attrs["dw_pad"]
-                dwp.zero_()
-                H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=wsp)
-                self.gviews[id(l.kernel)].add_(dwp[:, :kw, :cin])
+                H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=wsp, accumulate=False)
+                H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
             elif "dw_pad" in nd.attrs:
                 dwp = nd.attrs["dw_pad"]
-                dwp.zero_()
-                H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=wsp)
+                H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=wsp, accumulate=False)
                 kh, kw, cin, cout = l.kernel.shape
                 H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
             else:
@@ -1133,8 +1134,7 @@ class NativeGraphEngine(Engine):
                 H.colsum(dy, self.gviews[id(l.bias)])
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
-            dwp.zero_()
-            H.dense_wgrad(x2, dy, dwp, workspace=self.gemm_ws)
+            H.dense_wgrad(x2, dy, dwp, workspace=self.gemm_ws, accumulate=False)
             kin = l.kernel.shape[0]
             H.unpad_add(dwp, 1, kin, units, kin, dwp.shape[1], self.gviews[id(l.kernel)])
         else:

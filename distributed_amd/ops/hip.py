@@ -230,10 +230,12 @@ def conv_wgrad_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
             "ws": splits * M * N if splits > 1 else 0}
 
 
-def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
+def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=(), accumulate=True):
     t, splits, kps = wgrad_plan(M, N, K)
     if splits == 1 and not (_wgrad_slab1(M, N, K) and workspace is not None and workspace.numel() >= M * N):
         # one writer per element: the atomic epilogue is an uncontended add
+        if not accumulate:
+            dw.zero_()
         gemm(A, B, dw, amode=amode, bmode=B_NC, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N, epi=E_ATOMIC, geo=geo,
              tile=t)
         return
@@ -242,7 +244,7 @@ def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=()):
         raise ValueError(f"weight-gradient GEMM needs an fp32 workspace of {need} elements")
     gemm(A, B, workspace, amode=amode, bmode=B_NC, M=M, N=N, K=K, lda=lda, ldb=ldb, ldc=N, epi=E_SLAB,
          splits=splits, k_per_split=kps, tile=t, geo=geo)
-    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle())
+    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle(), accumulate=int(accumulate))
 
 
 def _stats_ptrs(stats):
@@ -344,8 +346,10 @@ def dense_dgrad(dy: torch.Tensor, w: torch.Tensor, dx: torch.Tensor, accumulate=
          R=dx if accumulate else None)
 
 
-def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, workspace: Optional[torch.Tensor] = None):
-    """dw[K,N] += x[M,K]^T @ dy[M,N] (fp32; split over M, slabs reduced in fixed order)."""
+def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, workspace: Optional[torch.Tensor] = None,
+                accumulate: bool = True):
+    """dw[K,N] (+)= x[M,K]^T @ dy[M,N] (fp32; split over M, slabs reduced in fixed order);
+    accumulate=False overwrites dw."""
     M, K = x.shape
     M2, N = dy.shape
     assert M == M2 and tuple(dw.shape) == (K, N)
@@ -354,7 +358,7 @@ def dense_wgrad(x: torch.Tensor, dy: torch.Tensor, dw: torch.Tensor, workspace: 
     _chk(dw, torch.float32, "dw")
     if workspace is None and wgrad_workspace_elems(K, N, M):
         workspace = torch.empty(wgrad_workspace_elems(K, N, M), device=x.device)
-    _wgrad_gemm(x, dy, dw, workspace, amode=A_MC, M=K, N=N, K=M, lda=K, ldb=N)
+    _wgrad_gemm(x, dy, dw, workspace, amode=A_MC, M=K, N=N, K=M, lda=K, ldb=N, accumulate=accumulate)
 
 
 # ---- conv ---------------------------------------------------------------------------------
@@ -426,7 +430,7 @@ def _check_stats(stats, plan, cout, who):
 
 
 def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
-                     workspace: Optional[torch.Tensor] = None):
+                     workspace: Optional[torch.Tensor] = None, accumulate: bool = True):
     """Packed-tap stem weight gradient: dw8 [KH][8][4][Cout] (fp32) += the gradient in the
     stem4_weight_shape layout (entries beyond the true kernel are junk to drop)."""
     k = kernel_size
@@ -442,13 +446,15 @@ def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
     geo = (h, wd, 4, ho, wo, kh, 8, s, pad)
     M, N, K, splits = plan["M"], plan["N"], plan["K"], plan["splits"]
     if splits == 1:
+        if not accumulate:
+            dw8.zero_()
         gemm(x, dy, dw8, amode=A_WGRAD64, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_ATOMIC, geo=geo,
              k_per_split=plan["kps"], tile=plan["tile"], kstep=plan["kstep"])
         return
     workspace = _workspace(workspace, plan["ws"], x.device)
     gemm(x, dy, workspace, amode=A_WGRAD64, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_SLAB,
          splits=splits, k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=plan["kstep"])
-    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw8), stream_handle())
+    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw8), stream_handle(), accumulate=int(accumulate))
 
 
 # ---- direct 3x3 / stride-1 / pad-1 convolution (csrc/kernels/conv3x3.hip) ---------------
@@ -598,9 +604,11 @@ def conv_wgrad_workspace_elems(x_shape, w_shape, strides=(1, 1), padding="valid"
     return conv_wgrad_plan(x_shape, w_shape, strides, padding)["ws"]
 
 
-def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid", workspace: Optional[torch.Tensor] = None):
-    """dw [KH,KW,Cin,Cout] += sum over pixels of im2col(x)^T dy (split-K over pixels, fp32
-    slabs in ``workspace`` (conv_wgrad_workspace_elems) reduced in fixed order)."""
+def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid", workspace: Optional[torch.Tensor] = None,
+               accumulate: bool = True):
+    """dw [KH,KW,Cin,Cout] (+)= sum over pixels of im2col(x)^T dy (split-K over pixels, fp32
+    slabs in ``workspace`` (conv_wgrad_workspace_elems) reduced in fixed order);
+    accumulate=False overwrites dw (no zeroing pass)."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, dw.shape, strides, padding)
     _chk(x, torch.bfloat16, "x")
     _chk(dy, torch.bfloat16, "dy")
@@ -611,13 +619,15 @@ def conv_wgrad(x, dy, dw, strides=(1, 1), padding="valid", workspace: Optional[t
     M, N, K, splits = plan["M"], plan["N"], plan["K"], plan["splits"]
     geo = (h, wd, cin, ho, wo, kh, kw, s, pad)
     if splits == 1:  # one writer per element: the atomic epilogue is an uncontended add
+        if not accumulate:
+            dw.zero_()
         gemm(x, dy, dw, amode=plan["amode"], bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_ATOMIC, geo=geo,
              k_per_split=plan["kps"], tile=plan["tile"], kstep=plan["kstep"])
         return
     workspace = _workspace(workspace, plan["ws"], x.device)
     gemm(x, dy, workspace, amode=plan["amode"], bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_SLAB,
          splits=splits, k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=plan["kstep"])
-    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle())
+    _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle(), accumulate=int(accumulate))
 
 
 # ---- BN / pooling / loss / optimizer -------------------------------------------------------------
