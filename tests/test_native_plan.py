@@ -116,3 +116,33 @@ def test_round3_layers_and_optimizers_are_native_eligible():
     assert ("Activation", False) in kinds.values()  # tanh is a real node (not an identity)
     pools = [nd for nd in pl.nodes if nd.kind == "AveragePooling2D"]
     assert pools[0].out.shape == (8, 7, 7, 16)
+
+
+def test_direct_conv3_planner_on_resnet18_shapes():
+    """The planner routes the ResNet-18 3x3/stride-1 convs of layers 1-3 (batch 64) to the
+    direct kernel (conv3x3.hip) for forward and backprop-input, and keeps the implicit
+    GEMM for layer 4 (7x7 images fill 49 of 128 MFMA rows), stride-2 and 1x1 convs; the
+    Python mirror of the row planner agrees with the C++ one."""
+    from distributed_amd.native import native_status
+    from distributed_amd.ops import hip as H
+
+    B = 64
+    for h, c, want in ((56, 64, True), (28, 128, True), (14, 256, True), (7, 512, False)):
+        f = H.conv_fwd_plan((B, h, h, c), (3, 3, c, c), (1, 1), "same")
+        d = H.conv_dgrad_plan((B, h, h, c), (3, 3, c, c), (1, 1), "same")
+        assert (f["amode"] == H.A_CONV3) == want and (d["amode"] == H.A_DGRAD3) == want, (h, c)
+        if want:
+            assert f["splits"] == 1 and f["ws"] == 0
+            r = H.conv3_rows(h, h, 64 if c % 128 else 128)
+            assert f["stats_T"] == B * -(-h // r)
+    assert H.conv_fwd_plan((B, 56, 56, 64), (3, 3, 64, 128), (2, 2), "same")["amode"] != H.A_CONV3
+    assert H.conv_fwd_plan((B, 56, 56, 64), (1, 1, 64, 128), (2, 2), "valid")["amode"] != H.A_CONV3
+    # small grids keep the split-K implicit GEMM (the default threshold is 256 blocks)
+    assert H.conv_fwd_plan((2, 56, 56, 64), (3, 3, 64, 64), (1, 1), "same")["amode"] != H.A_CONV3
+    if native_status().get("C"):
+        from distributed_amd.native import require_C
+
+        C = require_C()
+        for h in (7, 14, 20, 28, 30, 56, 112, 200):
+            for bn in (64, 128):
+                assert C.conv3_rows(h, h, bn) == H.conv3_rows(h, h, bn), (h, bn)
