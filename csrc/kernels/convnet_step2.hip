@@ -123,9 +123,12 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   }
   // conv parameters: current buffer by parity; their gradient is the previous step's
   // (bwd added it into hconv[par ^ 1])
+  // (both parities are loaded: the addresses do not wait for the ctrl block, only the select)
   const int tcl = min(tid, NCONV - 1);
-  const float cp = (par ? calt : P)[tcl], cv = (par ? calt + NCONV : V)[tcl];
-  const long long cq = hconv_r[(par ^ 1) * NCONV + tcl];
+  const float cp0 = P[tcl], cp1 = calt[tcl], cv0 = V[tcl], cv1 = calt[NCONV + tcl];
+  const long long cq0 = hconv_r[NCONV + tcl], cq1 = hconv_r[tcl];
+  const float cp = par ? cp1 : cp0, cv = par ? cv1 : cv0;
+  const long long cq = par ? cq1 : cq0;
   // b1/W2/b2: the grid's last two blocks own their pending update (nobody else in this
   // launch reads them; bwd reads the updated values)
   const int si = (lin - (nblk - 2)) * 512 + tid;
