@@ -17,7 +17,10 @@ enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4,
 enum GemmBMode { B_NC = 0, B_KC = 1 };
 // E_SLAB: split-K partial of split z stored (plain fp32 stores) to C + z * M * ldc; a
 // deterministic splitk_reduce then adds the slabs into the destination in fixed order.
-enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32, E_SLAB = 64 };
+// E_BNRED: the GEMM produces the gradient of a BN -> ReLU output (backprop-input of the
+// conv that consumes it): the tile's BN-backward partials (sum of the ReLU-masked stored
+// gradient, and of it times xhat, from bnx / bnst) go to `stats` as E_STATS would
+enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32, E_SLAB = 64, E_BNRED = 128 };
 
 struct GemmArgs {
   const void* A;       // bf16
@@ -37,6 +40,8 @@ struct GemmArgs {
   int kstep;           // conv_gemm.hip k-step depth: 32 | 64 (0: DAMD_CONV_KB / 64)
   double* stats_acc;   // E_STATS: non-null -> the tile's column sum / sumsq are added (fp64
                        // atomics) into stats_acc[2][N] instead of stored to `stats`
+  const uint16_t* bnx; // E_BNRED: the BN input x [M][ldc] bf16 and its st [4][N] (mean,
+  const float* bnst;   //   invstd, scale, shift)
 };
 
 // tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)

@@ -126,6 +126,28 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
           csq[j][e] += x * x;
         }
       }
+      if constexpr (EPI & E_BNRED) {
+        // BN-backward partials of the stored gradient dy: dz = dy * [bf16(relu(x sc + sh)) > 0]
+        // (the mask exactly as bn_apply stored the ReLU output), sum dz, sum dz * xhat
+        if (ok) {
+          const uint2 xr = *reinterpret_cast<const uint2*>(a.bnx + orow * a.ldc + n);
+          const float xv[4] = {__uint_as_float(xr.x << 16), __uint_as_float(xr.x & 0xffff0000u),
+                               __uint_as_float(xr.y << 16), __uint_as_float(xr.y & 0xffff0000u)};
+          const float4 mu = *reinterpret_cast<const float4*>(a.bnst + n);
+          const float4 iv = *reinterpret_cast<const float4*>(a.bnst + a.N + n);
+          const float4 sc = *reinterpret_cast<const float4*>(a.bnst + 2 * a.N + n);
+          const float4 sh = *reinterpret_cast<const float4*>(a.bnst + 3 * a.N + n);
+          const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w};
+          const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, h4[4] = {sh.x, sh.y, sh.z, sh.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float y = bf2f(f2bf(fmaxf(fmaf(xv[e], s4[e], h4[e]), 0.f)));
+            const float d = y > 0.f ? bf2f(f2bf(v[e])) : 0.f;
+            csum[j][e] += d;
+            csq[j][e] += d * (xv[e] - m4[e]) * i4[e];
+          }
+        }
+      }
       if constexpr (EPI & E_RELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -148,7 +170,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       }
     }
   }
-  if constexpr (EPI & E_STATS) {
+  if constexpr ((EPI & (E_STATS | E_BNRED)) != 0) {
     // reduce over the 16 rows held by lanes l&15 (xor 1,2,4,8), then over the wave grid's
     // M direction through LDS; one partial per column per M-tile: stats[tm][z][2][N]
 #pragma unroll

@@ -389,6 +389,9 @@ hipError_t launch3_epi(const GemmArgs& a, int epi, int R, hipStream_t s) {
     case E_BF16 | E_STATS: return launch3<BN, DG, E_BF16 | E_STATS>(a, R, s);
     case E_BIAS | E_BF16 | E_STATS: return launch3<BN, DG, E_BIAS | E_BF16 | E_STATS>(a, R, s);
     case E_BF16 | E_ADD: return launch3<BN, DG, E_BF16 | E_ADD>(a, R, s);
+    case E_BF16 | E_BNRED:
+      if constexpr (DG) return launch3<BN, DG, E_BF16 | E_BNRED>(a, R, s);
+      return hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }

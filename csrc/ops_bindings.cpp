@@ -29,9 +29,11 @@ void register_kernel_ops(py::module_& m) {
       "gemm",
       [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,
          uintptr_t stats, uintptr_t R, int M, int N, int K, int lda, int ldb, int ldc, std::vector<int> geo, int kc,
-         int k_per_split, uintptr_t stream, int kstep, uintptr_t stats_acc) {
+         int k_per_split, uintptr_t stream, int kstep, uintptr_t stats_acc, uintptr_t bnx, uintptr_t bnst) {
         damd::GemmArgs a{};
         a.stats_acc = P_<double>(stats_acc);
+        a.bnx = P_<const uint16_t>(bnx);
+        a.bnst = P_<const float>(bnst);
         a.A = P_<const void>(A);
         a.B = P_<const void>(B);
         a.C = P_<void>(C);
@@ -54,7 +56,7 @@ void register_kernel_ops(py::module_& m) {
       py::arg("amode"), py::arg("bmode"), py::arg("epi"), py::arg("splits"), py::arg("tile"), py::arg("A"),
       py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("stats"), py::arg("R"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
-      py::arg("stream"), py::arg("kstep") = 0, py::arg("stats_acc") = 0);
+      py::arg("stream"), py::arg("kstep") = 0, py::arg("stats_acc") = 0, py::arg("bnx") = 0, py::arg("bnst") = 0);
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
   m.def("conv_gemm_kstep", &damd::conv_gemm_kstep);
   m.def("conv3_rows", &damd::conv3_rows);

@@ -507,6 +507,7 @@ class NativeGraphEngine(Engine):
                 if _act_name(l) != "linear":
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
         self._plan_bn_fin()
+        self._plan_bn_dgrad_fusion()
         # one scratch bf16 buffer for "second writer" gradient accumulation
         big = max([int(np.prod(t.shape)) for t in self._all_tensors()] + [1])
         self.scratch = torch.zeros(big, dtype=torch.bfloat16, device=dev)
@@ -541,6 +542,31 @@ class NativeGraphEngine(Engine):
             nd.attrs["fin"] = H.BNFin(nd.attrs["acc_f"], self._view_or_none(l.gamma), self._view_or_none(l.beta),
                                       nd.attrs["st"], l.moving_mean.value, l.moving_variance.value, M, l.epsilon,
                                       l.momentum)
+
+    def _plan_bn_dgrad_fusion(self):
+        """BN -> ReLU -> Conv2D with the conv as the ReLU output's only consumer (the first
+        conv of every ResNet basic block's second half): the conv's backprop-input, when the
+        direct 3x3 kernel runs it, also writes the BN-backward partials in its epilogue
+        (E_BNRED), so that BN's backward skips its reduce pass (one read of dy and x less)."""
+        if not env.get_bool("DAMD_BN_DGRAD_FUSE", True) or not env.get_bool("DAMD_BN_MASK_FROM_X", True):
+            return
+        for bn in self.nodes:
+            a = bn.attrs
+            if (bn.kind != "BatchNormalization" or a.get("dead") or not a.get("relu") or a.get("stats_only")
+                    or a.get("pool") is not None or a.get("fin") is not None):
+                continue
+            outs = bn.out.consumers
+            if len(outs) != 1 or not outs[0].attrs.get("dead") or len(outs[0].out.consumers) != 1:
+                continue
+            conv = outs[0].out.consumers[0]
+            if conv.kind != "Conv2D" or conv.attrs.get("dead") or "w_pad" in conv.attrs:
+                continue
+            l = conv.layer
+            plan = H.conv_dgrad_plan(bn.out.shape, tuple(l.kernel.shape), l.strides, l.padding)
+            if plan["amode"] != H.A_DGRAD3:
+                continue
+            a["dgrad_part"] = torch.zeros(plan["stats_T"], 2, bn.out.shape[-1], device=self.device)
+            conv.attrs["bnred"] = bn
 
     def _view_or_none(self, var):
         return self.views[id(var)] if var is not None else None
@@ -967,7 +993,17 @@ class NativeGraphEngine(Engine):
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written
             xt.written = True
-            H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
+            bn = nd.attrs.get("bnred")
+            if bn is not None:
+                # first (only) writer of the BN -> ReLU output gradient: the BN-backward
+                # partials come out of this launch's epilogue
+                bn.attrs["dgrad_fused"] = not acc and H.conv_dgrad(
+                    dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws,
+                    bnred=(bn.inputs[0].root().buf, bn.attrs["st"], bn.attrs["dgrad_part"]))
+                if acc:
+                    H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
+            else:
+                H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
 
     def _bn_backward(self, bn, dy, ymask, relu, dz_out=None, mask_from_x=False):
         """BatchNorm backward of node ``bn`` for upstream gradient dy (masked by
@@ -993,8 +1029,12 @@ class NativeGraphEngine(Engine):
             if fin:
                 fin()
             return
-        C_.bn_bwd_reduce(dy.data_ptr(), ym, mode, x.buf.data_ptr(), st.data_ptr(),
-                         dz_out.data_ptr() if (dz_out is not None and relu) else 0, part.data_ptr(), Tn, M, C, s)
+        if bn.attrs.get("dgrad_fused") and mode == 2 and dz_out is None:
+            part = bn.attrs["dgrad_part"]  # written by the consuming conv's backprop-input epilogue
+            Tn = part.shape[0]
+        else:
+            C_.bn_bwd_reduce(dy.data_ptr(), ym, mode, x.buf.data_ptr(), st.data_ptr(),
+                             dz_out.data_ptr() if (dz_out is not None and relu) else 0, part.data_ptr(), Tn, M, C, s)
         C_.bn_bwd_finalize(part.data_ptr(), Tn, C, float(M), st.data_ptr(), 0,
                            self.gviews[id(l.gamma)].data_ptr() if l.gamma is not None else 0,
                            self.gviews[id(l.beta)].data_ptr() if l.beta is not None else 0, co.data_ptr(), s)

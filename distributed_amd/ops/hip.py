@@ -24,7 +24,7 @@ from ..native import require_C
 
 A_KC, A_IM2COL, A_DGRAD, A_MC, A_WGRAD, A_CONV64, A_DGRAD64, A_WGRAD64, A_WGRAD3, A_CONV3, A_DGRAD3 = range(11)
 B_NC, B_KC = 0, 1
-E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB = 1, 2, 4, 8, 16, 32, 64
+E_BIAS, E_RELU, E_BF16, E_ATOMIC, E_STATS, E_ADD, E_SLAB, E_BNRED = 1, 2, 4, 8, 16, 32, 64, 128
 BK = 32
 
 
@@ -259,12 +259,12 @@ def _stats_ptrs(stats):
 
 
 def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
-         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0):
+         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0, bnx=None, bnst=None):
     t = pick_tile(N) if tile is None else tile
     kps = k_per_split if k_per_split is not None else -(-K // BK) * BK
     sp, sa = _stats_ptrs(stats)
     _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), sp, _ptr(R), M, N, K,
-              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep, stats_acc=sa)
+              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep, stats_acc=sa, bnx=_ptr(bnx), bnst=_ptr(bnst))
 
 
 # ---- dense -------------------------------------------------------------------------------
@@ -560,7 +560,8 @@ def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
     M, N, K = n * h * wd, cin, kh * kw * cout
     c3 = conv3_tile(n, h, wd, cout, cin) if (kh == kw == 3 and s == 1 and pad == 1 and ho == h) else None
     if c3 is not None:
-        return {"M": M, "N": N, "K": K, "tile": c3[0], "splits": 1, "kps": K, "amode": A_DGRAD3, "ws": 0}
+        return {"M": M, "N": N, "K": K, "tile": c3[0], "splits": 1, "kps": K, "amode": A_DGRAD3, "ws": 0,
+                "stats_T": n * c3[2]}
     t = pick_tile(N)
     if (s == 2 and use_glds(cout) and h % 2 == 0 and wd % 2 == 0 and pad == 0
             and os.environ.get("DAMD_DGRAD_SUBPIX", "1") != "0"):
@@ -575,8 +576,12 @@ def conv_dgrad_plan(dx_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
 
 
 def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
-               workspace: Optional[torch.Tensor] = None):
-    """dx [N,H,W,Cin] (+)= backprop-input of dy [N,Ho,Wo,Cout] through w."""
+               workspace: Optional[torch.Tensor] = None, bnred=None) -> bool:
+    """dx [N,H,W,Cin] (+)= backprop-input of dy [N,Ho,Wo,Cout] through w.  ``bnred`` =
+    (x, st, part): dx is the gradient of relu(BN(x)) (BN coefficients st [4][Cin]); when the
+    direct kernel runs (conv_dgrad_plan stats_T rows) it also writes the BN-backward
+    partials (sum dz, sum dz * xhat per tile) into part [stats_T][2][Cin], replacing
+    bn_bwd_reduce.  Returns True when it did."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx.shape, w.shape, strides, padding)
     if s not in (1, 2):
         raise ValueError("conv_dgrad: stride 1 or 2")
@@ -588,16 +593,24 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
     plan = conv_dgrad_plan(dx.shape, w.shape, strides, padding)
     M, K = plan["M"], plan["K"]
     geo = (h, wd, cout, ho, wo, kh, kw, s, pad)
+    if bnred is not None and plan["amode"] == A_DGRAD3 and not accumulate:
+        bx, bst, part = bnred
+        if part.shape[0] != plan["stats_T"] or tuple(bx.shape) != tuple(dx.shape):
+            raise ValueError("conv_dgrad: bnred partials / BN input do not match the plan")
+        gemm(dy, w, dx, amode=A_DGRAD3, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_BF16 | E_BNRED, kc=cout,
+             geo=geo, stats=part, tile=plan["tile"], bnx=bx, bnst=bst)
+        return True
     if plan["splits"] == 1:
         epi = E_BF16 | (E_ADD if accumulate else 0)
         gemm(dy, w, dx, amode=plan["amode"], bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=epi, kc=cout, geo=geo,
              R=dx if accumulate else None, tile=plan["tile"])
-        return
+        return False
     ws = _workspace(workspace, plan["ws"], dx.device)
     gemm(dy, w, ws, amode=plan["amode"], bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_SLAB, kc=cout, geo=geo,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"])
     _C().splitk_finish(_ptr(ws), plan["splits"], M, cin, 0, _ptr(dx) if accumulate else 0, 0, 0, FINISH_RB,
                        _ptr(dx), cin, stream_handle())
+    return False
 
 
 def conv_wgrad_workspace_elems(x_shape, w_shape, strides=(1, 1), padding="valid") -> int:

@@ -362,6 +362,30 @@ def test_bn_fin_matches_partials_finalize():
     np.testing.assert_allclose(ha["loss"], hb["loss"], rtol=1e-5)
 
 
+def test_bn_backward_reduce_fused_into_dgrad_epilogue(monkeypatch):
+    """BN -> ReLU -> Conv2D: the conv's direct backprop-input kernel writes the BN-backward
+    partials in its epilogue (DAMD_BN_DGRAD_FUSE, default) == the separate bn_bwd_reduce
+    pass: two momentum steps of a ResNet whose 64-channel 16x16 stage runs the direct 3x3
+    kernel (DAMD_CONV3_MIN_WG=1 admits the small grid)."""
+    from distributed_amd.ops import hip as H
+
+    def build():
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    assert H.conv_dgrad_plan((32, 16, 16, 64), (3, 3, 64, 64), (1, 1), "same")["amode"] == H.A_DGRAD3
+    x, y = _data(64, (64, 64, 3), 10, seed=9)
+    tf.keras.backend.clear_session()
+    init = build().get_weights()
+    fused, hf, ef = _train(build, x, y, init, 32, 2, native=True, momentum=0.9)
+    unfused, hu, eu = _train(build, x, y, init, 32, 2, native=True, momentum=0.9,
+                             extra_env={"DAMD_BN_DGRAD_FUSE": "0"})
+    assert ef == eu == "native_graph"
+    for a, b in zip(fused, unfused):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
+    np.testing.assert_allclose(hf["loss"], hu["loss"], rtol=1e-5)
+
+
 def test_resnet18_full_size_trains():
     x, y = _data(64, (224, 224, 3), 1000, seed=3)
     tf.keras.backend.clear_session()
