@@ -438,3 +438,33 @@ def test_direct_conv3(H, monkeypatch, n, h, cin, cout, stationary):
     dx2 = base.bfloat16().contiguous()
     H.conv_dgrad(dyb, wb, dx2, (1, 1), "same", accumulate=True)
     close(dx2, gx + base, 1e-2, 4e-3)
+
+
+@pytest.mark.parametrize("n,h,cin,cout", [(2, 56, 64, 64), (2, 28, 128, 128), (2, 14, 256, 256), (32, 16, 64, 64)])
+def test_direct_conv3_dgrad_bnred(H, monkeypatch, n, h, cin, cout):
+    """Backprop-input with the BN-backward epilogue (E_BNRED): dx bitwise == the plain
+    direct kernel's, and the per-tile partials sum to sum(dz), sum(dz * xhat) with
+    dz = bf16(dx) * [bf16(relu(x sc + sh)) > 0] (fp32 reference)."""
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    monkeypatch.setenv("DAMD_CONV3W", "0")
+    shape = (n, h, h, cin)
+    dplan = H.conv_dgrad_plan(shape, (3, 3, cin, cout), (1, 1), "same")
+    assert dplan["amode"] == H.A_DGRAD3
+    wb = rb(rnd(3, 3, cin, cout, scale=0.05, seed=21)).bfloat16()
+    dyb = rb(rnd(n, h, h, cout, seed=22)).bfloat16()
+    xb = rb(rnd(*shape, scale=2.0, seed=23)).bfloat16()
+    st = torch.stack([rnd(cin, seed=24) * 0.1, rnd(cin, seed=25).abs() + 0.5,
+                      rnd(cin, seed=26).abs() + 0.5, rnd(cin, seed=27)]).float().contiguous()
+    dx0 = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+    assert not H.conv_dgrad(dyb, wb, dx0, (1, 1), "same")
+    dx = torch.empty_like(dx0)
+    part = torch.full((dplan["stats_T"], 2, cin), float("nan"), device=dev)
+    assert H.conv_dgrad(dyb, wb, dx, (1, 1), "same", bnred=(xb, st, part))
+    assert torch.equal(dx, dx0)
+    assert not torch.isnan(part).any()
+    x32 = xb.float().reshape(-1, cin)
+    mask = rb(torch.relu(x32 * st[2] + st[3])) > 0
+    dz = dx.float().reshape(-1, cin) * mask
+    xhat = (x32 - st[0]) * st[1]
+    close(part[:, 0].sum(0), dz.sum(0), 1e-3, 1e-4)
+    close(part[:, 1].sum(0), (dz * xhat).sum(0), 1e-3, 1e-4)

@@ -365,8 +365,13 @@ def test_bn_fin_matches_partials_finalize():
 def test_bn_backward_reduce_fused_into_dgrad_epilogue(monkeypatch):
     """BN -> ReLU -> Conv2D: the conv's direct backprop-input kernel writes the BN-backward
     partials in its epilogue (DAMD_BN_DGRAD_FUSE, default) == the separate bn_bwd_reduce
-    pass: two momentum steps of a ResNet whose 64-channel 16x16 stage runs the direct 3x3
-    kernel (DAMD_CONV3_MIN_WG=1 admits the small grid)."""
+    pass: one step of a ResNet whose 64-channel 16x16 stage runs the direct 3x3 kernel
+    (DAMD_CONV3_MIN_WG=1 admits the small grid).  One step: the partials differ from
+    bn_bwd_reduce's only in fp32 summation order (~1e-6 relative in the updates), but this
+    net's bf16 second step amplifies such perturbations (maxpool / ReLU decisions on
+    near-ties) to several percent for some random inits, for any two summation orders
+    (scripts/diag_bnred3.py); the partials themselves are pinned to an fp32 reference in
+    test_conv_gemm_gpu.py::test_direct_conv3_dgrad_bnred."""
     from distributed_amd.ops import hip as H
 
     def build():
@@ -377,9 +382,8 @@ def test_bn_backward_reduce_fused_into_dgrad_epilogue(monkeypatch):
     x, y = _data(64, (64, 64, 3), 10, seed=9)
     tf.keras.backend.clear_session()
     init = build().get_weights()
-    fused, hf, ef = _train(build, x, y, init, 32, 2, native=True, momentum=0.9)
-    unfused, hu, eu = _train(build, x, y, init, 32, 2, native=True, momentum=0.9,
-                             extra_env={"DAMD_BN_DGRAD_FUSE": "0"})
+    fused, hf, ef = _train(build, x, y, init, 32, 1, native=True)
+    unfused, hu, eu = _train(build, x, y, init, 32, 1, native=True, extra_env={"DAMD_BN_DGRAD_FUSE": "0"})
     assert ef == eu == "native_graph"
     for a, b in zip(fused, unfused):
         np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
