@@ -170,25 +170,35 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
       const char* ib = ring + stage * B_ST;
       const int kh = tap / 3, kw = tap - kh * 3;
       const int toff = DGRAD ? (2 - kh) * HW + (2 - kw) : kh * HW + kw;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[4], bfr[4];
+      // both 32-deep k-steps' fragments in distinct registers: all of k-step 0's LDS reads
+      // are issued before its MFMAs, k-step 1's overlap them (left to itself the scheduler
+      // reused one A register quad, i.e. one LDS round trip per 4 MFMAs)
+      bf16x8 af[2][4], bfr[2][4];
+      auto load = [&](int kk) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int q = hbase[i] + toff, c = 4 * kk + (lane >> 4);
-          af[i] = *reinterpret_cast<const bf16x8*>(halo + q * 128 + 16 * (c ^ (q & 7)));
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(halo + q * 128 + 16 * (c ^ (q & 7)));
           if constexpr (DGRAD) {
             const int r = wn * 64 + i * 16 + (lane & 15);
-            bfr[i] = *reinterpret_cast<const bf16x8*>(ib + r * 128 + 16 * (c ^ kc64_swz(r)));
+            bfr[kk][i] = *reinterpret_cast<const bf16x8*>(ib + r * 128 + 16 * (c ^ kc64_swz(r)));
           } else {
-            bfr[i] = tile::frag_mc<BN>(ib + kk * 32 * BN * 2, wn * 64 + i * 16, lane);
+            bfr[kk][i] = tile::frag_mc<BN>(ib + kk * 32 * BN * 2, wn * 64 + i * 16, lane);
           }
         }
+      };
+      auto mma = [&](int kk) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-      }
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[kk][j], af[kk][i], acc[i][j]);
+      };
+      load(0);
+      __builtin_amdgcn_sched_barrier(0);
+      load(1);
+      mma(0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma(1);
     };
     tap_loop<STAGES, NB>(issue, compute);
   }
