@@ -220,6 +220,121 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x,
   }
 }
 
+// Row-mapped apply kernels (no in-consumer finalize): thread t keeps channel group
+// t % (C/8) for the whole launch, so its per-channel coefficients are loaded once into
+// registers instead of once per 16-byte data vector (the flat kernels above fetched 2-7
+// coefficient vectors per data vector); BN_UNR rows per thread in flight.  Same arithmetic,
+// bitwise equal output.  Measured on ResNet-18: backward apply 9.9 -> 8.8 us per launch,
+// forward apply unchanged (already at HBM rate); the same unrolling of bn_bwd_reduce_k's
+// row loop was slower (8.6 -> 9.5 us) and is not used.
+constexpr int BN_UNR = 4;
+__global__ __launch_bounds__(NT) void bn_apply_rows_k(const uint16_t* __restrict__ x, const float* __restrict__ st,
+                                                      const uint16_t* __restrict__ r, const float* __restrict__ st2,
+                                                      int res_mode, int relu, uint16_t* __restrict__ y, long M, int C) {
+  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;
+  const int g = t % cg, rr = t / cg, c = g * 8;
+  if (rr >= rpi) return;
+  float sc[8], sh[8], sc2[8], sh2[8];
+  ld8f(st + 2 * C + c, sc);
+  ld8f(st + 3 * C + c, sh);
+  if (res_mode == 2) {
+    ld8f(st2 + 2 * C + c, sc2);
+    ld8f(st2 + 3 * C + c, sh2);
+  }
+  const long stride = (long)gridDim.x * rpi;
+  const uint4* x4 = reinterpret_cast<const uint4*>(x);
+  const uint4* r4 = reinterpret_cast<const uint4*>(r);
+  uint4* y4 = reinterpret_cast<uint4*>(y);
+  for (long row0 = (long)blockIdx.x * rpi + rr; row0 < M; row0 += stride * BN_UNR) {
+    uint4 xq[BN_UNR], rq[BN_UNR];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = min(row0 + u * stride, M - 1);
+      xq[u] = x4[row * cg + g];
+      if (res_mode) rq[u] = r4[row * cg + g];
+    }
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = row0 + u * stride;
+      if (row >= M) break;
+      float xv[8];
+      unpack8(xq[u], xv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) xv[e] = fmaf(xv[e], sc[e], sh[e]);
+      if (res_mode) {
+        float rv[8];
+        unpack8(rq[u], rv);
+        if (res_mode == 2) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) rv[e] = rv[e] * sc2[e] + sh2[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] += rv[e];
+      }
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = fmaxf(xv[e], 0.f);
+      }
+      y4[row * cg + g] = pack8(xv);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT) void bn_bwd_apply_rows_k(const uint16_t* __restrict__ dy,
+                                                          const uint16_t* __restrict__ y, int relu_mask,
+                                                          const uint16_t* __restrict__ x, const float* __restrict__ st,
+                                                          const float* __restrict__ co, uint16_t* __restrict__ dx,
+                                                          long M, int C) {
+  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;
+  const int g = t % cg, rr = t / cg, c = g * 8;
+  if (rr >= rpi) return;
+  float mean[8], inv[8], a[8], b[8], cc[8], sc[8], sh[8];
+  ld8f(st + c, mean);
+  ld8f(st + C + c, inv);
+  ld8f(co + c, a);
+  ld8f(co + C + c, b);
+  ld8f(co + 2 * C + c, cc);
+  if (relu_mask == 2) {
+    ld8f(st + 2 * C + c, sc);
+    ld8f(st + 3 * C + c, sh);
+  }
+  const long stride = (long)gridDim.x * rpi;
+  const uint4* d4 = reinterpret_cast<const uint4*>(dy);
+  const uint4* x4 = reinterpret_cast<const uint4*>(x);
+  const uint4* y4 = reinterpret_cast<const uint4*>(y);
+  uint4* o4 = reinterpret_cast<uint4*>(dx);
+  for (long row0 = (long)blockIdx.x * rpi + rr; row0 < M; row0 += stride * BN_UNR) {
+    uint4 dq[BN_UNR], xq[BN_UNR], yq[BN_UNR];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = min(row0 + u * stride, M - 1);
+      dq[u] = d4[row * cg + g];
+      xq[u] = x4[row * cg + g];
+      if (relu_mask == 1) yq[u] = y4[row * cg + g];
+    }
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = row0 + u * stride;
+      if (row >= M) break;
+      float d[8], xv[8];
+      unpack8(dq[u], d);
+      unpack8(xq[u], xv);
+      if (relu_mask) {
+        float yv[8];
+        if (relu_mask == 2)
+          bn_relu8(xv, sc, sh, yv);
+        else
+          unpack8(yq[u], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] = a[e] * d[e] + b[e] + cc[e] * (xv[e] - mean[e]) * inv[e];
+      o4[row * cg + g] = pack8(d);
+    }
+  }
+}
+
 // dz = dy * [y>0]; partial sums of dz and dz*xhat per channel for a contiguous row range
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
                                                       int relu_mask, const uint16_t* __restrict__ x,
@@ -1519,6 +1634,13 @@ hipError_t bn_finalize(const float* part, int T, int C, float count, const float
   return hipGetLastError();
 }
 
+// row-mapped apply kernels: about BN_UNR rows per thread (one batch of loads in flight)
+static int rows_grid(long M, int C) {
+  const long rpi = NT / (C / 8);
+  long g = (M + rpi * BN_UNR - 1) / (rpi * BN_UNR);
+  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+}
+
 // blocks of a consumer that finalizes in its prologue: every block pays one pass over the
 // C channels, so the grid-stride kernels run at most 8 blocks per CU
 constexpr int FIN_GRID_CAP = 2048;
@@ -1534,6 +1656,10 @@ hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const
   const size_t lds = (a.acc ? 4 * C * sizeof(float) : 0) + (b.acc ? 4 * C * sizeof(float) : 0);
   // (the f2 region starts at 4C: allocate it whenever f2 finalizes)
   const size_t lds2 = b.acc ? 8 * C * sizeof(float) : lds;
+  if (!a.acc && !b.acc && NT % (C / 8) == 0) {
+    hipLaunchKernelGGL(bn_apply_rows_k, dim3(rows_grid(M, C)), dim3(NT), 0, s, x, st, r, st2, res_mode, relu, y, M, C);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(n8, NT, (a.acc || b.acc) ? FIN_GRID_CAP : 8192)), dim3(NT), lds2, s,
                      x, st, r, st2, res_mode, relu, y, n8, C, a, b);
   return hipGetLastError();
@@ -1569,6 +1695,11 @@ hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, co
   const long n8 = M * C / 8;
   const BNBwdFin f = bf ? *bf : kNoBwdFin;
   if (f.acc && (!f.co || C > FIN_MAX_C)) return hipErrorInvalidValue;
+  if (!f.acc && NT % (C / 8) == 0) {
+    hipLaunchKernelGGL(bn_bwd_apply_rows_k, dim3(rows_grid(M, C)), dim3(NT), 0, s, dy, y, relu_mask, x, st, co, dx, M,
+                       C);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(bn_bwd_apply_k, dim3(grid_for(n8, NT, f.acc ? FIN_GRID_CAP : 8192)), dim3(NT),
                      f.acc ? 3 * C * sizeof(float) : 0, s, dy, y, relu_mask, x, st, co, dx, n8, C, f);
   return hipGetLastError();
