@@ -143,11 +143,16 @@ class ConvNetTrainer : public StepExecutor {
     if (b_.kernels == 2) HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
     else HIP_CHECK(convnet_launch_flush(b_, PP_, stream_));
   }
+  // timed runs: k steps + the flush of the last deferred update as one graph
+  void capture_final(int k) { StepExecutor::capture_final(k); }
+  bool run_final(int k) { return StepExecutor::run_final(k); }
+  bool warm_final(int k) { return StepExecutor::warm_final(k); }
   int kernels() const { return b_.kernels; }
   int num_slices() const { return convnet_num_slices(PP_); }
   int batch() const { return B_; }
 
  protected:
+  void enqueue_tail() override { flush(); }
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     if (b_.kernels == 2) HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
@@ -267,6 +272,9 @@ PYBIND11_MODULE(_C, m) {
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
       .def("capture", &ConvNetTrainer::capture)
       .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
+      .def("capture_final", &ConvNetTrainer::capture_final, py::arg("steps"))
+      .def("run_final", &ConvNetTrainer::run_final, py::arg("steps"), py::call_guard<py::gil_scoped_release>())
+      .def("warm_final", &ConvNetTrainer::warm_final, py::arg("steps"), py::call_guard<py::gil_scoped_release>())
       .def("run_persistent", &ConvNetTrainer::run_persistent, py::arg("steps"), py::arg("timeout_s") = 5.0,
            py::call_guard<py::gil_scoped_release>())
       .def("phase_times", &ConvNetTrainer::phase_times, py::arg("steps"), py::call_guard<py::gil_scoped_release>())

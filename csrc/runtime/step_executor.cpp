@@ -2,6 +2,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace damd {
 
@@ -28,19 +29,23 @@ StepExecutor::~StepExecutor() {
 
 void StepExecutor::invalidate_graphs() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  for (auto& kv : finals_) hipGraphExecDestroy(kv.second);
+  for (auto& kv : final_graphs_) hipGraphDestroy(kv.second);
   graphs_.clear();
+  finals_.clear();
+  final_graphs_.clear();
 }
 
 void StepExecutor::step(int k) {
   for (int i = 0; i < k; ++i) enqueue_one_step();
 }
 
-void StepExecutor::capture(int k) {
-  if (k <= 0 || graphs_.count(k)) return;
+hipGraphExec_t StepExecutor::capture_steps(int k, bool tail, hipGraph_t* keep) {
   hipGraph_t g = nullptr;
   HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
     for (int i = 0; i < k; ++i) enqueue_one_step();
+    if (tail) enqueue_tail();
   } catch (...) {
     hipStreamEndCapture(stream_, &g);
     if (g) hipGraphDestroy(g);
@@ -49,12 +54,49 @@ void StepExecutor::capture(int k) {
   HIP_CHECK(hipStreamEndCapture(stream_, &g));
   hipGraphExec_t ge = nullptr;
   hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-  hipGraphDestroy(g);
+  if (keep && e == hipSuccess) *keep = g;
+  else hipGraphDestroy(g);
   HIP_CHECK(e);
   // upload now, so the first replay inside a timed loop does not pay for it
   HIP_CHECK(hipGraphUpload(ge, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
-  graphs_[k] = ge;
+  return ge;
+}
+
+void StepExecutor::capture(int k) {
+  if (k <= 0 || graphs_.count(k)) return;
+  graphs_[k] = capture_steps(k, false);
+}
+
+void StepExecutor::capture_final(int k) {
+  if (k <= 0 || finals_.count(k)) return;
+  hipGraph_t g = nullptr;
+  finals_[k] = capture_steps(k, true, &g);
+  final_graphs_[k] = g;
+}
+
+bool StepExecutor::warm_final(int k) {
+  auto it = finals_.find(k);
+  auto gt = final_graphs_.find(k);
+  if (it == finals_.end() || gt == final_graphs_.end()) return false;
+  size_t n = 0;
+  if (hipGraphGetNodes(gt->second, nullptr, &n) != hipSuccess || n == 0) return false;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (hipGraphGetNodes(gt->second, nodes.data(), &n) != hipSuccess) return false;
+  size_t off = 0;
+  bool ok = true;
+  for (; off < n && ok; ++off) ok = hipGraphNodeSetEnabled(it->second, nodes[off], 0) == hipSuccess;
+  if (ok) ok = hipGraphLaunch(it->second, stream_) == hipSuccess && hipStreamSynchronize(stream_) == hipSuccess;
+  for (size_t i = 0; i < off; ++i) HIP_CHECK(hipGraphNodeSetEnabled(it->second, nodes[i], 1));
+  (void)hipGetLastError();
+  return ok;
+}
+
+bool StepExecutor::run_final(int k) {
+  auto it = finals_.find(k);
+  if (it == finals_.end()) return false;
+  HIP_CHECK(hipGraphLaunch(it->second, stream_));
+  return true;
 }
 
 void StepExecutor::run(int k) {

@@ -35,6 +35,14 @@ class StepExecutor {
   void capture(int k);
   // Run k steps: greedily replay the largest captured graph <= remaining, eager tail.
   void run(int k);
+  // k steps followed by enqueue_tail() (e.g. the deferred-update flush) as ONE graph:
+  // a timed run of k steps is then one replay (a graph boundary costs ~4.5 us, an eager
+  // launch after a graph ~10 us).  run_final returns false if no such graph was captured.
+  void capture_final(int k);
+  bool run_final(int k);
+  // One replay of the final graph with every node disabled (nothing executes): pays the
+  // first-launch cost of the graph outside a timed window.  False if unsupported.
+  bool warm_final(int k);
   // Block until the stream drains; false on watchdog timeout (comm aborted).
   bool sync(double timeout_s);
   void invalidate_graphs();
@@ -42,6 +50,7 @@ class StepExecutor {
 
  protected:
   virtual void enqueue_one_step() = 0;
+  virtual void enqueue_tail() {}
   hipStream_t stream_ = nullptr;
   RcclComm* comm_ = nullptr;
   PeerAllreduce* peer_ = nullptr;
@@ -49,6 +58,9 @@ class StepExecutor {
 
  private:
   std::map<int, hipGraphExec_t> graphs_;
+  std::map<int, hipGraphExec_t> finals_;
+  std::map<int, hipGraph_t> final_graphs_;  // kept for the node handles (warm_final)
+  hipGraphExec_t capture_steps(int k, bool tail, hipGraph_t* keep = nullptr);
 };
 
 }  // namespace damd

