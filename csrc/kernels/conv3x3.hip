@@ -49,14 +49,31 @@ using tile::glds16;
 // k-contiguous [rows][64] image swizzle (conv_gemm.hip kc_swz<64>)
 __device__ __forceinline__ int kc64_swz(int r) { return r & 7; }
 
-template <int STAGES, int NQ, class Issue, class Compute>
-__device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute) {
-  constexpr int NK = 9;
+// halo prefetch of the next 64-channel chunk (double-buffered halo): LDS-DMA instructions
+// per wave, uniform so that the stage waits can count them
+constexpr int C3_HQ = 6;
+
+// pf: issue prefetch() after tap KH's weight stage; the stage waits of the later taps then
+// leave those C3_HQ newer DMA instructions in flight
+template <int STAGES, int NQ, class Issue, class Compute, class Prefetch>
+__device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute, Prefetch& prefetch, bool pf) {
+  constexpr int NK = 9, KH = NK - STAGES;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s, s);
   for (int kt = 0; kt < NK; ++kt) {
     const int ahead = min(NK - 1 - kt, STAGES - 2);
-    if constexpr (STAGES >= 4) {
+    if (pf && kt > KH) {
+      if constexpr (STAGES >= 4) {
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQ + C3_HQ) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ + C3_HQ) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C3_HQ) : "memory");
+      } else if constexpr (STAGES == 3) {
+        if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ + C3_HQ) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C3_HQ) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C3_HQ) : "memory");
+      }
+    } else if constexpr (STAGES >= 4) {
       if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQ) : "memory");
       else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -69,6 +86,7 @@ __device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + STAGES - 1 < NK) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
+    if (pf && kt == KH) prefetch();
     compute(kt % STAGES, kt);
   }
 }
@@ -78,7 +96,7 @@ __device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute) {
 // (% 64), N = output channels (% BN); H, W the (shared) image size.  R output rows per
 // block, tpi = ceil(H / R) row blocks per image; grid (N / BN, Nimg * tpi).
 template <int BN, bool DGRAD, int EPI, int STAGES>
-__global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi) {
+__global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi, int hb2) {
   const bool stamps = g_c3_on != 0;
   unsigned long long st0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, st1 = 0ull, st2 = 0ull;
   constexpr int WN = BN / 64, WM = 4 / WN, BM = WM * 64;
@@ -90,8 +108,11 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
   const int HW = W + 2;
   const int hpix = (R + 2) * HW;
   const int halo_bytes = (hpix * 128 + 1023) & ~1023;
+  // hb2: two halo buffers (+ a 1 KiB sink for the padding DMA instructions): the next
+  // chunk's halo is fetched by LDS-DMA during the current chunk's last taps
   char* halo = smem;
-  char* ring = smem + halo_bytes;
+  char* sink = smem + 2 * halo_bytes;
+  char* ring = smem + (hb2 ? 2 * halo_bytes + 1024 : halo_bytes);
 
   const int tn = blockIdx.x, tm = blockIdx.y;
   const int img = tm / tpi, oh0 = (tm - img * tpi) * R;
@@ -141,20 +162,35 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = SC / 64;
+  // halo instruction j (all 64 lanes): pixel q = 8j + lane / 8, 16-byte slot lane & 7 of
+  // the swizzled image -> source (zeros outside the image / past the halo)
+  auto halo_src = [&](int j, int c0) __attribute__((always_inline)) -> const void* {
+    const int q = 8 * j + (lane >> 3);
+    const int hr = q / HW, hc = q - hr * HW;
+    const int ih = oh0 - 1 + hr, iw = hc - 1;
+    const bool ok = q < hpix && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+    const int cs = (lane & 7) ^ (q & 7);
+    return ok ? (const void*)(img_base + ((long)ih * W + iw) * SC + c0 + 8 * cs) : zero;
+  };
+  const bool pf_on = hb2 && nchunks > 1 && nhi <= 4 * C3_HQ;
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     const int c0 = chunk * 64;
+    char* hcur = halo + (pf_on ? (chunk & 1) * halo_bytes : 0);
     if (chunk) {  // every wave is done with the previous halo and weight stages
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     }
-    for (int j = wave; j < nhi; j += 4) {
-      const int q = 8 * j + (lane >> 3);
-      const int hr = q / HW, hc = q - hr * HW;
-      const int ih = oh0 - 1 + hr, iw = hc - 1;
-      const bool ok = q < hpix && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      const int cs = (lane & 7) ^ (q & 7);
-      glds16(ok ? (const void*)(img_base + ((long)ih * W + iw) * SC + c0 + 8 * cs) : zero, halo + j * 1024);
-    }
+    if (chunk == 0 || !pf_on)
+      for (int j = wave; j < nhi; j += 4) glds16(halo_src(j, c0), hcur + j * 1024);
+    // the next chunk's halo into the other buffer, from tap KH on
+    auto prefetch = [&]() __attribute__((always_inline)) {
+      char* nb = halo + ((chunk + 1) & 1) * halo_bytes;
+#pragma unroll
+      for (int u = 0; u < C3_HQ; ++u) {
+        const int j = wave + 4 * u;
+        glds16(halo_src(j, c0 + 64), j < nhi ? nb + j * 1024 : sink);
+      }
+    };
     auto issue = [&](int stage, int tap) __attribute__((always_inline)) {
       char* sb = ring + stage * B_ST;
 #pragma unroll
@@ -178,7 +214,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int q = hbase[i] + toff, c = 4 * kk + (lane >> 4);
-          af[kk][i] = *reinterpret_cast<const bf16x8*>(halo + q * 128 + 16 * (c ^ (q & 7)));
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(hcur + q * 128 + 16 * (c ^ (q & 7)));
           if constexpr (DGRAD) {
             const int r = wn * 64 + i * 16 + (lane & 15);
             bfr[kk][i] = *reinterpret_cast<const bf16x8*>(ib + r * 128 + 16 * (c ^ kc64_swz(r)));
@@ -200,7 +236,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
       __builtin_amdgcn_sched_barrier(0);
       mma(1);
     };
-    tap_loop<STAGES, NB>(issue, compute);
+    tap_loop<STAGES, NB>(issue, compute, prefetch, pf_on && chunk + 1 < nchunks);
   }
   if (stamps) st2 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();  // `red` of the epilogue aliases the halo
@@ -376,16 +412,31 @@ template <int BN, bool DG, int EPI>
 hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
   constexpr int ST = conv3_stages<BN>();
   const int tpi = (a.H + R - 1) / R;
-  const size_t lds = (size_t)halo_bytes_of(R, a.W) + (size_t)ST * BN * 64 * 2;
+  const size_t hb = (size_t)halo_bytes_of(R, a.W), ring = (size_t)ST * BN * 64 * 2;
   auto k = conv3_kernel<BN, DG, EPI, ST>;
   static bool attr = false;  // once per instantiation (host-side, before any capture)
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
   const int nimg = a.M / (a.H * a.W);
-  hipLaunchKernelGGL(k, dim3(a.N / BN, nimg * tpi), dim3(NT), lds, s, a, R, tpi);
+  const long grid = (long)(a.N / BN) * nimg * tpi;
+  // double-buffered halo: several chunks, the padded DMA count fits C3_HQ per wave, and no
+  // residency lost -- the grid fits one block per CU anyway, or two blocks still fit a CU's
+  // LDS (DAMD_CONV3_HB2=0: single buffer)
+  const size_t lds2 = 2 * hb + 1024 + ring;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  const char* ev = getenv("DAMD_CONV3_HB2");
+  const int hb2 = !(ev && ev[0] == '0') && a.Cin / 64 > 1 && (int)(hb / 1024) <= 4 * C3_HQ && lds2 <= 160 * 1024 &&
+                  (grid <= cus || lds2 <= 80 * 1024);
+  hipLaunchKernelGGL(k, dim3(a.N / BN, nimg * tpi), dim3(NT), hb2 ? lds2 : hb + ring, s, a, R, tpi, hb2);
   return hipGetLastError();
 }
 
