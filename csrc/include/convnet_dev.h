@@ -66,24 +66,33 @@ template <bool U8>
 __device__ __forceinline__ void x_load(XStage<U8>& st, const void* __restrict__ X, long row_base, int nsamples,
                                        int nvalid, int nimg, int r0, int nrows) {
   const int per_img = nrows * 7, total = nimg * per_img;
+  // i / per_img through a float reciprocal (exact here: i < 3072, per_img <= 42, so the
+  // quotient's fraction stays >= 0.5 / per_img away from an integer, far above the float
+  // error): an integer division by a runtime divisor is ~30 instructions per unit
+  const float rinv = 1.f / (float)per_img;
+  // 32-bit sample indices and byte offsets (the engine keeps the dataset below 2^31 bytes):
+  // 64-bit clamps and multiplies doubled the address math of every unit
+  const int rb = (int)row_base;
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
-    const int i = min((int)threadIdx.x + u * 512, total - 1);
-    const int b = i / per_img, rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-    const long g = row_base + b;
-    const bool ok = ((int)threadIdx.x + u * 512 < total) && b < nvalid && g < nsamples;
-    const long gs = max(0L, min(g, (long)nsamples - 1));
-    st.off[u] = ((int)threadIdx.x + u * 512 < total) ? (b * XR + r) * IMG + 4 * q : -1;
+    const int idx = (int)threadIdx.x + u * 512;
+    const int i = min(idx, total - 1);
+    const int b = (int)(((float)i + 0.5f) * rinv), rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
+    const int g = rb + b;
+    const bool ok = idx < total && b < nvalid && g < nsamples;
+    const int gs = max(0, min(g, nsamples - 1));
+    const unsigned eo = (unsigned)(gs * NPIX + (r0 + r) * IMG);  // element offset of the row
+    st.off[u] = idx < total ? (b * XR + r) * IMG + 4 * q : -1;
     if constexpr (U8) {
-      const uint32_t w = reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + gs * NPIX +
-                                                           (r0 + r) * IMG)[q];
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + (eo + 4u * q));
       st.w[u] = ok ? w : 0u;
     } else {
-      const float4 v = reinterpret_cast<const float4*>(static_cast<const float*>(X) + gs * NPIX + (r0 + r) * IMG)[q];
+      const float4 v = *reinterpret_cast<const float4*>(static_cast<const char*>(X) + (4u * eo + 16u * q));
       st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
+
 // lut: optional LDS table lut[k] = k / 255.f (exact: filled with the same correctly rounded
 // division), which replaces four full-precision divisions per unit by four LDS reads
 template <bool U8>

@@ -79,6 +79,30 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
   float* lut = cw + NCONV + IB * PP * 32 / 4;                              // [256] k / 255
+  const int n4 = K * HID / 4;  // <= 2048
+  // ---- first the loads whose addresses do not depend on the ctrl block: the bf16 W1 slice
+  // (eager), both parities of the conv parameters, the b1/W2/b2 triplet; the scheduling
+  // barrier keeps them ahead of the ctrl load (left alone, hipcc issued the ctrl load first
+  // and waited for it with the kernel arguments, then sank these below further waits) ----
+  uint4 bq[2];  // eager: the bf16 W1 slice (bwd already applied the update)
+  if (eager) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      bq[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n4 / 2 - 1)];
+  }
+  // conv parameters: current buffer by parity; their gradient is the previous step's
+  // (bwd added it into hconv[par ^ 1])
+  const int tcl = min(tid, NCONV - 1);
+  const float cp0 = P[tcl], cp1 = calt[tcl], cv0 = V[tcl], cv1 = calt[NCONV + tcl];
+  const long long cq0 = hconv_r[NCONV + tcl], cq1 = hconv_r[tcl];
+  // b1/W2/b2: the grid's last two blocks own their pending update (nobody else in this
+  // launch reads them; bwd reads the updated values)
+  const int si = (lin - (nblk - 2)) * 512 + tid;
+  const bool small_on = lin >= nblk - 2 && si >= 0 && si < NSMALL;
+  const int sic = OFF_B1 + max(0, min(si, NSMALL - 1));
+  const float sp = P[sic], sg = G[sic], sv = V[sic];
+  __builtin_amdgcn_sched_barrier(0);
+
   const Ctrl c = *ctrl;
   const int par = c.wpar;
   if (lin == 0 && tid == 0) {
@@ -91,12 +115,10 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const bool mom = c.momentum != 0.f;
 
-  // ---- issue every independent load of the prologue ----
+  // ---- then the ctrl-dependent loads: the batch rows (and, deferred update, W1 by parity) ----
   XStage<U8> xst;
   x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
-  const int n4 = K * HID / 4;  // <= 2048
   float4 wv[4], gv[4], vv[4];
-  uint4 bq[2];  // eager: the bf16 W1 slice (bwd already applied the update)
   const float* Wcur = c.wpar ? W1alt : P + OFF_W1;
   const float* Vcur = c.wpar ? V1alt : V + OFF_W1;
   float* Wnext = c.wpar ? P + OFF_W1 : W1alt;
@@ -108,11 +130,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   float4* Wn4 = reinterpret_cast<float4*>(Wnext + p0 * 32 * HID);
   float4* Vn4 = reinterpret_cast<float4*>(Vnext + p0 * 32 * HID);
   uint2* Wb = reinterpret_cast<uint2*>(w1bf + p0 * 32 * HID);
-  if (eager) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      bq[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n4 / 2 - 1)];
-  } else {
+  if (!eager) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int ic = min(tid + u * 512, n4 - 1);
@@ -121,20 +139,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
       vv[u] = V4[ic];
     }
   }
-  // conv parameters: current buffer by parity; their gradient is the previous step's
-  // (bwd added it into hconv[par ^ 1])
-  // (both parities are loaded: the addresses do not wait for the ctrl block, only the select)
-  const int tcl = min(tid, NCONV - 1);
-  const float cp0 = P[tcl], cp1 = calt[tcl], cv0 = V[tcl], cv1 = calt[NCONV + tcl];
-  const long long cq0 = hconv_r[NCONV + tcl], cq1 = hconv_r[tcl];
+  __builtin_amdgcn_sched_barrier(0);
   const float cp = par ? cp1 : cp0, cv = par ? cv1 : cv0;
   const long long cq = par ? cq1 : cq0;
-  // b1/W2/b2: the grid's last two blocks own their pending update (nobody else in this
-  // launch reads them; bwd reads the updated values)
-  const int si = (lin - (nblk - 2)) * 512 + tid;
-  const bool small_on = lin >= nblk - 2 && si >= 0 && si < NSMALL;
-  const int sic = OFF_B1 + max(0, min(si, NSMALL - 1));
-  const float sp = P[sic], sg = G[sic], sv = V[sic];
   if (U8 && tid < 256) lut[tid] = (float)tid / 255.f;
   lds_barrier();  // the table is read by x_store (the loads above stay in flight)
 

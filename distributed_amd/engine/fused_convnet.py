@@ -286,6 +286,9 @@ class FusedConvNetEngine(Engine):
         if self.feed is None or getattr(self, "_feed_key", None) != key:
             self.trainer.sync(0.0)
             self.feed = DataFeed(x, y, self.device, flatten=True, allow_u8=env.get_bool("DAMD_X_U8", True))
+            if self.feed.n * 784 * (1 if self.feed.x_u8 else 4) >= 2 ** 31:
+                # the step kernels address the (epoch-permuted) dataset with 32-bit offsets
+                raise ValueError(f"fused ConvNet engine: {self.feed.n} rows exceed the 2 GiB dataset limit")
             self._feed_key = key
             torch.cuda.synchronize(self.device)
             self.x_ep = torch.empty_like(self.feed.x)
