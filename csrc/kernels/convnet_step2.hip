@@ -301,6 +301,54 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   float* db1p = rc + CH;           // [16][64] db1 partials
   int* ylds = reinterpret_cast<int*>(db1p + 16 * HID);  // [CH] label of the row, -1 if invalid
   float* lut = reinterpret_cast<float*>(cs + CH * KC + 16);  // [256] k / 255 (after the codes)
+  const int r0 = 2 * (p0 / PO);
+  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int ko = 8 * (lane >> 4), lr16 = lane & 15;
+
+  // ---- this block's aux elements ----
+  const int chunk_aux = (NAUX2 + NS - 1) / NS;
+  const int tpe = max(1, min(512 / chunk_aux, 64));  // threads per aux element
+  const int ae_local = tid / tpe, aq = tid - ae_local * tpe;
+  const int ae = s * chunk_aux + ae_local;
+  const bool aux_on = ae_local < chunk_aux && ae < NAUX2;
+  const int aec = min(ae, NAUX2 - 1);
+  float arsum = 0.f;
+
+  // ---- prologue: first the loads whose addresses do not depend on the ctrl block (the
+  // previous metric, b1/W2/b2, the bf16 W1 slice, chunk 0's pooled tile and argmax codes),
+  // kept ahead of the ctrl load by a scheduling barrier (as in fwd) ----
+  const float ag_old = Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];  // previous step's reduced metric
+  // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
+  const float spv0 = P[OFF_B1 + tid], spv1 = P[OFF_B1 + min(tid + 512, NSMALL - 1)];
+  const int n8 = K * HID / 8;
+  uint4 wv0, wv1;
+  wv0 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid, n8 - 1)];
+  wv1 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + 512, n8 - 1)];
+  XStage<U8> xst;
+  uint4 hq0, hq1, hq2, hq3;  // hacc row (tid >> 3), columns 8 (tid & 7) .. + 8
+  uint4 pv0, pv1;
+  uint4 cv;                  // argmax codes, zeroed at the LDS store unless cok
+  bool cok = false;
+  int ylab = 0;
+  bool yval = false;
+  const int BP = (B + CH - 1) / CH * CH;
+  const int kc = K / 16;
+  auto load_indep = [&](int chunk) __attribute__((always_inline)) {
+    {
+      const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
+      pv0 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i0 >> 3)) * BP + chunk * CH + (i0 & 7) * 8);
+      pv1 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i1 >> 3)) * BP + chunk * CH + (i1 & 7) * 8);
+    }
+    {
+      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
+      cok = i < CH * kc && lb < B;
+      cv = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF + min(q, kc - 1) * 16);
+    }
+  };
+  load_indep(0);
+  __builtin_amdgcn_sched_barrier(0);
+
   const Ctrl c = *ctrl;
   const int cur = c.cur2, par = c.par2;
   const long long* hcur = hacc + (long)par * B * HID;
@@ -314,39 +362,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   const long row_base = gstart + c.row0;
   const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
   const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
-  const int r0 = 2 * (p0 / PO);
-  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int ko = 8 * (lane >> 4), lr16 = lane & 15;
 
-  // ---- this block's aux elements ----
-  const int chunk_aux = (NAUX2 + NS - 1) / NS;
-  const int tpe = max(1, min(512 / chunk_aux, 64));  // threads per aux element
-  const int ae_local = tid / tpe, aq = tid - ae_local * tpe;
-  const int ae = s * chunk_aux + ae_local;
-  const bool aux_on = ae_local < chunk_aux && ae < NAUX2;
-  const int aec = min(ae, NAUX2 - 1);
-  const float ag_old = Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];  // previous step's reduced metric
-  float arsum = 0.f;
-
-  // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
-  const float spv0 = P[OFF_B1 + tid], spv1 = P[OFF_B1 + min(tid + 512, NSMALL - 1)];
-
-  // ---- prologue loads ----
-  const int n8 = K * HID / 8;
-  uint4 wv[2];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-    wv[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n8 - 1)];
-  XStage<U8> xst;
-  uint4 hq0, hq1, hq2, hq3;  // hacc row (tid >> 3), columns 8 (tid & 7) .. + 8
-  uint4 pv0, pv1;
-  uint4 cv;
-  int ylab = 0;
-  bool yval = false;
-  const int BP = (B + CH - 1) / CH * CH;
-  const int kc = K / 16;
-  auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
+  // then the ctrl-dependent ones: the dense-1 sums by parity, the labels, the batch rows
+  auto load_dep = [&](int chunk) __attribute__((always_inline)) {
     {
       const int r = tid >> 3, q = tid & 7;
       const int row = min(chunk * CH + r, B - 1);
@@ -357,18 +375,6 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       hq3 = hp[3];
     }
     {
-      const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
-      pv0 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i0 >> 3)) * BP + chunk * CH + (i0 & 7) * 8);
-      pv1 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i1 >> 3)) * BP + chunk * CH + (i1 & 7) * 8);
-    }
-    {
-      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
-      const bool ok = i < CH * kc && lb < B;
-      const uint4 v = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF +
-                                                      min(q, kc - 1) * 16);
-      cv = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-    }
-    {
       const int b = chunk * CH + min(tid, CH - 1);
       const long g = row_base + b;
       yval = tid < CH && b < B && g < c.nsamples;
@@ -376,25 +382,26 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     }
     x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
   };
+  auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
+    load_indep(chunk);
+    load_dep(chunk);
+  };
   auto store_chunk = [&](int chunk) __attribute__((always_inline)) {
     if (tid < K * 8) *reinterpret_cast<uint4*>(pt + (tid >> 3) * HP + (tid & 7) * 8) = pv0;
     if (tid + 512 < K * 8) *reinterpret_cast<uint4*>(pt + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = pv1;
     if (tid < CH * kc) {
       const int bb = tid / kc, q = tid - bb * kc;
-      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cv;
+      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cok ? cv : make_uint4(0u, 0u, 0u, 0u);
     }
     x_store<U8>(xst, xs, lut);
     spl[tid] = spv0;
     if (tid + 512 < NSMALL) spl[tid + 512] = spv1;
     if (tid < CH) ylds[tid] = yval ? ylab : -1;
   };
-  load_chunk(0);
+  load_dep(0);
   if (U8 && tid < 256) lut[tid] = (float)tid / 255.f;
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int i = tid + u * 512;
-    if (i < n8) *reinterpret_cast<uint4*>(w1s + (i >> 3) * HP + (i & 7) * 8) = wv[u];
-  }
+  if (tid < n8) *reinterpret_cast<uint4*>(w1s + (tid >> 3) * HP + (tid & 7) * 8) = wv0;
+  if (tid + 512 < n8) *reinterpret_cast<uint4*>(w1s + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = wv1;
   lds_barrier();  // lut visible to x_store
 
   const int dn = wave & 3, dm0 = wave >> 2;
