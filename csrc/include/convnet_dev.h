@@ -93,22 +93,26 @@ __device__ __forceinline__ void x_load(XStage<U8>& st, const void* __restrict__ 
   }
 }
 
-// lut: optional LDS table lut[k] = k / 255.f (exact: filled with the same correctly rounded
-// division), which replaces four full-precision divisions per unit by four LDS reads
+// k / 255 rounded to fp32 exactly as float32(k / 255.0) for every k < 256 (checked for all
+// 256 with exact fma arithmetic): q = k * (1/255) plus one fma-residual correction -- three
+// VALU ops instead of a correctly rounded division (~10) or an LDS table read (a serial
+// LDS round trip per staged unit)
+__device__ __forceinline__ float u8_over_255(uint32_t k) {
+  const float r = 1.f / 255.f, x = (float)k, q = x * r;
+  return fmaf(fmaf(-q, 255.f, x), r, q);
+}
+// (lut: unused, kept for the callers that still stage a k / 255 table)
 template <bool U8>
 __device__ __forceinline__ void x_store(const XStage<U8>& st, float* xs, const float* lut = nullptr) {
+  (void)lut;
 #pragma unroll
   for (int u = 0; u < 6; ++u) {
     if (st.off[u] >= 0) {
       float4 v;
       if constexpr (U8) {
         const uint32_t w = st.w[u];
-        if (lut != nullptr) {
-          v = make_float4(lut[w & 0xff], lut[(w >> 8) & 0xff], lut[(w >> 16) & 0xff], lut[w >> 24]);
-        } else {
-          v = make_float4((float)(w & 0xff) / 255.f, (float)((w >> 8) & 0xff) / 255.f,
-                          (float)((w >> 16) & 0xff) / 255.f, (float)(w >> 24) / 255.f);
-        }
+        v = make_float4(u8_over_255(w & 0xff), u8_over_255((w >> 8) & 0xff), u8_over_255((w >> 16) & 0xff),
+                        u8_over_255(w >> 24));
       } else {
         v = st.v[u];
       }

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   uint16_t* as = reinterpret_cast<uint16_t*>(smem + IB * XR * IMG * 4);    // [IB][KP] pooled tile
   uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
-  float* lut = cw + NCONV + IB * PP * 32 / 4;                              // [256] k / 255
+  const float* lut = nullptr;  // (x_store converts k / 255 arithmetically)
   const int n4 = K * HID / 4;  // <= 2048
   // ---- first the loads whose addresses do not depend on the ctrl block: the bf16 W1 slice
   // (eager), both parities of the conv parameters, the b1/W2/b2 triplet; the scheduling
@@ -142,8 +142,6 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   __builtin_amdgcn_sched_barrier(0);
   const float cp = par ? cp1 : cp0, cv = par ? cv1 : cv0;
   const long long cq = par ? cq1 : cq0;
-  if (U8 && tid < 256) lut[tid] = (float)tid / 255.f;
-  lds_barrier();  // the table is read by x_store (the loads above stay in flight)
 
   // ---- pending SGD updates ----
   if (eager) {
@@ -300,7 +298,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   float* rc = rl + CH;             // [CH] per-row correct
   float* db1p = rc + CH;           // [16][64] db1 partials
   int* ylds = reinterpret_cast<int*>(db1p + 16 * HID);  // [CH] label of the row, -1 if invalid
-  float* lut = reinterpret_cast<float*>(cs + CH * KC + 16);  // [256] k / 255 (after the codes)
+  const float* lut = nullptr;  // (x_store converts k / 255 arithmetically)
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const int wave = tid >> 6, lane = tid & 63;
@@ -399,10 +397,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     if (tid < CH) ylds[tid] = yval ? ylab : -1;
   };
   load_dep(0);
-  if (U8 && tid < 256) lut[tid] = (float)tid / 255.f;
   if (tid < n8) *reinterpret_cast<uint4*>(w1s + (tid >> 3) * HP + (tid & 7) * 8) = wv0;
   if (tid + 512 < n8) *reinterpret_cast<uint4*>(w1s + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = wv1;
-  lds_barrier();  // lut visible to x_store
+  lds_barrier();  // w1s / staging visible
 
   const int dn = wave & 3, dm0 = wave >> 2;
   const bool mom = c.momentum != 0.f;
