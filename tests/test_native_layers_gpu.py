@@ -213,9 +213,11 @@ def test_native_dropout_trains_and_rate0_is_identity():
     w1, h1, e1 = _train(_mnist, x, y, init, 64, 5, native=True, lr=0.05)
     assert e0 == e1 == "native_graph"
     # (the conv bias colsum adds fp32 partials atomically in arrival order: after 5 SGD
-    # steps at lr 0.05 that is seen as <= ~2e-8 absolute on weights of ~1e-2)
+    # steps at lr 0.05 that is usually <= ~2e-8 absolute on weights of ~1e-2, but an
+    # order-dependent last bit that flips a bf16 activation rounding has been seen as
+    # 2.1e-7 on 3 of 346,112 elements)
     for a, b in zip(w0, w1):
-        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
     # rate 0.4: trains (loss falls over two epochs' worth of steps), differs from rate 0
     w2, h2, e2 = _train(lambda: _dropout_model(0.4), x, y, init, 64, 10, native=True, lr=0.05, momentum=0.9)
     assert e2 == "native_graph"
