@@ -47,18 +47,22 @@ def spawn_ranks(n: int, argv) -> int:
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL,
                                       start_new_session=True, text=True))
-    out = []
-    rc = 0
-    try:
+    import threading
+
+    def relay():  # rank 0's stdout, relayed on a thread: the main loop keeps polling every rank
         for line in procs[0].stdout:
-            out.append(line)
             print(line, end="", flush=True)
+
+    th = threading.Thread(target=relay, daemon=True)
+    th.start()
+    try:
         deadline = None
         while any(p.poll() is None for p in procs):
-            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
-            if bad:
+            if any(p.returncode not in (None, 0) for p in procs):
+                # a rank failed: the others may be blocked in a collective with it -- give
+                # them a moment to exit on their own, then kill the gang
                 if deadline is None:
-                    deadline = time.time() + 30  # give the others a moment, then kill the gang
+                    deadline = time.time() + 10
                 if time.time() > deadline:
                     break
             time.sleep(0.1)
@@ -70,6 +74,8 @@ def spawn_ranks(n: int, argv) -> int:
                 except (ProcessLookupError, PermissionError):
                     pass
                 p.wait()
+        th.join(timeout=5)
+    rc = 0
     rcs = [p.returncode for p in procs]
     if any(rcs):
         print(f"bench.py: rank exit codes {rcs}", file=sys.stderr)

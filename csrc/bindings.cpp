@@ -43,28 +43,14 @@ class ConvNetTrainer : public StepExecutor {
     b_.X = nullptr; b_.labels = nullptr; b_.x_u8 = 0;
     b_.P = P_<float>(g("params")); b_.G = P_<float>(g("grads")); b_.V = P_<float>(g("velocity"));
     b_.ctrl = P_<Ctrl>(g("ctrl"));
-    b_.slabs = P_<float>(g("slabs")); b_.dhq = P_<uint16_t>(g("dhq"));
     b_.pooled = P_<uint16_t>(g("pooled")); b_.code = P_<uint8_t>(g("code"));
-    b_.hpart = P_<float>(g("hpart"));
     b_.W1alt = P_<float>(g("w1alt")); b_.V1alt = P_<float>(g("v1alt")); b_.w1bf = P_<uint16_t>(g("w1bf"));
     b_.stamps = bufs.contains("stamps") ? P_<unsigned long long>(g("stamps")) : nullptr;
-    b_.fuse_head = bufs.contains("fuse_head") ? (int)g("fuse_head") : 0;
-    b_.kernels = bufs.contains("kernels") ? (int)g("kernels") : 2;
     b_.eager_w1 = bufs.contains("eager_w1") ? (int)g("eager_w1") : 0;
-    if (b_.kernels != 2 && b_.kernels != 3) throw std::invalid_argument("kernels must be 2 or 3");
-    b_.hacc = bufs.contains("hacc") ? P_<long long>(g("hacc")) : nullptr;
-    b_.hconv = bufs.contains("hconv") ? P_<long long>(g("hconv")) : nullptr;
-    b_.calt = bufs.contains("calt") ? P_<float>(g("calt")) : nullptr;
-    if (b_.kernels == 2 && (!b_.hacc || !b_.hconv || !b_.calt))
-      throw std::invalid_argument("2-launch step needs hacc / hconv / calt");
-    HIP_CHECK(convnet_set_lds_limits());
+    b_.hacc = P_<long long>(g("hacc"));
+    b_.hconv = P_<long long>(g("hconv"));
+    b_.calt = P_<float>(g("calt"));
     HIP_CHECK(convnet2_set_lds_limits());
-    HIP_CHECK(convnet_persist_set_lds_limits());
-    if (bufs.contains("phacc")) {
-      phacc_ = P_<long long>(g("phacc"));
-      phconv_ = P_<long long>(g("phconv"));
-      psync_ = P_<unsigned>(g("psync"));
-    }
   }
   // Phase timing: k eager steps of the 2-launch step with HIP events
   // between the forward launch, the backward launch and the gradient all-reduce; returns
@@ -72,7 +58,6 @@ class ConvNetTrainer : public StepExecutor {
   // forward kernel: it applies the previous step's deferred update)
   std::vector<std::vector<float>> phase_times(int k) {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
-    if (b_.kernels != 2) throw std::runtime_error("phase timing covers the 2-launch step");
     hipEvent_t ev[4];
     for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
     std::vector<std::vector<float>> out;
@@ -96,13 +81,6 @@ class ConvNetTrainer : public StepExecutor {
     for (auto& e : ev) hipEventDestroy(e);
     return out;
   }
-  // k training steps in ONE launch of the persistent kernel (world 1; no graph needed)
-  void run_persistent(int k, double timeout_s) {
-    if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
-    if (!phacc_) throw std::runtime_error("ConvNetTrainer: persistent buffers not given");
-    if (k <= 0) return;
-    HIP_CHECK(convnet_persist_launch(b_, B_, k, phacc_, phconv_, psync_, timeout_s, stream_));
-  }
   // X [n][784] (fp32, or uint8 holding k for inputs k/255) and labels [n] int32:
   // epoch-permuted copies (stable pointers).
   void set_data(uintptr_t X, uintptr_t labels, int x_u8) {
@@ -116,7 +94,7 @@ class ConvNetTrainer : public StepExecutor {
   void set_peer_fold(PeerAllreduce* p, bool fold) {
     if (!G_own_) { G_own_ = b_.G; hconv_own_ = b_.hconv; }
     set_peer(p);
-    fold_ = fold && p && p->world() > 1 && b_.kernels == 2;
+    fold_ = fold && p && p->world() > 1;
     if (fold_) {
       const long n = (long)convnet_grad_count(PP_), nfp = (n + 3) / 4 * 4;
       if (PeerAllreduce::message_words(n, 2 * kConvNetNConv) > p->capacity())
@@ -140,14 +118,12 @@ class ConvNetTrainer : public StepExecutor {
     return t;
   }
   void flush() {
-    if (b_.kernels == 2) HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
-    else HIP_CHECK(convnet_launch_flush(b_, PP_, stream_));
+    HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
   }
   // timed runs: k steps + the flush of the last deferred update as one graph
   void capture_final(int k) { StepExecutor::capture_final(k); }
   bool run_final(int k) { return StepExecutor::run_final(k); }
   bool warm_final(int k) { return StepExecutor::warm_final(k); }
-  int kernels() const { return b_.kernels; }
   int num_slices() const { return convnet_num_slices(PP_); }
   int batch() const { return B_; }
 
@@ -155,13 +131,12 @@ class ConvNetTrainer : public StepExecutor {
   void enqueue_tail() override { flush(); }
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
-    if (b_.kernels == 2) HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
-    else HIP_CHECK(convnet_launch_step(b_, B_, PP_, stream_));
+    HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
     if (!grad_allreduce_) return;
-    // the 2-launch step keeps the conv gradient as int64 fixed point (hconv): reduced
-    // exactly, in the same call as the fp32 gradient + metric buffer
-    long long* aux = b_.kernels == 2 ? b_.hconv : nullptr;
-    const long n64 = b_.kernels == 2 ? 2 * kConvNetNConv : 0;  // both parities (see convnet_step2.hip)
+    // the conv gradient is int64 fixed point (hconv): reduced exactly, in the same call as
+    // the fp32 gradient + metric buffer; both parities (see convnet_step2.hip)
+    long long* aux = b_.hconv;
+    const long n64 = 2 * kConvNetNConv;
     if (peer_ && fold_)  // the message is already in the peer `in` staging: exchange only
       peer_->allreduce_staged((long)convnet_grad_count(PP_), n64, stream_);
     else if (peer_)  // native xGMI two-shot all-reduce
@@ -176,22 +151,16 @@ class ConvNetTrainer : public StepExecutor {
   long long* hconv_own_ = nullptr;
   bool fold_ = false;
   int B_, PP_, grad_allreduce_;
-  long long* phacc_ = nullptr;
-  long long* phconv_ = nullptr;
-  unsigned* psync_ = nullptr;
 };
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_amd native runtime (HIP/gfx950 kernels, RCCL, hipGraph executor)";
   m.attr("CONVNET_NPARAM") = kConvNetNParam;
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
-  m.attr("CONVNET_REC") = kConvNetRec;
   m.attr("CONVNET_NCONV") = kConvNetNConv;
-  m.def("convnet_persist_lds_bytes", &convnet_persist_lds);
   m.def("convnet2_lds_bytes", [](int PP) { return py::make_tuple(convnet2_fwd_lds(PP, 4), convnet2_bwd_lds(PP)); });
   m.def("convnet_num_slices", &convnet_num_slices);
   m.def("convnet_grad_count", &convnet_grad_count);
-  m.def("convnet_lds_bytes", [](int PP) { return py::make_tuple(convnet_f1_lds(PP, 4), convnet_f1_lds(PP, 6), convnet_f3_lds(PP)); });
 
   m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) n = 0; return n; });
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
@@ -275,8 +244,6 @@ PYBIND11_MODULE(_C, m) {
       .def("capture_final", &ConvNetTrainer::capture_final, py::arg("steps"))
       .def("run_final", &ConvNetTrainer::run_final, py::arg("steps"), py::call_guard<py::gil_scoped_release>())
       .def("warm_final", &ConvNetTrainer::warm_final, py::arg("steps"), py::call_guard<py::gil_scoped_release>())
-      .def("run_persistent", &ConvNetTrainer::run_persistent, py::arg("steps"), py::arg("timeout_s") = 5.0,
-           py::call_guard<py::gil_scoped_release>())
       .def("phase_times", &ConvNetTrainer::phase_times, py::arg("steps"), py::call_guard<py::gil_scoped_release>())
       .def("flush", &ConvNetTrainer::flush)
       .def("sync", &ConvNetTrainer::sync, py::arg("timeout_s") = 0.0,
@@ -284,7 +251,6 @@ PYBIND11_MODULE(_C, m) {
       .def("invalidate_graphs", &ConvNetTrainer::invalidate_graphs)
       .def_property_readonly("num_graphs", &ConvNetTrainer::num_graphs)
       .def_property_readonly("num_slices", &ConvNetTrainer::num_slices)
-      .def_property_readonly("kernels", &ConvNetTrainer::kernels)
       .def_property_readonly("batch", &ConvNetTrainer::batch)
       .def_property_readonly("stream", [](ConvNetTrainer& t) { return reinterpret_cast<uintptr_t>(t.stream()); });
 

@@ -1,4 +1,4 @@
-// Host interface of the fused MNIST-CNN step kernels (csrc/kernels/convnet_fused.hip).
+// Host interface of the fused MNIST-CNN step kernels (csrc/kernels/convnet_step2.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -11,19 +11,15 @@ struct ConvNetBuffers {
   int x_u8;
   float* P; float* G; float* V; Ctrl* ctrl;
   float* W1alt; float* V1alt; uint16_t* w1bf;  // W1 double buffer (fp32, velocity) + bf16 copy
-  uint16_t* pooled /* [5408][BP] */; uint8_t* code /* [B][5408] */; float* slabs; uint16_t* dhq; float* hpart;
+  uint16_t* pooled /* [5408][BP] */; uint8_t* code /* [B][5408] */;
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
-  // 1: the head (F2) runs inside F1 (hacc + counters in `slabs`, see convnet_fused.hip)
-  int fuse_head;
-  // 2-launch step (convnet_step2.hip): fixed-point accumulators of the cross-block sums
+  // fixed-point accumulators of the cross-block sums
   long long* hacc;   // [2][B][64] dense-1 pre-activations x 2^32, by step parity
   long long* hconv;  // [2][320] conv weight/bias gradient x 2^40, by step parity (both all-reduced)
   float* calt;       // [2][320] alternate conv parameters / velocity (double buffer by parity)
-  int kernels;       // 2 (default) or 3 (convnet_fused.hip)
-  // 2-launch step, no gradient all-reduce (world 1): bwd applies the W1 update as soon as
-  // its block has the slice's gradient (fp32 master + velocity in place, bf16 copy); fwd
-  // then reads only the bf16 copy.  0: the update is deferred into the next fwd (after
-  // the all-reduce of G)
+  // no gradient all-reduce (world 1): bwd applies the W1 update as soon as its block has
+  // the slice's gradient (fp32 master + velocity in place, bf16 copy); fwd then reads only
+  // the bf16 copy.  0: the update is deferred into the next fwd (after the all-reduce of G)
   int eager_w1;
   // read side of the gradient when the peer all-reduce is folded into the step (the
   // all-reduce's `out` staging; G / hconv are then its `in` staging, written by bwd):
@@ -34,14 +30,8 @@ struct ConvNetBuffers {
 constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;
 constexpr int kConvNetNGrad = 347152;
-constexpr int kConvNetRec = 716;  // F2 record columns (hpart is [kConvNetRec][B])
 int convnet_num_slices(int PP);
 int convnet_f1_lg(int B);
-size_t convnet_f1_lds(int PP, int lg);
-size_t convnet_f3_lds(int PP);
-hipError_t convnet_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
-hipError_t convnet_launch_flush(const ConvNetBuffers& b, int PP, hipStream_t st);
-// the 2-launch step (convnet_step2.hip)
 size_t convnet2_fwd_lds(int PP, int lg);
 size_t convnet2_bwd_lds(int PP);
 hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
@@ -50,12 +40,6 @@ hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream
 hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st);
 hipError_t convnet2_set_lds_limits();
-// the persistent multi-step kernel (convnet_persist.hip): world 1, B <= 64, 3 positions per slice
-size_t convnet_persist_lds();
-hipError_t convnet_persist_launch(const ConvNetBuffers& b, int B, int nsteps, long long* hacc3, long long* hconv3,
-                                  unsigned* sync, double timeout_s, hipStream_t st);
-hipError_t convnet_persist_set_lds_limits();
 // elements of the all-reduced gradient buffer
 size_t convnet_grad_count(int PP);
-hipError_t convnet_set_lds_limits();
 }  // namespace damd

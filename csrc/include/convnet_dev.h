@@ -1,7 +1,6 @@
-// Device-side building blocks shared by the fused MNIST-CNN step kernels
-// (csrc/kernels/convnet_fused.hip: 3-launch step; csrc/kernels/convnet_step2.hip:
-// 2-launch step): model constants and flat-buffer layout, input-row staging, and the
-// conv 3x3 + bias + ReLU + 2x2 max-pool on MFMA.
+// Device-side building blocks of the fused MNIST-CNN step kernels
+// (csrc/kernels/convnet_step2.hip): model constants and flat-buffer layout, input-row
+// staging, the conv 3x3 + bias + ReLU + 2x2 max-pool on MFMA, fixed-point sums.
 #pragma once
 #include "convnet.h"
 #include "damd_common.h"
@@ -21,15 +20,12 @@ constexpr int NPARAM = OFF_B2 + NCLS;        // 347146
 constexpr int OFF_LOSS = NPARAM, OFF_CORR = NPARAM + 1, OFF_CNT = NPARAM + 2;
 constexpr int NGRAD = NPARAM + 6;            // padded to 16 B: 347152
 constexpr int NSMALL = HID + HID * NCLS + NCLS;  // b1, W2, b2 contiguous: 714
-constexpr int REC = NSMALL + 2;              // F2 record columns: dW2[640] db2[10] db1[64] loss corr
-constexpr int NAUX = NSMALL + 3;             // F3 "aux" elements: b1/W2/b2 + metric tail
 constexpr int CH = 64;                       // images per chunk
 constexpr int XR = 6;                        // staged input rows per image
-constexpr int MAXPP = 4;                     // max pooled positions per F1/F3 block
+constexpr int MAXPP = 4;                     // max pooled positions per fwd / bwd block
 constexpr int XS_BYTES = CH * XR * IMG * 4;  // 43008
 constexpr int HP = 72;                       // bf16 pitch of 64-wide tiles (conflict-free)
 static_assert(NPARAM == kConvNetNParam && NGRAD == kConvNetNGrad, "param count");
-static_assert(REC == kConvNetRec, "record count");
 
 __host__ __device__ constexpr int kpitch(int pp) { return pp * 32 + 8; }
 __host__ __device__ constexpr int nsp(int ns) { return (ns + 3) & ~3; }
@@ -121,7 +117,7 @@ __device__ __forceinline__ void x_store(const XStage<U8>& st, float* xs, const f
   }
 }
 
-// ---- conv 3x3 + bias + ReLU + 2x2 max-pool of a slice on MFMA (shared by F1 and F3) ----
+// ---- conv 3x3 + bias + ReLU + 2x2 max-pool of a slice on MFMA ----
 // One 16x16x32 bf16 MFMA per tile with a split-precision K packing:
 //   k in [0,9): x_hi*w_hi   [9,18): x_lo*w_hi   [18,27): x_hi*w_lo   [27,32): 0
 // (x = hi + lo, w = hi + lo in bf16) -> ~16-bit-mantissa conv outputs, so the pool
@@ -208,7 +204,19 @@ constexpr double HINV = 1.0 / 4294967296.0;
 constexpr float CSCALE = 1099511627776.f;       // 2^40
 constexpr double CINV = 1.0 / 1099511627776.0;
 
-__device__ __forceinline__ long long to_fix(float v, float scale) { return (long long)__builtin_rintf(v * scale); }
+// |v * scale| < 2^54: a sum of up to 512 such terms (57 slices x 8 ranks) stays inside int64.
+// Anything else -- NaN, inf, a diverged partial -- is not representable: it is counted as 0
+// and raises the sticky ctrl->bad flag, and the step reports loss = NaN from then on (the
+// fp32 engines would show the NaN; a wrapped integer must not turn it into finite garbage)
+constexpr float FIX_LIMIT = 18014398509481984.f;  // 2^54
+__device__ __forceinline__ long long to_fix(float v, float scale, int* bad) {
+  const float q = v * scale;
+  if (!(fabsf(q) < FIX_LIMIT)) {
+    __hip_atomic_fetch_or(bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  return (long long)__builtin_rintf(q);
+}
 __device__ __forceinline__ float from_fix(long long q, double inv) { return (float)((double)q * inv); }
 
 __device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {

@@ -60,8 +60,13 @@ struct Ctrl {
                             //    is still to be applied (set by the last kernel of a step,
                             //    cleared by flush: the first step after a flush applies none)
   int   par2;               // 19 step parity as seen by the 2nd kernel of a 2-launch step (set by the 1st)
-  int   pad[12];              // 20 pad[0]: persistent kernel's global step (buffer rotation / barrier
-                              //    targets); 21 pad[1]: its error word (a grid wait timed out)
+  int   bad;                // 20 sticky: a fixed-point conversion met a non-finite / out-of-range
+                            //    value (the fused step reports loss = NaN from then on)
+  int   xcnt;               // 21 gradient-exchange epoch of the sharded multi-rank step (counts forever)
+  int   xcnt2;              // 22 xcnt as seen by the step's bwd (set by its fwd)
+  int   ticket;             // 23 arrival ticket of the sharded bwd (its last block publishes the
+                            //    rank's small-gradient message)
+  int   pad[8];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

@@ -255,154 +255,6 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
   }
 }
 
-// ---- weight-stationary persistent variant: 64 -> 64 channels (opt-in, DAMD_CONV3W=1) ----
-// All nine 64 x 64 weight taps (72 KiB) stay in LDS for the whole launch and each of the 256
-// blocks (one per CU) walks its output tiles (R rows of one image), prefetching the next
-// tile's halo into the second halo buffer while it computes the current one: no weight
-// traffic and no per-tap barriers, the halo load latency hidden behind the MFMAs.
-// LDS = 72 KiB weights + 2 halos (R = 4, W <= 56: 44.5 KiB each) = 160 KiB.
-template <bool DGRAD, int EPI>
-__global__ __launch_bounds__(NT, 1) void conv3w_kernel(GemmArgs a, int R, int tpi, int ntiles) {
-  constexpr int BN = 64, BM = 256, B_ST = 64 * 64 * 2;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int H = a.H, W = a.W;
-  const int HW = W + 2, hpix = (R + 2) * HW;
-  const int halo_bytes = (hpix * 128 + 1023) & ~1023;
-  const int nhi = halo_bytes / 1024;
-  char* wimg = smem;                 // [9][B_ST]
-  char* halos = smem + 9 * B_ST;     // [2][halo_bytes]
-  const int t = threadIdx.x, lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const uint16_t* src = (const uint16_t*)a.A;
-  const uint16_t* wsrc = (const uint16_t*)a.B;
-  const void* zero = tile::pinned_addr(g_zero16_c3);
-  if ((int)blockIdx.x >= ntiles) return;
-
-  // all nine weight taps (2 DMA instructions per wave and tap)
-  {
-    constexpr int CPR = BN / 8, RPI = 64 / CPR;
-    const int ca = (lane & 7) ^ kc64_swz(lane >> 3);
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int q = wave + 4 * j;
-        const void* p;
-        if constexpr (DGRAD) {
-          p = wsrc + ((long)tap * BN + 8 * q + (lane >> 3)) * a.kc + 8 * ca;
-        } else {
-          const int kr = q * RPI + lane / CPR;
-          const int ch = (lane % CPR) ^ tile::mc_swz<BN>(kr);
-          p = wsrc + (long)(tap * 64 + kr) * BN + 8 * ch;
-        }
-        glds16(p, wimg + tap * B_ST + q * 1024);
-      }
-  }
-  auto issue_halo = [&](int tile_i, char* dst) __attribute__((always_inline)) {
-    const int img = tile_i / tpi, oh0 = (tile_i - img * tpi) * R;
-    const uint16_t* base = src + (long)img * H * W * 64;
-    for (int j = wave; j < nhi; j += 4) {
-      const int q = 8 * j + (lane >> 3);
-      const int hr = (int)(((float)q + 0.5f) * (1.f / (float)HW));  // exact: q < 2^21
-      const int hc = q - hr * HW;
-      const int ih = oh0 - 1 + hr, iw = hc - 1;
-      const bool ok = q < hpix && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
-      const int cs = (lane & 7) ^ (q & 7);
-      glds16(ok ? (const void*)(base + ((long)ih * W + iw) * 64 + 8 * cs) : zero, dst + j * 1024);
-    }
-  };
-  issue_halo(blockIdx.x, halos);
-  const int wm = wave;
-  int it = 0;
-  for (int ti = blockIdx.x; ti < ntiles; ti += gridDim.x, ++it) {
-    char* halo = halos + (it & 1) * halo_bytes;
-    const int img = ti / tpi, oh0 = (ti - img * tpi) * R;
-    const int npx = min(R, H - oh0) * W;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's halo (and the weights) landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();                      // ... for every wave; the other buffer is free
-    if (ti + (int)gridDim.x < ntiles) issue_halo(ti + gridDim.x, halos + ((it + 1) & 1) * halo_bytes);
-    int hbase[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int p = min(wm * 64 + i * 16 + (lane & 15), npx - 1);
-      const int r = (int)(((float)p + 0.5f) * (1.f / (float)W));
-      hbase[i] = r * HW + (p - r * W);
-    }
-    f32x4 acc[4][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const char* ib = wimg + tap * B_ST;
-      const int kh = tap / 3, kw = tap - kh * 3;
-      const int toff = DGRAD ? (2 - kh) * HW + (2 - kw) : kh * HW + kw;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[4], bfr[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = hbase[i] + toff, c = 4 * kk + (lane >> 4);
-          af[i] = *reinterpret_cast<const bf16x8*>(halo + q * 128 + 16 * (c ^ (q & 7)));
-          if constexpr (DGRAD) {
-            const int r = i * 16 + (lane & 15);
-            bfr[i] = *reinterpret_cast<const bf16x8*>(ib + r * 128 + 16 * (c ^ kc64_swz(r)));
-          } else {
-            bfr[i] = tile::frag_mc<BN>(ib + kk * 32 * BN * 2, i * 16, lane);
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // every wave is done with this halo: the epilogue's `red` reuses it
-    GemmArgs e = a;
-    const int m0 = (img * H + oh0) * W;
-    e.M = m0 + npx;
-    tile::epilogue<BM, BN, EPI>(e, acc, m0, 0, ti, wm, 0, wave, lane, reinterpret_cast<float*>(halo));
-  }
-}
-
-template <bool DG, int EPI>
-hipError_t launch3w(const GemmArgs& a, int R, hipStream_t s) {
-  const int tpi = (a.H + R - 1) / R;
-  const int nimg = a.M / (a.H * a.W);
-  const int ntiles = nimg * tpi;
-  const int halo = (((R + 2) * (a.W + 2)) * 128 + 1023) & ~1023;
-  const size_t lds = (size_t)9 * 64 * 64 * 2 + 2 * (size_t)halo;
-  auto k = conv3w_kernel<DG, EPI>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int grid = ntiles < cus ? ntiles : cus;  // one block per CU, each walks its tiles
-  hipLaunchKernelGGL(k, dim3(grid), dim3(NT), lds, s, a, R, tpi, ntiles);
-  return hipGetLastError();
-}
-
-template <bool DG>
-hipError_t launch3w_epi(const GemmArgs& a, int epi, int R, hipStream_t s) {
-  switch (epi) {
-    case E_BF16: return launch3w<DG, E_BF16>(a, R, s);
-    case E_BIAS | E_BF16: return launch3w<DG, E_BIAS | E_BF16>(a, R, s);
-    case E_BIAS | E_RELU | E_BF16: return launch3w<DG, E_BIAS | E_RELU | E_BF16>(a, R, s);
-    case E_RELU | E_BF16: return launch3w<DG, E_RELU | E_BF16>(a, R, s);
-    case E_BF16 | E_STATS: return launch3w<DG, E_BF16 | E_STATS>(a, R, s);
-    case E_BIAS | E_BF16 | E_STATS: return launch3w<DG, E_BIAS | E_BF16 | E_STATS>(a, R, s);
-    case E_BF16 | E_ADD: return launch3w<DG, E_BF16 | E_ADD>(a, R, s);
-    default: return hipErrorInvalidValue;
-  }
-}
-
 template <int BN>
 constexpr int conv3_stages() { return BN == 64 ? 4 : 3; }
 
@@ -488,14 +340,10 @@ hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream
     return hipErrorInvalidValue;
   if (dgrad && a.kc != a.Cin) return hipErrorInvalidValue;
   if (epi & (E_SLAB | E_ATOMIC)) return hipErrorInvalidValue;
-  // 64 -> 64 channels, DAMD_CONV3W=1: the weight-stationary persistent kernel (72 KiB of
-  // weights + two halos = the CU's 160 KiB).  Opt-in: measured slower on ResNet layer 1
-  // (forward 42 vs 33 us, backprop-input 37 vs 29 us; one 4-wave block per CU cannot hide
-  // the LDS / MFMA latencies that two streamed-weight blocks per CU overlap)
-  const char* ev = getenv("DAMD_CONV3W");
-  const bool w_ok = ev && ev[0] == '1' && bn == 64 && a.Cin == 64 && a.N == 64 &&
-                    9 * 64 * 64 * 2 + 2 * halo_bytes_of(R, a.W) <= 160 * 1024;
-  if (w_ok) return dgrad ? launch3w_epi<true>(a, epi, R, s) : launch3w_epi<false>(a, epi, R, s);
+  // (a weight-stationary persistent variant for 64 -> 64 channels -- 72 KiB of weights +
+  // two halos = the CU's 160 KiB -- measured slower on ResNet layer 1, forward 42 vs 33 us,
+  // backprop-input 37 vs 29 us: one 4-wave block per CU cannot hide the LDS / MFMA
+  // latencies that two streamed-weight blocks per CU overlap; removed in round 4)
   if (bn == 64) return dgrad ? launch3_epi<64, true>(a, epi, R, s) : launch3_epi<64, false>(a, epi, R, s);
   return dgrad ? launch3_epi<128, true>(a, epi, R, s) : launch3_epi<128, false>(a, epi, R, s);
 }

@@ -255,7 +255,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // one wave instruction = one 512-B row of 64 int64 adds
   long long* hp = hacc + (long)par * B * HID;
   for (int r = wave; r < IB; r += 8)
-    if (img0 + r < B) atomic_add_i64(hp + (long)(img0 + r) * HID + lane, to_fix(part[r * HID + lane], HSCALE));
+    if (img0 + r < B) atomic_add_i64(hp + (long)(img0 + r) * HID + lane, to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
   stamp(sts, st, 4);
   if (st != nullptr && tid == 0 && lin < 256)
     for (int i = 0; i < 5; ++i) st[lin * 16 + i] = sts.t[i];
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
-    atomic_add_i64(hconv + par * NCONV + i, to_fix(a, CSCALE));
+    atomic_add_i64(hconv + par * NCONV + i, to_fix(a, CSCALE, &ctrl->bad));
   }
   // ---- aux: new b1/W2/b2 gradient, metric tail ----
   if (aux_on && aq == 0) {
@@ -666,7 +666,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       float* accp = m == 0 ? &ctrl->acc_loss : (m == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
       const float old = m == 0 ? c.acc_loss : (m == 1 ? c.acc_correct : c.acc_count);
       *accp = old + ag_old;  // fold the previous step's all-reduced metric into the epoch total
-      G[OFF_LOSS + m] = m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
+      // (a non-finite / out-of-range fixed-point input so far: the loss is NaN from now on)
+      G[OFF_LOSS + m] = m == 0 && c.bad ? __builtin_nanf("") : m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
   }
   // zero the dead hacc parity (read by the previous step's bwd) for the next fwd,
@@ -743,6 +744,12 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
 // ---------------------------------------------------------------------------------
 // Host-side launchers (no allocation / sync: capturable into a hipGraph).
 // ---------------------------------------------------------------------------------
+int convnet_num_slices(int PP) { return (convnet::NPOS + PP - 1) / PP; }
+size_t convnet_grad_count(int) { return (size_t)convnet::NGRAD; }
+// fwd images per block = 2^lg: 16 up to B = 256 (more blocks, shorter per-block chains),
+// 64 beyond (bounded replication of the W1-slice / conv-parameter loads)
+int convnet_f1_lg(int B) { return B <= 256 ? 4 : 6; }
+
 size_t convnet2_fwd_lds(int PP, int lg) {
   using namespace convnet;
   const int KP = kpitch(PP), IB = 1 << lg;

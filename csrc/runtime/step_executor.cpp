@@ -83,12 +83,22 @@ bool StepExecutor::warm_final(int k) {
   if (hipGraphGetNodes(gt->second, nullptr, &n) != hipSuccess || n == 0) return false;
   std::vector<hipGraphNode_t> nodes(n);
   if (hipGraphGetNodes(gt->second, nodes.data(), &n) != hipSuccess) return false;
+  // off = number of nodes actually disabled: a node whose type cannot be toggled stops the
+  // walk, and only [0, off) is re-enabled (the failed node was never disabled)
   size_t off = 0;
-  bool ok = true;
-  for (; off < n && ok; ++off) ok = hipGraphNodeSetEnabled(it->second, nodes[off], 0) == hipSuccess;
+  while (off < n && hipGraphNodeSetEnabled(it->second, nodes[off], 0) == hipSuccess) ++off;
+  bool ok = off == n;
   if (ok) ok = hipGraphLaunch(it->second, stream_) == hipSuccess && hipStreamSynchronize(stream_) == hipSuccess;
-  for (size_t i = 0; i < off; ++i) HIP_CHECK(hipGraphNodeSetEnabled(it->second, nodes[i], 1));
+  bool restored = true;
+  for (size_t i = 0; i < off; ++i) restored = hipGraphNodeSetEnabled(it->second, nodes[i], 1) == hipSuccess && restored;
   (void)hipGetLastError();
+  if (!restored) {  // a half-disabled graph must never be replayed: drop it
+    hipGraphExecDestroy(it->second);
+    finals_.erase(it);
+    hipGraphDestroy(gt->second);
+    final_graphs_.erase(gt);
+    return false;
+  }
   return ok;
 }
 

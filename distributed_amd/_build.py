@@ -90,7 +90,11 @@ def _build_C(verbose=False, jobs=None) -> Path:
         n = jobs or min(8, os.cpu_count() or 4, len(jobs_list))
         with cf.ThreadPoolExecutor(n) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
-    if _deps_newer(out, objs):
+    # relink also when the object SET changed (a source added or deleted): mtimes alone
+    # would keep a deleted kernel file's object inside the library
+    manifest = BUILD / "C.objs"
+    listing = "\n".join(o.name for o in objs)
+    if _deps_newer(out, objs) or not manifest.exists() or manifest.read_text() != listing:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out)] + [str(o) for o in objs] + [
             "-L",
             str(ROCM / "lib"),
@@ -99,6 +103,7 @@ def _build_C(verbose=False, jobs=None) -> Path:
             f"-Wl,-rpath,{ROCM / 'lib'}",
         ]
         _run(cmd, verbose)
+        manifest.write_text(listing)
     return out
 
 

@@ -4,10 +4,11 @@ Pattern: ``Conv2D(32, 3, relu, input (28,28,1)) -> MaxPooling2D(2) -> Flatten ->
 Dense(64, relu) -> Dense(10)`` + ``SparseCategoricalCrossentropy(from_logits=True)`` +
 ``SGD`` (any lr / momentum / nesterov) + accuracy metric.
 
-Execution (csrc/kernels/convnet_fused.hip, csrc/runtime/step_executor.cpp): a step is
-three HIP launches plus one in-place RCCL SUM all-reduce of the flat gradient buffer
-(347,146 grads + [loss, correct, count] tail); the SGD update is deferred into the next
-step's consumer kernels; k steps are captured into one hipGraph and replayed.  Model
+Execution (csrc/kernels/convnet_step2.hip, csrc/runtime/step_executor.cpp): a step is
+two HIP launches (fwd, bwd) plus, at world > 1, the per-step SUM all-reduce of the flat
+gradient buffer (347,146 grads + [loss, correct, count] tail); the SGD update is applied
+eagerly by bwd (world 1) or deferred into the next step's fwd; k steps are captured into
+one hipGraph and replayed.  Model
 variables are views of the fp32 master buffer, so ``get_weights``/checkpoints see the
 trained values after ``finish()`` (which applies the last pending update).
 """
@@ -26,10 +27,9 @@ from .data import DataFeed
 NPARAM = 347146
 NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
-REC = 716
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
 (C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
- C_FLUSHT, C_PEND, C_PAR2, C_PSTEP, C_PERR) = range(22)
+ C_FLUSHT, C_PEND, C_PAR2, C_BAD, C_XCNT, C_XCNT2, C_TICKET) = range(24)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -72,6 +72,8 @@ class FusedConvNetEngine(Engine):
             return False, "loss"
         if type(model.optimizer) is not optimizers.SGD:
             return False, "optimizer"
+        if len(model.trainable_weights) != len(SHAPES):
+            return False, "frozen layer weights"
         for m in model.compiled_metrics:
             if m.name not in ("accuracy", "acc", "sparse_categorical_accuracy"):
                 return False, f"metric {m.name}"
@@ -96,29 +98,11 @@ class FusedConvNetEngine(Engine):
         self.G = torch.zeros(C.convnet_grad_count(self.PP), **f32)  # grads + metric tail
         self.V = torch.zeros(NGRAD, **f32)
         self.ctrl = torch.zeros(32, dtype=torch.int32, device=dev)
-        self.slabs = torch.zeros(NS, B, HID, **f32)
-        self.dhq = torch.zeros(4, BP * HID, dtype=torch.bfloat16, device=dev)  # dh hi/lo, two layouts
-        self.hpart = torch.zeros(C.CONVNET_REC, B, **f32)   # column-major per-row records
         self.w1alt = torch.zeros(FEAT * HID, **f32)   # W1 double buffer (by step parity)
         self.v1alt = torch.zeros(FEAT * HID, **f32)
         self.w1bf = torch.zeros(FEAT * HID, dtype=torch.bfloat16, device=dev)
         self.pooled = torch.zeros(FEAT, BP, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
-        # DAMD_CONVNET_KERNELS=2 (default): the 2-launch step (convnet_step2.hip) with
-        # int64 fixed-point cross-block sums -- bitwise reproducible; 3: the older 3-launch
-        # step (convnet_fused.hip, fp32 atomics for the conv gradient)
-        self.kernels = env.get_int("DAMD_CONVNET_KERNELS", 2)
-        if self.kernels not in (2, 3):
-            raise ValueError("DAMD_CONVNET_KERNELS must be 2 or 3")
-        # persistent multi-step kernel (convnet_persist.hip): world 1, B <= 64, 3 positions
-        # per slice.  Opt-in (DAMD_PERSIST=1): measured at parity with the 2-launch step
-        # (24.7 vs 24.1 us/step, profiles/r03_mnist): it keeps W1 resident and has no launch
-        # boundaries, but runs the whole step on 57 CUs, where the 2-launch forward uses 228
-        self.persist = (env.get_bool("DAMD_PERSIST", False) and self.kernels == 2 and B <= 64 and self.PP == 3
-                        and self.world == 1 and not env.get_bool("DAMD_FORCE_ALLREDUCE", False))
-        self.phacc = torch.zeros(3 * 64 * HID, dtype=torch.int64, device=dev)
-        self.phconv = torch.zeros(64 * NCONV, dtype=torch.int64, device=dev)  # >= 57 x 320 fp32 slab
-        self.psync = torch.zeros(2, dtype=torch.int32, device=dev)
         self.hacc = torch.zeros(2 * B * HID, dtype=torch.int64, device=dev)  # by step parity
         self.hconv = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
         self.calt = torch.zeros(2 * NCONV, **f32)  # alternate conv parameters + velocity
@@ -144,24 +128,16 @@ class FusedConvNetEngine(Engine):
         torch.cuda.synchronize(dev)
         bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
                     ctrl=self.ctrl.data_ptr(),
-                    slabs=self.slabs.data_ptr(), dhq=self.dhq.data_ptr(), hpart=self.hpart.data_ptr(),
                     pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
-                    v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr(), kernels=self.kernels,
-                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr(),
-                    phacc=self.phacc.data_ptr(), phconv=self.phconv.data_ptr(), psync=self.psync.data_ptr())
-        # DAMD_CONVNET_FUSE_HEAD=1: the head (F2) folded into F1 by last-arriver tails with
-        # fp32 atomics (csrc/kernels/convnet_fused.hip). Measured slower on MI355X (37.5 vs
-        # 30.0 us/step at B=64: same-address atomic serialisation + a serial tail on the
-        # critical path) and not bitwise reproducible, so the separate F2 launch is default.
-        bufs["fuse_head"] = 1 if env.get_bool("DAMD_CONVNET_FUSE_HEAD", False) else 0
+                    v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr(),
+                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr())
         # world 1 (no gradient all-reduce): bwd applies the W1 update itself as soon as it
         # has the slice's gradient, and fwd reads only the bf16 copy (DAMD_EAGER_W1=0: the
         # deferred update in fwd, as with an all-reduce between the launches)
         force_ar = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
         # (B <= 64: the single-chunk backward; the multi-chunk one has no registers to spare
         # for the slice's masters)
-        self.eager_w1 = (self.kernels == 2 and self.world == 1 and not force_ar and not self.persist
-                         and B <= 64 and env.get_bool("DAMD_EAGER_W1", True))
+        self.eager_w1 = self.world == 1 and not force_ar and B <= 64 and env.get_bool("DAMD_EAGER_W1", True)
         bufs["eager_w1"] = int(self.eager_w1)
         self.stamps = None
         if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
@@ -183,7 +159,7 @@ class FusedConvNetEngine(Engine):
             # in-kernel wait deadline: the collective watchdog's when one is set, so a missing
             # peer costs at most that much GPU spinning per wait
             wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
-            n64 = 2 * NCONV if self.kernels == 2 else 0
+            n64 = 2 * NCONV
             self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0,
                                             C.PeerAllreduce.message_words(C.convnet_grad_count(self.PP), n64),
                                             blocks=env.get_int("DAMD_PEER_BLOCKS", 64),
@@ -225,15 +201,6 @@ class FusedConvNetEngine(Engine):
     def _check_peer(self):
         if self.peer is not None and self.peer.status():
             raise RuntimeError("xGMI peer all-reduce: a wait for a peer timed out (peer missing or wedged)")
-        if self.persist and int(self.ctrl[C_PERR].item()) != 0:
-            # a grid-wide wait of the persistent kernel timed out (workgroups not co-resident):
-            # its state is inconsistent -- reset the rotation / counters and fail loudly
-            self.ctrl[C_PERR] = 0
-            self.ctrl[C_PSTEP] = 0
-            self.phacc.zero_()
-            self.phconv.zero_()
-            self.psync.zero_()
-            raise RuntimeError("persistent ConvNet kernel: a grid-wide wait timed out (set DAMD_PERSIST=0)")
 
     def _ctrl_write(self, updates: dict):
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
@@ -314,20 +281,12 @@ class FusedConvNetEngine(Engine):
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
 
     def run(self, n_steps):
-        if self.persist and n_steps > 0:
-            # the deferred update of a previous 2-launch step is applied first; the persistent
-            # kernel applies every update of its own steps before it returns
-            self._flush()
-            self.trainer.run_persistent(n_steps, env.get_float("DAMD_PERSIST_TIMEOUT_S", 5.0))
-            self.steps_done += n_steps
-            return
         if self.host_collective:
             for _ in range(n_steps):
                 self.trainer.step(1)
                 self.trainer.sync(0.0)
                 self.strategy.communicator.allreduce_(self.G, "sum")
-                if self.kernels == 2:
-                    self.strategy.communicator.allreduce_(self.hconv, "sum")  # exact int64 sum
+                self.strategy.communicator.allreduce_(self.hconv, "sum")  # exact int64 sum
                 torch.cuda.synchronize(self.device)
             self._pending = True
             self.steps_done += n_steps
@@ -344,7 +303,7 @@ class FusedConvNetEngine(Engine):
     def phase_times(self, n_steps: int) -> dict:
         """forward (incl. the fused SGD update of the previous step's gradient), backward and
         gradient all-reduce, from HIP events between the launches of eager 2-launch steps."""
-        if self.kernels != 2 or self.host_collective:
+        if self.host_collective:
             return super().phase_times(n_steps)
         self.sync()
         rows = self.trainer.phase_times(int(n_steps))
@@ -361,8 +320,6 @@ class FusedConvNetEngine(Engine):
                 "allreduce_kind": self.allreduce_kind}
 
     def prepare(self, n_steps):
-        if self.persist:
-            return
         if self.use_graph and not self.host_collective and n_steps >= self.graph_steps:
             self.trainer.capture(self.graph_steps)
 
@@ -370,18 +327,23 @@ class FusedConvNetEngine(Engine):
         """Capture ``n_steps`` steps followed by the flush of the last deferred update as ONE
         graph, for a timed run that must end with every update applied (bench.py): one
         replay instead of n / graph_steps replays plus an eager flush launch."""
-        if self.persist or self.host_collective or not self.use_graph or n_steps <= 0:
+        if self.host_collective or not self.use_graph or n_steps <= 0:
             return False
-        self.trainer.capture_final(int(n_steps))
-        # one replay with every node disabled: the graph's first-launch cost (~9 us measured,
-        # scripts/probe_cold_graph.py) is paid here, outside the timed window
-        self.trainer.warm_final(int(n_steps))
+        try:
+            self.trainer.capture_final(int(n_steps))
+            # one replay with every node disabled: the graph's first-launch cost (~9 us
+            # measured, scripts/probe_cold_graph.py) is paid here, outside the timed window.
+            # A graph whose nodes cannot be toggled is only not pre-warmed.
+            self.trainer.warm_final(int(n_steps))
+        except RuntimeError as e:
+            dlog.warning("final-graph capture unavailable (%s): timed run replays step graphs + flush", e)
+            return False
         return True
 
     def run_and_flush(self, n_steps):
         """``n_steps`` steps, then the pending update applied (run + _flush), through the
         prepare_final graph when one was captured for this count."""
-        if (n_steps > 0 and not self.persist and not self.host_collective and self.use_graph
+        if (n_steps > 0 and not self.host_collective and self.use_graph
                 and self.trainer.run_final(int(n_steps))):
             self._pending = False
             self.steps_done += n_steps
@@ -402,7 +364,9 @@ class FusedConvNetEngine(Engine):
         corr = _i2f(c[C_AC]) + tail[1]
         cnt = _i2f(c[C_AN]) + tail[2]
         d = max(cnt, 1.0)
-        out = {"loss": loss / d, "_count": cnt}
+        # a non-finite / out-of-range value met a fixed-point sum (ctrl.bad): NaN, like the
+        # fp32 engines would show it (TerminateOnNaN must fire)
+        out = {"loss": float("nan") if c[C_BAD] else loss / d, "_count": cnt}
         for m in self.model.compiled_metrics:
             out[m.name] = corr / d
         return out
@@ -429,6 +393,7 @@ class FusedConvNetEngine(Engine):
 
     def after_external_write(self):
         self._refresh_w1bf()
+        self._ctrl_write({C_BAD: 0})  # new weights: a past overflow no longer applies
 
     def sync(self):
         # host readers (get_weights, checkpoints, callbacks) see the trained values: the

@@ -26,7 +26,6 @@ Fusion rules (decided on the layer graph, not traced):
 """
 from __future__ import annotations
 
-import contextlib
 import gc
 import math
 import struct
@@ -110,6 +109,16 @@ def _act_name(layer) -> str:
     return getattr(act, "__name__", "linear") if act is not None else "linear"
 
 
+def _param_weights(model):
+    """Every layer weight the forward plan reads (kernels, biases, BN gamma / beta),
+    trainable or frozen -- i.e. all weights except the BN moving statistics."""
+    out = []
+    for l in model.layers:
+        stats = {id(getattr(l, "moving_mean", None)), id(getattr(l, "moving_variance", None))}
+        out += [w for w in l.weights if id(w) not in stats]
+    return out
+
+
 def _opt_kernel_slots(opt):
     """(opt_step kind, slot names for S0..S2; '' = unused) of a Keras optimizer."""
     from ..keras import optimizers
@@ -148,6 +157,11 @@ class NativeGraphEngine(Engine):
         for m in model.compiled_metrics:
             if m.name not in ("accuracy", "acc", "sparse_categorical_accuracy"):
                 return False, f"metric {m.name}"
+        # the training plan keeps one flat buffer of trainable weights: a frozen kernel /
+        # bias / gamma / beta (layer.trainable = False) trains on the generic path
+        trainable = {id(w) for w in model.trainable_weights}
+        if any(id(w) not in trainable for w in _param_weights(model)):
+            return False, "frozen layer weights"
         return NativeGraphEngine.layers_eligible(model)
 
     @staticmethod
@@ -256,12 +270,6 @@ class NativeGraphEngine(Engine):
         self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0))
         # created up front: no stream creation while a graph is being captured
         self._comm_stream = torch.cuda.Stream(dev) if self.native_comm is not None else None
-        # DAMD_WGRAD_STREAM=1: conv weight gradients on a side stream (a parallel branch of the
-        # step graph).  Measured slower on ResNet-18 (3.55 vs 3.43 ms/step; 3.64 with the main
-        # chain at high priority): each conv kernel already fills the chip, and two at once
-        # slow the dgrad/BN chain more than the overlap saves -- so off by default.
-        self._wgrad_stream = torch.cuda.Stream(dev) if env.get_bool("DAMD_WGRAD_STREAM", False) else None
-        self.gemm_ws_w = torch.zeros_like(self.gemm_ws) if self._wgrad_stream is not None else None
         opt._iter_source = self._iterations
         torch.cuda.synchronize(dev)
         dlog.info("native graph engine: %d nodes, %d params, %.1f MB planned activations", len(self.nodes), n,
@@ -635,8 +643,6 @@ class NativeGraphEngine(Engine):
                 continue
             cs = self._comm_stream
             cs.wait_stream(main)
-            if self._wgrad_stream is not None:
-                cs.wait_stream(self._wgrad_stream)
             self.native_comm.allreduce(self.G.data_ptr() + 4 * b["lo"], self.G.data_ptr() + 4 * b["lo"],
                                        b["hi"] - b["lo"], 0, 0, cs.cuda_stream)
             b["sent"] = True
@@ -780,8 +786,6 @@ class NativeGraphEngine(Engine):
         for nd in reversed(live):
             getattr(self, "_bwd_" + nd.kind)(nd)
             self._bucket_progress(nd)
-        if self._wgrad_stream is not None:  # join the weight-gradient branch
-            torch.cuda.current_stream(self.device).wait_stream(self._wgrad_stream)
         self._mark("backward")
         self._bucket_progress(None, final=True)
         self._mark("allreduce")  # the part of the all-reduce not hidden behind backward
@@ -967,28 +971,20 @@ class NativeGraphEngine(Engine):
         if "dz" in nd.attrs:
             self._act_bwd(nd, dy, y.buf, nd.attrs["dz"])
             dy = nd.attrs["dz"]
-        ws_s = self._wgrad_stream
-        if ws_s is not None:
-            # the weight gradient only feeds the optimizer / all-reduce: it runs on a side
-            # stream (a parallel branch of the step graph) beside the dgrad + BN chain; it
-            # reads dy and x, which nothing rewrites before the step's join
-            ws_s.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(ws_s) if ws_s is not None else contextlib.nullcontext():
-            wsp = self.gemm_ws_w if ws_s is not None else self.gemm_ws
-            if l.use_bias:
-                H.colsum(dy, self.gviews[id(l.bias)])
-            if nd.attrs.get("stem4"):
-                kh, kw, cin, cout = l.kernel.shape
-                dwp = nd.attrs["dw_pad"]
-                H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=wsp, accumulate=False)
-                H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
-            elif "dw_pad" in nd.attrs:
-                dwp = nd.attrs["dw_pad"]
-                H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=wsp, accumulate=False)
-                kh, kw, cin, cout = l.kernel.shape
-                H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
-            else:
-                H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=wsp)
+        if l.use_bias:
+            H.colsum(dy, self.gviews[id(l.bias)])
+        if nd.attrs.get("stem4"):
+            kh, kw, cin, cout = l.kernel.shape
+            dwp = nd.attrs["dw_pad"]
+            H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=self.gemm_ws, accumulate=False)
+            H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
+        elif "dw_pad" in nd.attrs:
+            dwp = nd.attrs["dw_pad"]
+            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=self.gemm_ws, accumulate=False)
+            kh, kw, cin, cout = l.kernel.shape
+            H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
+        else:
+            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=self.gemm_ws)
         if xt.needs_grad:
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written

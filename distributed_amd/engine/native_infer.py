@@ -28,7 +28,8 @@ import torch
 
 from ..ops import hip as H
 from ..utils import logging as dlog
-from .native_graph import C_AL, C_AC, C_AN, C_CUR, C_GB, C_NS, C_ROW0, C_WRAP, NativeGraphEngine, _i2f, _pad8
+from .native_graph import (C_AL, C_AC, C_AN, C_CUR, C_GB, C_NS, C_ROW0, C_WRAP, NativeGraphEngine, _i2f, _pad8,
+                           _param_weights)
 
 
 class NativeInference(NativeGraphEngine):
@@ -68,7 +69,8 @@ class NativeInference(NativeGraphEngine):
             t.needs_grad = False
         self._allocate()
         dev = self.device
-        self.vars = list(model.trainable_weights)
+        # every weight the forward reads, frozen layers included (not only trainable_weights)
+        self.vars = _param_weights(model)
         self.sizes = [int(np.prod(v.shape)) for v in self.vars]
         offs, off = [], 0
         for sz in self.sizes:

@@ -432,17 +432,30 @@ class Model(L.Layer):
         if self._inputs is None:
             return {"name": self.name, "layers": self._layer_configs()}
         calls = {}
-        for t in self._nodes:
+        for t in list(self._inputs) + list(self._nodes):
             calls.setdefault(id(t.layer), []).append(t)
+        # a layer's node index is its call counter, global to the layer: calls made outside
+        # this model (a shared layer, a sub-model built first) would leave gaps.  The config
+        # numbers each layer's nodes by their position among THIS model's calls, which is
+        # how inbound_nodes / input_layers / output_layers are resolved on load (Keras
+        # remaps node indices the same way)
+        local = {}
+        for lid, ts in calls.items():
+            for pos, t in enumerate(sorted({id(t): t for t in ts}.values(), key=lambda t: t.node_index)):
+                local[id(t)] = pos
+
+        def ref(t):
+            return [t.layer.name, local.get(id(t), 0), 0]
+
         layers = []
         for l in self.layers:
-            nodes = sorted(calls.get(id(l), []), key=lambda t: t.node_index)
-            inbound = [[[i.layer.name, i.node_index, 0, {}] for i in t.inputs] for t in nodes]
+            nodes = sorted({id(t): t for t in calls.get(id(l), []) if t.inputs}.values(), key=lambda t: t.node_index)
+            inbound = [[ref(i) + [{}] for i in t.inputs] for t in nodes]
             layers.append({"name": l.name, "class_name": type(l).__name__, "config": l.get_config(),
                            "inbound_nodes": inbound})
         return {"name": self.name, "layers": layers,
-                "input_layers": [[t.layer.name, t.node_index, 0] for t in self._inputs],
-                "output_layers": [[t.layer.name, t.node_index, 0] for t in self._outputs]}
+                "input_layers": [ref(t) for t in self._inputs],
+                "output_layers": [ref(t) for t in self._outputs]}
 
     def to_json(self, **kw):
         return json.dumps({"class_name": type(self).__name__, "config": self.get_config(),

@@ -33,25 +33,9 @@ def main():
     eng.sync()
     st = eng.stamps.cpu().numpy()
     NS = eng.trainer.num_slices
-    if getattr(eng, "persist", False):
-        a = st[0, :NS].astype(np.int64)
-        names = ["step start", "conv done", "atomics issued", "B1 passed", "h", "head+dh", "small+dW1",
-                 "dP", "convgrad issued", "B2 passed", "step end"]
-        base = a[:, 0].min()
-        print(f"persistent kernel, last step of the launch, {NS} workgroups (us since the earliest start):")
-        for j, nm in enumerate(names):
-            d = (a[:, j] - base) / 100.0
-            print(f"   {j:2d} {nm:16s} median {statistics.median(d):7.2f}  min {d.min():7.2f}  max {d.max():7.2f} us")
-        return
-    if eng.trainer.kernels == 2:
-        grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, NS)}
-        names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued"],
-                 "bwd": ["start", "loads staged", "head done", "mfma", "convgrad", "end", "h", "softmax", "dh"]}
-    else:
-        grids = {"F1": (0, NS * ((B + 15) // 16)), "F2": (1, B), "F3": (2, NS)}
-        names = {"F1": ["start", "ctrl", "sgd+loads", "xs staged", "conv done", "end"],
-                 "F2": ["start", "slabs+params", "end"],
-                 "F3": ["start", "loads staged", "mfma", "convgrad", "end"]}
+    grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, NS)}
+    names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued"],
+             "bwd": ["start", "loads staged", "head done", "mfma", "convgrad", "end", "h", "softmax", "dh"]}
     t0 = None
     for kn, (k, n) in grids.items():
         a = st[k, :n].astype(np.int64)

@@ -180,3 +180,26 @@ def test_shared_layer_node_indices():
     m2.set_weights(m.get_weights())
     xx = np.random.default_rng(0).random((4, 6), dtype=np.float32)
     np.testing.assert_array_equal(m.predict(xx), m2.predict(xx))
+
+
+def test_layer_called_outside_the_model_roundtrips():
+    """a layer also called outside this model (here by a sub-model built first)
+    has global call counters that run past this model's nodes; the config renumbers each
+    layer's nodes by position among this model's calls, so the saved graph reloads."""
+    L = tf.keras.layers
+    d = L.Dense(6, name="shared_outside")
+    other_in = tf.keras.Input(shape=(6,))
+    tf.keras.Model(other_in, d(other_in))          # call #0 of d belongs to another model
+    inp = tf.keras.Input(shape=(6,))
+    out = L.Dense(2, name="head2")(d(d(inp)))      # calls #1 and #2 of d
+    m = tf.keras.Model(inp, out)
+    c = json.loads(m.to_json())["config"]
+    by = {l["name"]: l for l in c["layers"]}
+    nodes = by["shared_outside"]["inbound_nodes"]
+    assert len(nodes) == 2
+    assert nodes[1] == [["shared_outside", 0, 0, {}]]   # the second local call eats the first
+    assert by["head2"]["inbound_nodes"] == [[["shared_outside", 1, 0, {}]]]
+    m2 = tf.keras.models.model_from_config({"class_name": "Model", "config": c})
+    x = np.random.default_rng(0).random((4, 6), dtype=np.float32)
+    m2.set_weights(m.get_weights())
+    np.testing.assert_allclose(m2.predict(x), m.predict(x), rtol=1e-6, atol=1e-7)

@@ -391,16 +391,13 @@ CONV3_CASES = [
 ]
 
 
-@pytest.mark.parametrize("stationary", ["1", "0"])
 @pytest.mark.parametrize("n,h,cin,cout", CONV3_CASES)
-def test_direct_conv3(H, monkeypatch, n, h, cin, cout, stationary):
+def test_direct_conv3(H, monkeypatch, n, h, cin, cout):
     """The direct 3x3/s1/p1 kernel (csrc/kernels/conv3x3.hip: input halo resident in LDS,
     weights streamed per tap) against the fp32 conv and the implicit-GEMM kernel, forward
     with bias + ReLU and with the BN-statistics epilogue, backprop-input plain and
-    accumulating.  64 -> 64 shapes also through the weight-stationary persistent kernel
-    (DAMD_CONV3W=1)."""
+    accumulating."""
     monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
-    monkeypatch.setenv("DAMD_CONV3W", stationary)
     x = rb(rnd(n, h, h, cin, seed=11)).requires_grad_(True)
     w = rb(rnd(3, 3, cin, cout, scale=0.05, seed=12)).requires_grad_(True)
     bias = rnd(cout, scale=0.1, seed=13)
@@ -446,7 +443,6 @@ def test_direct_conv3_dgrad_bnred(H, monkeypatch, n, h, cin, cout):
     direct kernel's, and the per-tile partials sum to sum(dz), sum(dz * xhat) with
     dz = bf16(dx) * [bf16(relu(x sc + sh)) > 0] (fp32 reference)."""
     monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
-    monkeypatch.setenv("DAMD_CONV3W", "0")
     shape = (n, h, h, cin)
     dplan = H.conv_dgrad_plan(shape, (3, 3, cin, cout), (1, 1), "same")
     assert dplan["amode"] == H.A_DGRAD3

@@ -118,3 +118,25 @@ def test_validation_split_runs_native_inference():
         h = m.fit(x, y, batch_size=64, epochs=2, validation_split=0.2, verbose=0)
     assert len(h.history["val_loss"]) == 2 and np.isfinite(h.history["val_loss"]).all()
     assert any(isinstance(p, NativeInference) for p in m._infer_plans.values())
+
+
+def test_frozen_layer_predict_and_fit():
+    """A layer frozen with ``trainable = False``: its kernel / bias leave
+    ``trainable_weights``, but the inference plan still reads them, and training
+    falls back to the generic path (the native training plan holds trainable weights only)."""
+    x, y = _data(256, (32, 32, 3), 10, seed=6)
+    m = _trained(_small_resnet, x, y, steps=2)
+    conv = [l for l in m.layers if type(l).__name__ == "Conv2D"][1]
+    dense = [l for l in m.layers if type(l).__name__ == "Dense"][-1]
+    conv.trainable = False
+    dense.trainable = False
+    assert conv.kernel not in m.trainable_weights
+    nat, ref = _both(lambda: m.predict(x[:64], batch_size=32))
+    assert any(isinstance(p, NativeInference) for p in m._infer_plans.values())
+    assert np.abs(nat - ref).max() / (np.abs(ref).max() + 1e-9) < 3e-2
+    k0 = conv.kernel.numpy().copy()
+    m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tf.keras.optimizers.SGD(learning_rate=0.05), metrics=["accuracy"])
+    m.fit(x, y, batch_size=32, epochs=1, steps_per_epoch=2, verbose=0)
+    assert m._engine.name == "generic"
+    np.testing.assert_array_equal(conv.kernel.numpy(), k0)  # frozen: unchanged
