@@ -67,7 +67,7 @@ class ConvNetTrainer : public StepExecutor {
       HIP_CHECK(hipEventRecord(ev[1], stream_));
       HIP_CHECK(convnet2_launch_bwd(b_, B_, PP_, stream_));
       HIP_CHECK(hipEventRecord(ev[2], stream_));
-      if (grad_allreduce_) {
+      if (grad_allreduce_ && !sharded_) {
         if (peer_ && fold_) peer_->allreduce_staged((long)convnet_grad_count(PP_), 2 * kConvNetNConv, stream_);
         else if (peer_) peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, b_.hconv, 2 * kConvNetNConv);
         else if (comm_) comm_->allreduce_f32_i64(b_.G, convnet_grad_count(PP_), b_.hconv, 2 * kConvNetNConv, stream_);
@@ -109,15 +109,59 @@ class ConvNetTrainer : public StepExecutor {
     invalidate_graphs();
   }
   bool folded() const { return fold_; }
+  // Sharded multi-rank step (convnet.h XArgs): the gradient exchange runs inside the step
+  // kernels through the peer all-reduce's mapped staging (its `in` holds the partial slots,
+  // its `out` the reduced gradient, small messages and flags) -- no all-reduce launch.
+  // hred: [2][320] int64 (the conv-gradient sums convnet2_launch_gather writes for flush)
+  void set_sharded(PeerAllreduce* p, uintptr_t hred, int gbf16) {
+    if (!p || p->world() < 2 || p->world() > kXMaxRanks) throw std::invalid_argument("sharded step: 2..8 ranks");
+    const int NU = 4 * convnet_num_slices(PP_);
+    if (p->capacity() < convnet_xin_floats(p->world(), NU) || p->capacity() < convnet_xout_floats(NU))
+      throw std::invalid_argument("sharded step: peer staging too small");
+    const PeerArgs& a = p->args();
+    XArgs x{};
+    for (int r = 0; r < p->world(); ++r) {
+      if (!a.in[r] || !a.out[r]) throw std::runtime_error("sharded step: peer staging not mapped");
+      x.in[r] = a.in[r];
+      x.out[r] = a.out[r];
+    }
+    x.status = a.status;
+    x.timeout_ticks = a.timeout_ticks;
+    x.world = p->world();
+    x.rank = p->rank();
+    x.gbf16 = gbf16;
+    xa_ = x;
+    set_peer(p);
+    sharded_ = true;
+    fold_ = false;
+    // the flags start at 0 (the self-test wrote over the whole staging): the caller joins a
+    // barrier of all ranks after this returns, before any step
+    HIP_CHECK(hipMemset(p->out_local() + kXFlags, 0,
+                        (size_t)(convnet_xout_floats(NU) - kXFlags) * sizeof(float)));
+    HIP_CHECK(hipDeviceSynchronize());
+    b_.xa = &xa_;
+    b_.Gr = p->out_local() + kXGred;
+    b_.hconv_r = P_<long long>(hred);
+    invalidate_graphs();
+  }
+  bool sharded() const { return sharded_; }
+  // in-kernel wait deadline of the sharded exchange (follows the collective watchdog)
+  void set_exchange_timeout(double s) { xa_.timeout_ticks = (unsigned long long)(s * 1e8); invalidate_graphs(); }
+  // sharded step: the pending update's reduced small gradients / metric tail gathered into Gr
+  void gather() {
+    if (sharded_) HIP_CHECK(convnet2_launch_gather(b_, PP_, stream_));
+  }
   // the reduced [loss, correct, count] tail of the last step (host copy, synchronizes)
   std::vector<float> metric_tail() {
     std::vector<float> t(3);
+    gather();
     HIP_CHECK(hipStreamSynchronize(stream_));
     const float* g = b_.Gr ? b_.Gr : b_.G;
     HIP_CHECK(hipMemcpy(t.data(), g + kConvNetNParam, 3 * sizeof(float), hipMemcpyDeviceToHost));
     return t;
   }
   void flush() {
+    gather();
     HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
   }
   // timed runs: k steps + the flush of the last deferred update as one graph
@@ -132,7 +176,7 @@ class ConvNetTrainer : public StepExecutor {
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
     HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
-    if (!grad_allreduce_) return;
+    if (!grad_allreduce_ || sharded_) return;  // sharded: the exchange is inside the step kernels
     // the conv gradient is int64 fixed point (hconv): reduced exactly, in the same call as
     // the fp32 gradient + metric buffer; both parities (see convnet_step2.hip)
     long long* aux = b_.hconv;
@@ -150,6 +194,8 @@ class ConvNetTrainer : public StepExecutor {
   float* G_own_ = nullptr;         // the engine's gradient buffer (b_.G unless folded)
   long long* hconv_own_ = nullptr;
   bool fold_ = false;
+  bool sharded_ = false;
+  XArgs xa_{};  // b_.xa points here (kernels take it by value at launch)
   int B_, PP_, grad_allreduce_;
 };
 
@@ -237,6 +283,12 @@ PYBIND11_MODULE(_C, m) {
       .def("set_peer", [](ConvNetTrainer& t, PeerAllreduce* p, bool fold) { t.set_peer_fold(p, fold); },
            py::arg("peer"), py::arg("fold") = false, py::keep_alive<1, 2>())
       .def_property_readonly("folded", &ConvNetTrainer::folded)
+      .def("set_sharded", &ConvNetTrainer::set_sharded, py::arg("peer"), py::arg("hred"), py::arg("gbf16") = 0,
+           py::keep_alive<1, 2>())
+      .def_property_readonly("sharded", &ConvNetTrainer::sharded)
+      .def("set_exchange_timeout", &ConvNetTrainer::set_exchange_timeout)
+      .def("gather", &ConvNetTrainer::gather)
+      .def("restrict_cus", &ConvNetTrainer::restrict_cus, py::arg("part"), py::arg("nparts"))
       .def("metric_tail", &ConvNetTrainer::metric_tail)
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
       .def("capture", &ConvNetTrainer::capture)

@@ -5,6 +5,33 @@
 
 namespace damd {
 struct Ctrl;
+
+// ---- sharded gradient exchange of the multi-rank step (world > 1, one GPU per rank) ----
+// The dW1 gradient is split into units (slice s, 16-column quarter q) = 96 x 16 values; unit
+// u = 4 s + q is owned by rank u % world.  bwd pushes each unit's partial to its owner, the
+// owner's bwd sums the world partials in rank order and pushes the reduced unit to every
+// rank; the small gradients (conv, b1 / W2 / b2) and the metric tail travel as one message
+// per rank that every rank sums in rank order.  All buffers below live in uncached device
+// memory exported over IPC (PeerAllreduce's staging), mapped on every rank.
+constexpr int kXMaxRanks = 8;
+constexpr int kXPSlot = 2048;        // floats per (source, unit) partial slot (fragment layout)
+constexpr int kXSmsg = 1408;         // floats per small message: 320 int64 conv | 714 grads | 3 metrics
+constexpr long kXGred = 0;           // out: reduced gradient, flat [kConvNetNGrad] (W1 part from owners)
+constexpr long kXSmall = 347648;     // out: small messages [2 parity][kXMaxRanks][kXSmsg]
+constexpr long kXFlags = kXSmall + 2L * kXMaxRanks * kXSmsg;  // out: flag words (unsigned)
+constexpr int kXPFlagPitch = 2 * kXMaxRanks;                  // partial flags [unit][src * 2 + half]
+struct XArgs {
+  float* in[kXMaxRanks];    // rank p's partial staging [src][unit][kXPSlot]
+  float* out[kXMaxRanks];   // rank p's gred | small messages | flags
+  unsigned* status;         // local error word (a bounded wait expired)
+  unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  int world, rank;          // world <= 1: not sharded
+  int gbf16;                // DAMD_GRAD_DTYPE=bf16: partials and reduced units travel as bf16
+};
+constexpr long kXG16 = kXFlags + 16384;  // out: bf16 reduced dW1 [5408][64] (DAMD_GRAD_DTYPE=bf16)
+// floats of `out` the exchange needs for nunits units (<= 909 units: the flag area)
+inline long convnet_xout_floats(int nunits) { return kXG16 + 5408L * 64 / 2; }
+inline long convnet_xin_floats(int world, int nunits) { return (long)world * nunits * kXPSlot; }
 // X / labels are the epoch-permuted copies of the dataset (row g = global sample g).
 struct ConvNetBuffers {
   const void* X; const int* labels;  // X: fp32 [n][784], or uint8 [n][784] when x_u8
@@ -26,6 +53,10 @@ struct ConvNetBuffers {
   // fwd, bwd's metric fold and flush read Gr / hconv_r.  Null: G / hconv.
   float* Gr;
   long long* hconv_r;
+  // sharded multi-rank step (world > 1): the exchange staging of every rank; null otherwise.
+  // Then Gr = this rank's gradient staging and hconv_r = the conv-gradient sums that
+  // convnet2_launch_gather fills for flush / the host
+  const XArgs* xa;
 };
 constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;
@@ -39,6 +70,8 @@ hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStrea
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st);
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st);
+// sharded step: gather the pending update's reduced small gradients (before flush / host reads)
+hipError_t convnet2_launch_gather(const ConvNetBuffers& b, int PP, hipStream_t st);
 hipError_t convnet2_set_lds_limits();
 // elements of the all-reduced gradient buffer
 size_t convnet_grad_count(int PP);

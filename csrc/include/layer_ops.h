@@ -104,8 +104,10 @@ hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n,
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t s);
 // uint8 (k) -> bf16(k * scale)
 hipError_t cast_u8_bf16(const uint8_t* x, float scale, uint16_t* y, long n, hipStream_t s);
-// out[n] += sum_m x[m][n]  (x bf16 or fp32, [M][ld])
-hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hipStream_t s);
+// out[n] += sum_m x[m][n]  (x bf16 or fp32, [M][ld]) in a fixed order; when
+// colsum_splits(M, N) > 1 the row splits go through ws[splits][N] (fp32 workspace)
+int colsum_splits(int M, int N);
+hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, float* ws, hipStream_t s);
 
 // Loss --------------------------------------------------------------------------------------
 // Sparse softmax cross-entropy from fp32 logits [B][ld]: dlogits (bf16, [B][K]) =
@@ -114,8 +116,10 @@ hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hi
 // gradient, no loss/metric).  ctrl != nullptr: scale = 1 / real rows of the global batch
 // (short final batch; see softmax_xent_k), else the given scale.
 // dlogits shares the row pitch ld of the logits; its padding columns are left untouched.
+// rows: scratch of 3 B floats + one int arrival counter (zero before the first call; the
+// kernel re-arms it): the batch sums are formed in a fixed order, not by float atomics.
 hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale,
-                        const Ctrl* ctrl, uint16_t* dlogits, float* tail, hipStream_t s);
+                        const Ctrl* ctrl, uint16_t* dlogits, float* tail, float* rows, hipStream_t s);
 
 // Optimizer ---------------------------------------------------------------------------------
 // flat multi-tensor Keras SGD over the master buffer: P, V fp32 updated from G; Pb = bf16(P)

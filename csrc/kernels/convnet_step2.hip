@@ -51,6 +51,53 @@ constexpr int ZP = 11;                          // pitch of the logit / dz rows
 constexpr int HEAD_FLOATS = CH * HPITCH + 716 + CH * ZP + 2 * CH + 16 * HID + CH;
 constexpr int HEAD_BYTES = HEAD_FLOATS * 4;
 
+// ---- sharded multi-rank exchange (XArgs, convnet.h) ----------------------------------
+// Flag words live in every rank's uncached `out` staging; a flag holds the exchange epoch
+// E (ctrl.xcnt after the step's bwd) of the last message it announces.  Publish: a wave
+// drains its stores (s_waitcnt vmcnt(0): uncached stores are acknowledged by the owning
+// device's memory) and one lane stores E with a relaxed system-scope atomic.  Consume: a
+// lane polls with relaxed system-scope loads; the data loads follow in program order
+// (uncached: nothing stale in any L1 / L2).  Every wait is bounded: on expiry the status
+// word records which kind of wait expired and the kernel goes on (no GPU hang; the host
+// raises on a non-zero status).
+constexpr int SM_CONV = 0, SM_GRAD = 2 * NCONV, SM_MET = SM_GRAD + NSMALL;  // small-message fields
+static_assert(SM_MET + 3 <= kXSmsg, "small message");
+__device__ __forceinline__ unsigned* x_flags(float* out) { return reinterpret_cast<unsigned*>(out + kXFlags); }
+__device__ __forceinline__ unsigned* x_pflag(float* out, int u, int slot) {
+  return x_flags(out) + u * kXPFlagPitch + slot;
+}
+__device__ __forceinline__ unsigned* x_gflag(float* out, int nu, int u, int half) {
+  return x_flags(out) + nu * kXPFlagPitch + u * 2 + half;
+}
+__device__ __forceinline__ unsigned* x_sflag(float* out, int nu, int par, int src) {
+  return x_flags(out) + nu * (kXPFlagPitch + 2) + par * kXMaxRanks + src;
+}
+__device__ __forceinline__ float* x_small(float* out, int par, int src) {
+  return out + kXSmall + ((long)par * kXMaxRanks + src) * kXSmsg;
+}
+__device__ __forceinline__ void x_signal(unsigned* f, unsigned e) {
+  __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void x_wait(const XArgs& xa, unsigned* f, unsigned e, unsigned bit) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+    __builtin_amdgcn_s_sleep(1);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+      __hip_atomic_fetch_or(xa.status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+  }
+}
+constexpr unsigned XW_SMALL = 1u << 8, XW_UNIT = 1u << 9, XW_PART = 1u << 10;  // status bits
+__device__ __forceinline__ uint2 pack_bf16x4(const f32x4& v) {
+  return make_uint2((uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16),
+                    (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+}
+__device__ __forceinline__ float4 unpack_bf16x4(uint2 q) {
+  return make_float4(bf2f((uint16_t)(q.x & 0xffffu)), bf2f((uint16_t)(q.x >> 16)), bf2f((uint16_t)(q.y & 0xffffu)),
+                     bf2f((uint16_t)(q.y >> 16)));
+}
+
 // =================================================================================
 // fwd: grid (NS slices, IG image groups of IB = 2^lg images)
 // =================================================================================
@@ -64,9 +111,11 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
                                            uint16_t* __restrict__ pooled, uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv,
                                            float* __restrict__ calt, int B, int PP, int lg, int eager,
-                                           unsigned long long* st, const long long* __restrict__ hconv_r) {
+                                           unsigned long long* st, const long long* __restrict__ hconv_r,
+                                           const XArgs xa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
   const int nblk = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + s;
   Stamps sts;
   stamp(sts, st, 0);
@@ -94,20 +143,22 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // (bwd added it into hconv[par ^ 1])
   const int tcl = min(tid, NCONV - 1);
   const float cp0 = P[tcl], cp1 = calt[tcl], cv0 = V[tcl], cv1 = calt[NCONV + tcl];
-  const long long cq0 = hconv_r[NCONV + tcl], cq1 = hconv_r[tcl];
+  const long long cq0 = sh ? 0 : hconv_r[NCONV + tcl], cq1 = sh ? 0 : hconv_r[tcl];
   // b1/W2/b2: the grid's last two blocks own their pending update (nobody else in this
   // launch reads them; bwd reads the updated values)
   const int si = (lin - (nblk - 2)) * 512 + tid;
   const bool small_on = lin >= nblk - 2 && si >= 0 && si < NSMALL;
   const int sic = OFF_B1 + max(0, min(si, NSMALL - 1));
-  const float sp = P[sic], sg = G[sic], sv = V[sic];
+  const float sp = P[sic], sg0 = sh ? 0.f : G[sic], sv = V[sic];
   __builtin_amdgcn_sched_barrier(0);
 
   const Ctrl c = *ctrl;
   const int par = c.wpar;
+  const unsigned xe = (unsigned)c.xcnt;  // sharded: exchange epoch of the pending update
   if (lin == 0 && tid == 0) {
     ctrl->cur2 = c.cursor;
     ctrl->par2 = par;
+    ctrl->xcnt2 = c.xcnt;
   }
   const bool pend = c.pending != 0;
   const long row_base = (long)c.cursor * c.global_batch + c.row0 + img0;
@@ -135,13 +186,37 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     for (int u = 0; u < 4; ++u) {
       const int ic = min(tid + u * 512, n4 - 1);
       wv[u] = P4[ic];
-      gv[u] = G4[ic];
+      gv[u] = sh ? make_float4(0.f, 0.f, 0.f, 0.f) : G4[ic];  // sharded: after its unit flags
       vv[u] = V4[ic];
     }
   }
   __builtin_amdgcn_sched_barrier(0);
   const float cp = par ? cp1 : cp0, cv = par ? cv1 : cv0;
-  const long long cq = par ? cq1 : cq0;
+  long long cq = par ? cq1 : cq0;
+  float sg = sg0;
+  // sharded: the previous step's conv / b1 / W2 / b2 gradients and metric tail are the
+  // rank-ordered sums of every rank's small message (published by each rank's last bwd block)
+  if (sh && pend) {
+    const int ps = xe & 1;
+    float* xo = xa.out[xa.rank];
+    if (tid < xa.world) x_wait(xa, x_sflag(xo, 4 * gridDim.x, ps, tid), xe, XW_SMALL);
+    __syncthreads();
+    long long q = 0;
+    float g = 0.f;
+    for (int r = 0; r < xa.world; ++r) {
+      const float* m = x_small(xo, ps, r);
+      q += reinterpret_cast<const long long*>(m + SM_CONV)[tcl];
+      if (small_on) g += m[SM_GRAD + max(0, min(si, NSMALL - 1))];
+    }
+    cq = q;
+    sg = g;
+    if (lin == nblk - 1 && tid < 3) {  // fold the reduced metric tail into the epoch totals
+      float a = 0.f;
+      for (int r = 0; r < xa.world; ++r) a += x_small(xo, ps, r)[SM_MET + tid];
+      float* accp = tid == 0 ? &ctrl->acc_loss : (tid == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
+      *accp = (tid == 0 ? c.acc_loss : (tid == 1 ? c.acc_correct : c.acc_count)) + a;
+    }
+  }
 
   // ---- pending SGD updates ----
   if (eager) {
@@ -159,38 +234,47 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
       }
     }
   }
+  // deferred W1 update of the slice (registers -> bf16 W1^T tile in LDS; the image group 0
+  // block also writes the next fp32 buffer, velocity and bf16 copy)
+  auto w1_update = [&]() __attribute__((always_inline)) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int i = tid + u * 512;
-    if (!eager && i < n4) {
-      float4 wn, vn;
-      sgd_or_keep(pend, wv[u].x, gv[u].x, vv[u].x, c, wn.x, vn.x);
-      sgd_or_keep(pend, wv[u].y, gv[u].y, vv[u].y, c, wn.y, vn.y);
-      sgd_or_keep(pend, wv[u].z, gv[u].z, vv[u].z, c, wn.z, vn.z);
-      sgd_or_keep(pend, wv[u].w, gv[u].w, vv[u].w, c, wn.w, vn.w);
-      const int e = i * 4, kr = e >> 6, n = e & 63;
-      const uint16_t h0 = f2bf(wn.x), h1 = f2bf(wn.y), h2 = f2bf(wn.z), h3 = f2bf(wn.w);
-      w1t[(n + 0) * KP + kr] = h0;
-      w1t[(n + 1) * KP + kr] = h1;
-      w1t[(n + 2) * KP + kr] = h2;
-      w1t[(n + 3) * KP + kr] = h3;
-      if (owner) {
-        Wn4[i] = wn;
-        if (mom) Vn4[i] = vn;
-        Wb[i] = make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), (uint32_t)h2 | ((uint32_t)h3 << 16));
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + u * 512;
+      if (!eager && i < n4) {
+        float4 wn, vn;
+        sgd_or_keep(pend, wv[u].x, gv[u].x, vv[u].x, c, wn.x, vn.x);
+        sgd_or_keep(pend, wv[u].y, gv[u].y, vv[u].y, c, wn.y, vn.y);
+        sgd_or_keep(pend, wv[u].z, gv[u].z, vv[u].z, c, wn.z, vn.z);
+        sgd_or_keep(pend, wv[u].w, gv[u].w, vv[u].w, c, wn.w, vn.w);
+        const int e = i * 4, kr = e >> 6, n = e & 63;
+        const uint16_t h0 = f2bf(wn.x), h1 = f2bf(wn.y), h2 = f2bf(wn.z), h3 = f2bf(wn.w);
+        w1t[(n + 0) * KP + kr] = h0;
+        w1t[(n + 1) * KP + kr] = h1;
+        w1t[(n + 2) * KP + kr] = h2;
+        w1t[(n + 3) * KP + kr] = h3;
+        if (owner) {
+          Wn4[i] = wn;
+          if (mom) Vn4[i] = vn;
+          Wb[i] = make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), (uint32_t)h2 | ((uint32_t)h3 << 16));
+        }
       }
     }
-  }
+  };
+  if (!sh) w1_update();
   float cwn = 0.f, cvn = 0.f;
   if (tid < NCONV) {
     sgd_or_keep(pend, cp, from_fix(cq, CINV), cv, c, cwn, cvn);
     cw[tid] = cwn;
+    // the conv epilogue's ReLU (fmaxf) and the head's would turn a NaN parameter into 0:
+    // a non-finite conv / b1 / W2 / b2 value raises ctrl.bad (loss NaN) here instead
+    if (!__builtin_isfinite(cwn)) __hip_atomic_fetch_or(&ctrl->bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (small_on) {
     float wn, vn;
     sgd_or_keep(pend, sp, sg, sv, c, wn, vn);
     P[sic] = wn;
     if (mom) V[sic] = vn;
+    if (!__builtin_isfinite(wn)) __hip_atomic_fetch_or(&ctrl->bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // the owner writes the next conv buffer and zeroes the hconv parity bwd adds into next
   if (lin == 0 && tid < NCONV) {
@@ -235,6 +319,25 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
       *reinterpret_cast<uint32_t*>(code + (long)(img0 + bo) * FEAT + p0 * NF + 4 * w) =
           reinterpret_cast<const uint32_t*>(csl + bo * K)[w];
   }
+  if (sh) {
+    // sharded: the slice's reduced dW1 arrives as 4 units (2 halves each) from their owners,
+    // pushed at the end of every owner's bwd -- waited for only now, after the conv
+    if (pend) {
+      if (tid < 8) x_wait(xa, x_gflag(xa.out[xa.rank], 4 * gridDim.x, 4 * s + (tid >> 1), tid & 1), xe, XW_UNIT);
+      __syncthreads();
+      if (xa.gbf16) {
+        const uint2* R2 = reinterpret_cast<const uint2*>(xa.out[xa.rank] + kXG16) + p0 * 32 * HID / 4;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gv[u] = unpack_bf16x4(R2[min(tid + u * 512, n4 - 1)]);
+      } else {
+        const float4* R4 = reinterpret_cast<const float4*>(xa.out[xa.rank] + kXGred + OFF_W1 + p0 * 32 * HID);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gv[u] = R4[min(tid + u * 512, n4 - 1)];
+      }
+    }
+    w1_update();
+    lds_barrier();
+  }
   // ---- dense-1 partial of the slice: part[row][n] = sum_k pooled[row][k] W1[k][n] ----
   const int ko = 8 * (lane >> 4);
   const int ntiles = (IB >> 4) * 4;
@@ -262,6 +365,103 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
 }
 
 // =================================================================================
+// sharded exchange, end of bwd (every wave of every block calls it)
+// =================================================================================
+//  1. the partial pushes of this wave have drained (nothing else was issued since, so the
+//     wait costs nothing): raise the partial flag at the owner
+//  2. arrival ticket: the last block of the launch reads this rank's conv-gradient int64
+//     sums, b1 / W2 / b2 gradient and metric tail (all complete: every block drained its
+//     stores before its ticket) and publishes them as this rank's small message on every rank
+//  3. owner waves: wait for the other ranks' halves of their unit, sum the world partials
+//     in rank order (own from registers), push the reduced unit to every rank's gradient
+//     staging, raise the unit flag there
+__device__ __forceinline__ void exchange_tail(const XArgs& xa, Ctrl* ctrl, const float* G, const long long* hconv_p,
+                                              const f32x4* accw, unsigned xe, int s, int NS, int np, int p0, int dn,
+                                              int dm0, int lane, int tid, bool xown, int xo, int xu) {
+  __shared__ int last_flag;
+  const int NU = 4 * NS, W = xa.world, ps = xe & 1;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (!xown && lane == 0) x_signal(x_pflag(xa.out[xo], xu, xa.rank * 2 + dm0), xe);
+  // 2. ticket (counts forever: NS arrivals per step)
+  __syncthreads();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const int t = __hip_atomic_fetch_add(&ctrl->ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t % NS) == NS - 1;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    last_flag = last;
+  }
+  __syncthreads();
+  if (last_flag) {
+    const float* hc = reinterpret_cast<const float*>(hconv_p);
+    for (int i = tid; i < SM_MET + 3; i += 512) {
+      const float v = i < SM_GRAD ? hc[i] : (i < SM_MET ? G[OFF_B1 + i - SM_GRAD] : G[OFF_LOSS + i - SM_MET]);
+      for (int r = 0; r < W; ++r) x_small(xa.out[r], ps, xa.rank)[i] = v;
+    }
+    __syncthreads();  // (drains every wave's stores)
+    if (tid < W) x_signal(x_sflag(xa.out[tid], NU, ps, xa.rank), xe);
+  }
+  // 3. owners
+  if (xown) {
+    if (lane < W && lane != xa.rank) x_wait(xa, x_pflag(xa.out[xa.rank], xu, lane * 2 + dm0), xe, XW_PART);
+    asm volatile("" ::: "memory");
+    f32x4 g[MAXPP];
+#pragma unroll
+    for (int i = 0; i < MAXPP; ++i) g[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < W; ++r) {
+      const float* slot = xa.in[xa.rank] + ((long)r * NU + xu) * kXPSlot;
+#pragma unroll
+      for (int i = 0; i < MAXPP; ++i) {
+        if (i >= np) break;
+        float4 v;
+        if (xa.gbf16)  // own partial rounded like the others': the sum is symmetric in the ranks
+          v = unpack_bf16x4(r == xa.rank ? pack_bf16x4(accw[i])
+                                         : reinterpret_cast<const uint2*>(slot)[(dm0 * MAXPP + i) * 64 + lane]);
+        else
+          v = r == xa.rank ? make_float4(accw[i][0], accw[i][1], accw[i][2], accw[i][3])
+                           : reinterpret_cast<const float4*>(slot)[(dm0 * MAXPP + i) * 64 + lane];
+        g[i][0] += v.x;
+        g[i][1] += v.y;
+        g[i][2] += v.z;
+        g[i][3] += v.w;
+      }
+    }
+    const int lr16 = lane & 15;
+    if (xa.gbf16) {
+      // bf16 reduced unit, row-major [k][n]: column pairs packed into 32-bit words (the even
+      // lane of each pair stores both), i.e. 16 lanes write one 32-byte row piece
+      for (int r = 0; r < W; ++r) {
+        uint32_t* dst = reinterpret_cast<uint32_t*>(xa.out[r] + kXG16) + ((long)p0 * 32 * HID + 16 * dn + lr16) / 2;
+#pragma unroll
+        for (int i = 0; i < MAXPP; ++i) {
+          if (i >= np) break;
+          const int mt = dm0 + 2 * i;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t h = f2bf(g[i][j]);
+            const uint32_t o = (uint32_t)__shfl_xor((int)h, 1);
+            if (!(lr16 & 1)) dst[(16 * mt + 4 * (lane >> 4) + j) * (HID / 2)] = h | (o << 16);
+          }
+        }
+      }
+    } else {
+      for (int r = 0; r < W; ++r) {
+        float* dst = xa.out[r] + kXGred + OFF_W1 + (long)p0 * 32 * HID + 16 * dn + lr16;
+#pragma unroll
+        for (int i = 0; i < MAXPP; ++i) {
+          if (i >= np) break;
+          const int mt = dm0 + 2 * i;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dst[(16 * mt + 4 * (lane >> 4) + j) * HID] = g[i][j];
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane < W) x_signal(x_gflag(xa.out[lane], NU, xu, dm0), xe);
+  }
+}
+
+// =================================================================================
 // bwd: grid NS slices
 // =================================================================================
 // aux element e (parameter order at G + OFF_B1): [0,64) db1, [64,704) dW2
@@ -273,8 +473,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
-                                           unsigned long long* st, const float* __restrict__ Gr) {
+                                           unsigned long long* st, const float* __restrict__ Gr, const XArgs xa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   Stamps sts;
   stamp(sts, st, 0);
   const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x;
@@ -316,7 +517,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   // ---- prologue: first the loads whose addresses do not depend on the ctrl block (the
   // previous metric, b1/W2/b2, the bf16 W1 slice, chunk 0's pooled tile and argmax codes),
   // kept ahead of the ctrl load by a scheduling barrier (as in fwd) ----
-  const float ag_old = Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];  // previous step's reduced metric
+  // previous step's reduced metric (sharded: fwd folds it from the small messages)
+  const float ag_old = sh ? 0.f : Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];
   // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
   const float spv0 = P[OFF_B1 + tid], spv1 = P[OFF_B1 + min(tid + 512, NSMALL - 1)];
   const int n8 = K * HID / 8;
@@ -349,12 +551,14 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 
   const Ctrl c = *ctrl;
   const int cur = c.cur2, par = c.par2;
+  const unsigned xe = (unsigned)c.xcnt2 + 1u;  // sharded: this step's exchange epoch
   const long long* hcur = hacc + (long)par * B * HID;
   if (s == 0 && tid == 0) {
     ctrl->cursor = next_cursor(c, cur);
     ctrl->iterations = c.iterations + 1;
     ctrl->wpar = c.wpar ^ 1;  // fwd of this step wrote the next W1 buffer
     ctrl->pending = 1;
+    if (sh) ctrl->xcnt = (int)xe;
   }
   const long gstart = (long)cur * c.global_batch;
   const long row_base = gstart + c.row0;
@@ -407,6 +611,26 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   f32x4 accw[MAXPP];
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) accw[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ---- sharded exchange: this wave's dW1 tiles form half of unit u = 4 s + dn (rows of
+  // tiles dm0 + 2 i, 16 columns), owned by rank u % world ----
+  const int NU = 4 * NS, xu = 4 * s + dn;
+  const int xo = sh ? xu % xa.world : 0;
+  const bool xown = sh && xo == xa.rank;
+  auto push_partials = [&]() __attribute__((always_inline)) {
+    if (!sh || xown) return;
+    float* slot = xa.in[xo] + ((long)xa.rank * NU + xu) * kXPSlot;
+    if (xa.gbf16) {  // bf16 partials: half the bytes (the owner accumulates in fp32)
+      uint2* dst = reinterpret_cast<uint2*>(slot) + dm0 * MAXPP * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < MAXPP; ++i)
+        if (i < np) dst[i * 64] = pack_bf16x4(accw[i]);
+    } else {
+      float4* dst = reinterpret_cast<float4*>(slot) + dm0 * MAXPP * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < MAXPP; ++i)
+        if (i < np) dst[i * 64] = make_float4(accw[i][0], accw[i][1], accw[i][2], accw[i][3]);
+    }
+  };
   const int ch = tid & 31, grp = tid >> 5;
   float gw[9], gb = 0.f;
 #pragma unroll
@@ -566,6 +790,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
         accw[i] = mfma16(a, bl, accw[i]);
       }
     }
+    // sharded: a unit owned by another rank leaves now (data only; its flag is raised once
+    // the stores have drained, after the conv gradient) and travels during dP / conv grad
+    if (ONE && sh) push_partials();
     // eager: the slice's SGD update now, its stores overlapping dP and the conv gradient
     // (fp32 master and velocity in place, bf16 copy for the next fwd; this block read its
     // old bf16 slice in the prologue and nobody else touches the slice in this launch)
@@ -628,11 +855,12 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     }
   }
   stamp(sts, st, 4);
+  if (!ONE && sh) push_partials();
   // ---- dW1 straight into the flat gradient buffer (this block owns these rows), unless
-  // the update was applied eagerly above ----
+  // the update was applied eagerly above or the exchange carries it ----
 #pragma unroll
   for (int i = 0; i < MAXPP; ++i) {
-    if (i >= np || (ONE && eager)) break;
+    if (i >= np || (ONE && eager) || sh) break;
     const int mt = dm0 + 2 * i;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -665,7 +893,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       const int m = ae - NSMALL;  // 0 loss, 1 correct, 2 count
       float* accp = m == 0 ? &ctrl->acc_loss : (m == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
       const float old = m == 0 ? c.acc_loss : (m == 1 ? c.acc_correct : c.acc_count);
-      *accp = old + ag_old;  // fold the previous step's all-reduced metric into the epoch total
+      if (!sh) *accp = old + ag_old;  // fold the previous step's all-reduced metric into the epoch total
       // (a non-finite / out-of-range fixed-point input so far: the loss is NaN from now on)
       G[OFF_LOSS + m] = m == 0 && c.bad ? __builtin_nanf("") : m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
@@ -676,6 +904,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     uint4* h4 = reinterpret_cast<uint4*>(hacc + (long)(par ^ 1) * B * HID);
     for (int i = s * 512 + tid; i < B * HID / 2; i += NS * 512) h4[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  if (sh) exchange_tail(xa, ctrl, G, hconv + par * NCONV, accw, xe, s, NS, np, p0, dn, dm0, lane, tid, xown, xo, xu);
   stamp(sts, st, 5);
   stamp_flush(sts, st, 9);
 }
@@ -686,7 +915,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 // =================================================================================
 // G / hconv: the reduced gradient (the peer all-reduce's `out` when it is folded into the
 // step, see ConvNetBuffers::Gr); hconv_w: the buffer bwd adds into (both parities cleared)
-__global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
+__global__ __launch_bounds__(256) void flush(float* __restrict__ P, const float* __restrict__ G, float* __restrict__ V,
                                              const float* __restrict__ W1alt, const float* __restrict__ V1alt,
                                              long long* __restrict__ hconv, const float* __restrict__ calt,
                                              long long* __restrict__ hacc, int B, int eager,
@@ -712,7 +941,6 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
     P[i] = wn;
     if (mom) V[i] = vn;
     if (w1) w1bf[i - OFF_W1] = f2bf(wn);
-    G[i] = 0.f;
   }
   // both parities of the fixed-point accumulators start the next step at zero
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * NCONV + 2 * B * HID; i += gridDim.x * blockDim.x) {
@@ -722,11 +950,10 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
     }
     else hacc[i - 2 * NCONV] = 0;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && pend) {  // (G is read only while an update is pending)
     ctrl->acc_loss = c.acc_loss + G[OFF_LOSS];
     ctrl->acc_correct = c.acc_correct + G[OFF_CORR];
     ctrl->acc_count = c.acc_count + G[OFF_CNT];
-    for (int i = NPARAM; i < NGRAD; ++i) G[i] = 0.f;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -735,7 +962,51 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
       ctrl->wpar = 0;
       ctrl->pending = 0;
       ctrl->flush_ticket = 0;
+      ctrl->ticket = 0;  // (the sharded bwd's arrival count: bounded between flushes)
     }
+  }
+}
+
+// =================================================================================
+// sharded step: the pending update's reduced gradient gathered for flush / the host
+// (waits for every unit and every rank's small message of the last exchange epoch, then
+// writes the small sums into the gradient staging's b1 / W2 / b2 / metric slots and the
+// conv sum into hred[wpar ^ 1], where flush reads them).  One block; nothing pending: no-op.
+// It depends only on every rank having run that step's bwd -- not on their calling it.
+// =================================================================================
+__global__ __launch_bounds__(512) void sh_gather(Ctrl* __restrict__ ctrl, const XArgs xa, long long* __restrict__ hred,
+                                                 int NS, int PP) {
+  const Ctrl c = *ctrl;
+  if (!c.pending) return;
+  const unsigned xe = (unsigned)c.xcnt;
+  const int ps = xe & 1, NU = 4 * NS, tid = threadIdx.x;
+  float* xo = xa.out[xa.rank];
+  // every block: its units (u = block, block + grid, ...); bf16 exchange: expanded into the
+  // fp32 staging that flush reads
+  for (int u = blockIdx.x; u < NU; u += gridDim.x) {
+    if (tid < 2) x_wait(xa, x_gflag(xo, NU, u, tid), xe, XW_UNIT);
+    __syncthreads();
+    if (xa.gbf16) {
+      const int sl = u >> 2, q = u & 3, k0 = sl * PP * 32, k1 = min(FEAT, k0 + PP * 32);
+      const uint16_t* g16 = reinterpret_cast<const uint16_t*>(xo + kXG16);
+      for (int e = tid; e < (k1 - k0) * 16; e += 512) {
+        const long idx = (long)(k0 + (e >> 4)) * HID + 16 * q + (e & 15);
+        xo[kXGred + OFF_W1 + idx] = bf2f(g16[idx]);
+      }
+    }
+  }
+  if (blockIdx.x != 0) return;
+  if (tid < xa.world) x_wait(xa, x_sflag(xo, NU, ps, tid), xe, XW_SMALL);
+  __syncthreads();
+  for (int i = tid; i < NSMALL + 3; i += 512) {
+    float a = 0.f;
+    for (int r = 0; r < xa.world; ++r) a += x_small(xo, ps, r)[SM_GRAD + i];
+    xo[kXGred + (i < NSMALL ? OFF_B1 + i : OFF_LOSS + i - NSMALL)] = a;
+  }
+  for (int i = tid; i < NCONV; i += 512) {
+    long long q = 0;
+    for (int r = 0; r < xa.world; ++r) q += reinterpret_cast<const long long*>(x_small(xo, ps, r) + SM_CONV)[i];
+    hred[(c.wpar ^ 1) * NCONV + i] = q;
   }
 }
 
@@ -770,6 +1041,12 @@ size_t convnet2_bwd_lds(int PP) {
 // eager W1 update: world-1 runs with the single-chunk backward (B <= 64) only
 static int eager2(const ConvNetBuffers& b, int B) { return b.eager_w1 && B <= convnet::CH ? 1 : 0; }
 
+static XArgs xargs(const ConvNetBuffers& b) {
+  if (b.xa) return *b.xa;
+  XArgs a{};
+  return a;  // world 0: not sharded
+}
+
 template <bool U8>
 static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
@@ -779,7 +1056,7 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P,
                      b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, eager2(b, B), b.stamps,
-                     b.hconv_r ? b.hconv_r : b.hconv);
+                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b));
 }
 
 template <bool U8>
@@ -789,11 +1066,13 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G);
+                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
+                       xargs(b));
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G);
+                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
+                       xargs(b));
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
@@ -814,6 +1093,13 @@ hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream
 hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   hipError_t e = convnet2_launch_fwd(b, B, PP, st);
   return e != hipSuccess ? e : convnet2_launch_bwd(b, B, PP, st);
+}
+
+hipError_t convnet2_launch_gather(const ConvNetBuffers& b, int PP, hipStream_t st) {
+  if (!b.xa || b.xa->world < 2 || !b.hconv_r) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(convnet2::sh_gather, dim3(57), dim3(512), 0, st, b.ctrl, *b.xa, b.hconv_r, convnet_num_slices(PP),
+                     PP);
+  return hipGetLastError();
 }
 
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {

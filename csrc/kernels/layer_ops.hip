@@ -1232,8 +1232,12 @@ __global__ __launch_bounds__(NT) void cast_u8_bf16_k(const uint8_t* x, float sca
     y[i] = f2bf((float)x[i] * scale);
 }
 
-// out[n] += sum over rows; grid (ceil(N/64), splits), 4 row phases per block
-__global__ __launch_bounds__(NT) void colsum_k(const void* x, int x_f32, int M, int N, int ld, float* out) {
+// Column sums in a fixed order (bias gradients; no float atomics).  grid (ceil(N/64),
+// splits), 4 row phases per block: split y sums rows y*4+ph, y*4+ph + 4*splits, ...; one
+// split adds straight into out[n], several write slab[y][n] and colsum_fin_k adds the
+// slabs in split order.
+__global__ __launch_bounds__(NT) void colsum_k(const void* x, int x_f32, int M, int N, int ld, float* out,
+                                               float* slab) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int n = blockIdx.x * 64 + cl;
@@ -1243,7 +1247,18 @@ __global__ __launch_bounds__(NT) void colsum_k(const void* x, int x_f32, int M, 
       a += x_f32 ? ((const float*)x)[(size_t)m * ld + n] : bf2f(((const uint16_t*)x)[(size_t)m * ld + n]);
   red[ph][cl] = a;
   __syncthreads();
-  if (ph == 0 && n < N) atomicAdd(out + n, red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl]);
+  if (ph == 0 && n < N) {
+    const float v = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    if (gridDim.y == 1) out[n] += v;
+    else slab[(size_t)blockIdx.y * N + n] = v;
+  }
+}
+__global__ __launch_bounds__(NT) void colsum_fin_k(const float* slab, int splits, int N, float* out) {
+  const int n = blockIdx.x * NT + threadIdx.x;
+  if (n >= N) return;
+  float a = 0.f;
+  for (int y = 0; y < splits; ++y) a += slab[(size_t)y * N + n];
+  out[n] += a;
 }
 
 // ---- loss ------------------------------------------------------------------------------------
@@ -1254,61 +1269,85 @@ __global__ __launch_bounds__(NT) void colsum_k(const void* x, int x_f32, int M, 
 __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ logits, int ld,
                                                      const int32_t* __restrict__ labels, int K, float scale,
                                                      const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ dl,
-                                                     float* tail) {
+                                                     float* tail, float* rows) {
   __shared__ float sv[NT];
   __shared__ int si[NT];
-  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ int last;
+  const int b = blockIdx.x, t = threadIdx.x, B = gridDim.x;
   const int y = labels[b];
+  float row_loss = 0.f, row_corr = 0.f;
   if (y < 0) {
     for (int k = t; k < K; k += NT) dl[(size_t)b * ld + k] = 0;
-    return;
-  }
-  if (ctrl) {
-    const int gb = ctrl->global_batch;
-    const int left = ctrl->nsamples - ctrl->cursor * gb;
-    scale = 1.f / (float)(ctrl->wrap > 0 ? gb : max(1, min(gb, left)));
-  }
-  const float* z = logits + (size_t)b * ld;
-  float mx = -INFINITY;
-  int mi = 0x7fffffff;
-  for (int k = t; k < K; k += NT) {
-    const float v = z[k];
-    if (v > mx) { mx = v; mi = k; }
-  }
-  sv[t] = mx;
-  si[t] = mi;
-  __syncthreads();
-  for (int s = NT / 2; s > 0; s >>= 1) {
-    if (t < s) {
-      const float o = sv[t + s];
-      const int oi = si[t + s];
-      if (o > sv[t] || (o == sv[t] && oi < si[t])) { sv[t] = o; si[t] = oi; }
+  } else {
+    if (ctrl) {
+      const int gb = ctrl->global_batch;
+      const int left = ctrl->nsamples - ctrl->cursor * gb;
+      scale = 1.f / (float)(ctrl->wrap > 0 ? gb : max(1, min(gb, left)));
     }
+    const float* z = logits + (size_t)b * ld;
+    float mx = -INFINITY;
+    int mi = 0x7fffffff;
+    for (int k = t; k < K; k += NT) {
+      const float v = z[k];
+      if (v > mx) { mx = v; mi = k; }
+    }
+    sv[t] = mx;
+    si[t] = mi;
     __syncthreads();
-  }
-  const float zmax = sv[0];
-  const int amax = si[0];
-  __syncthreads();
-  float se = 0.f;
-  for (int k = t; k < K; k += NT) se += __expf(z[k] - zmax);
-  sv[t] = se;
-  __syncthreads();
-  for (int s = NT / 2; s > 0; s >>= 1) {
-    if (t < s) sv[t] += sv[t + s];
+    for (int s = NT / 2; s > 0; s >>= 1) {
+      if (t < s) {
+        const float o = sv[t + s];
+        const int oi = si[t + s];
+        if (o > sv[t] || (o == sv[t] && oi < si[t])) { sv[t] = o; si[t] = oi; }
+      }
+      __syncthreads();
+    }
+    const float zmax = sv[0];
+    const int amax = si[0];
     __syncthreads();
+    float se = 0.f;
+    for (int k = t; k < K; k += NT) se += __expf(z[k] - zmax);
+    sv[t] = se;
+    __syncthreads();
+    for (int s = NT / 2; s > 0; s >>= 1) {
+      if (t < s) sv[t] += sv[t + s];
+      __syncthreads();
+    }
+    const float sum = sv[0];
+    const float inv = 1.f / sum;
+    for (int k = t; k < K; k += NT) {
+      const float p = __expf(z[k] - zmax) * inv;
+      dl[(size_t)b * ld + k] = f2bf((p - (k == y ? 1.f : 0.f)) * scale);
+    }
+    row_loss = logf(sum) + zmax - z[y];
+    row_corr = amax == y ? 1.f : 0.f;
   }
-  const float sum = sv[0];
-  const float inv = 1.f / sum;
-  for (int k = t; k < K; k += NT) {
-    const float p = __expf(z[k] - zmax) * inv;
-    dl[(size_t)b * ld + k] = f2bf((p - (k == y ? 1.f : 0.f)) * scale);
-  }
+  // the batch sums in a fixed order (no float atomics: replays and graph / eager runs give
+  // the same bits): every row stores (loss, correct, valid), the last block to arrive adds
+  // them up by a fixed tree and re-arms the arrival counter rows[3 B]
   if (t == 0) {
-    const float loss = logf(sum) + zmax - z[y];
-    atomicAdd(tail, loss);
-    atomicAdd(tail + 1, amax == y ? 1.f : 0.f);
-    atomicAdd(tail + 2, 1.f);
+    rows[3 * b] = row_loss;
+    rows[3 * b + 1] = row_corr;
+    rows[3 * b + 2] = y < 0 ? 0.f : 1.f;
   }
+  int* counter = reinterpret_cast<int*>(rows + 3 * B);
+  if (!last_arriver(counter, B, &last)) return;
+  float a[3] = {0.f, 0.f, 0.f};
+  for (int r = t; r < B; r += NT)
+#pragma unroll
+    for (int q = 0; q < 3; ++q) a[q] += rows[3 * r + q];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    __syncthreads();
+    sv[t] = a[q];
+    __syncthreads();
+    for (int s = NT / 2; s > 0; s >>= 1) {
+      if (t < s) sv[t] += sv[t + s];
+      __syncthreads();
+    }
+    if (t == 0) tail[q] += sv[0];
+  }
+  if (t == 0) *counter = 0;
 }
 
 // ---- inference (predict / evaluate through the native forward plan) ----------------------
@@ -1855,17 +1894,24 @@ hipError_t cast_u8_bf16(const uint8_t* x, float scale, uint16_t* y, long n, hipS
   return hipGetLastError();
 }
 
-hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, hipStream_t s) {
-  int splits = (M + 255) / 256;
-  if (splits > 64) splits = 64;
-  if (splits < 1) splits = 1;
-  hipLaunchKernelGGL(colsum_k, dim3((N + 63) / 64, splits), dim3(NT), 0, s, x, x_f32, M, N, ld, out);
+int colsum_splits(int M, int N) {
+  // one pass while the column tiles alone give the chip enough blocks or M is short
+  if (M <= 4096 || (N + 63) / 64 >= 64) return 1;
+  int splits = (M + 1023) / 1024;
+  return splits > 64 ? 64 : splits;
+}
+hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, float* ws, hipStream_t s) {
+  const int splits = colsum_splits(M, N);
+  if (splits > 1 && !ws) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_k, dim3((N + 63) / 64, splits), dim3(NT), 0, s, x, x_f32, M, N, ld, out, ws);
+  if (splits > 1) hipLaunchKernelGGL(colsum_fin_k, dim3((N + NT - 1) / NT), dim3(NT), 0, s, ws, splits, N, out);
   return hipGetLastError();
 }
 
 hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale, const Ctrl* ctrl,
-                        uint16_t* dlogits, float* tail, hipStream_t s) {
-  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, ctrl, dlogits, tail);
+                        uint16_t* dlogits, float* tail, float* rows, hipStream_t s) {
+  if (!rows || B < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, ctrl, dlogits, tail, rows);
   return hipGetLastError();
 }
 

@@ -261,12 +261,15 @@ void register_kernel_ops(py::module_& m) {
   m.def("cast_u8_bf16", [](U x, float scale, U y, long n, U s) {
     check(damd::cast_u8_bf16(P_<const uint8_t>(x), scale, P_<u16>(y), n, P_<ihipStream_t>(s)), "cast_u8_bf16");
   });
-  m.def("colsum", [](U x, int x_f32, int M, int N, int ld, U out, U s) {
-    check(damd::colsum(P_<const void>(x), x_f32, M, N, ld, P_<float>(out), P_<ihipStream_t>(s)), "colsum");
+  m.def("colsum_splits", &damd::colsum_splits);
+  m.def("colsum", [](U x, int x_f32, int M, int N, int ld, U out, U s, U ws) {
+    check(damd::colsum(P_<const void>(x), x_f32, M, N, ld, P_<float>(out), P_<float>(ws), P_<ihipStream_t>(s)),
+          "colsum");
   });
-  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U ctrl, U dl, U tail, U s) {
+  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U ctrl, U dl, U tail, U rows, U s) {
     check(damd::softmax_xent(P_<const float>(logits), ld, P_<const int32_t>(labels), B, K, scale,
-                             P_<const damd::Ctrl>(ctrl), P_<u16>(dl), P_<float>(tail), P_<ihipStream_t>(s)),
+                             P_<const damd::Ctrl>(ctrl), P_<u16>(dl), P_<float>(tail), P_<float>(rows),
+                             P_<ihipStream_t>(s)),
           "softmax_xent");
   });
   m.def("sgd_step", [](U P, U G, U V, U Pb, long n, U ctrl, U tail, U s) {

@@ -81,6 +81,9 @@ class PeerAllreduce {
   // only after this call's previous instance completed on its stream and reads `out` only
   // after this one did (stream order), which is what keeps the buffer reuse safe.
   void allreduce_staged(long n, long n64, hipStream_t st);
+  // the pointer table of every rank's mapped staging (for kernels that exchange through it
+  // directly, e.g. the sharded MNIST step)
+  const PeerArgs& args() const { return a_; }
   float* in_local() const { return in_; }
   float* out_local() const { return out_; }
   // message words (fp32 slots) of a call with n floats and n64 int64 values

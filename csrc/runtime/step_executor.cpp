@@ -120,6 +120,21 @@ void StepExecutor::run(int k) {
   step(k);
 }
 
+void StepExecutor::restrict_cus(int part, int nparts) {
+  if (nparts < 2) return;
+  if (part < 0 || part >= nparts) throw std::invalid_argument("restrict_cus: bad part");
+  hipDeviceProp_t prop;
+  HIP_CHECK(hipGetDeviceProperties(&prop, device_));
+  const int ncu = prop.multiProcessorCount;
+  std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+  for (int cu = part; cu < ncu; cu += nparts) mask[cu / 32] |= 1u << (cu % 32);
+  invalidate_graphs();
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  HIP_CHECK(hipStreamDestroy(stream_));
+  stream_ = nullptr;
+  HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()));
+}
+
 bool StepExecutor::sync(double timeout_s) { return stream_wait_with_deadline(stream_, timeout_s, comm_); }
 
 }  // namespace damd

@@ -45,6 +45,11 @@ class StepExecutor {
   bool warm_final(int k);
   // Block until the stream drains; false on watchdog timeout (comm aborted).
   bool sync(double timeout_s);
+  // Several ranks sharing ONE device (the single-GPU rehearsal of a multi-GPU run): this
+  // rank's step stream is limited to every nparts-th CU starting at `part`, so a rank's
+  // blocks that spin on another rank's message can never occupy the CUs the other rank
+  // needs to produce it.  (One rank per GPU -- the real deployment -- never calls this.)
+  void restrict_cus(int part, int nparts);
   void invalidate_graphs();
   int num_graphs() const { return (int)graphs_.size(); }
 

@@ -149,40 +149,73 @@ class FusedConvNetEngine(Engine):
         # at world 1: the multi-GPU graph path exercised on a single GPU
         force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
         native = strategy.communicator.native if (self.world > 1 or force) else None
-        # per-step gradient all-reduce: the native xGMI peer-to-peer kernel when every rank
-        # can map every peer (DAMD_ALLREDUCE=auto|xgmi), else RCCL inside the captured step
+        # per-step gradient exchange at world > 1 (DAMD_ALLREDUCE):
+        #   auto / sharded -- inside the two step kernels (convnet.h XArgs): each rank owns a
+        #       quarter-slice unit of dW1 per 1/world of the units, bwd pushes partials to the
+        #       owners over xGMI, owners reduce in rank order and push the reduced units back;
+        #       the small gradients + metrics travel as one message per rank.  No extra launch.
+        #   xgmi -- the standalone two-shot peer all-reduce kernel after bwd (folded staging)
+        #   rccl -- RCCL inside the captured step
+        # Both peer modes need every rank to map every peer (one node); else RCCL.
         self.peer = None
+        self.sharded = False
+        self.hred = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)  # sharded: conv sums for flush
         mode = env.get_str("DAMD_ALLREDUCE", "auto").lower()
-        if self.world > 1 and mode in ("auto", "xgmi"):
+        if mode not in ("auto", "sharded", "xgmi", "rccl"):
+            raise ValueError("DAMD_ALLREDUCE must be auto, sharded, xgmi or rccl")
+        # DAMD_GRAD_DTYPE=bf16: the exchanged dW1 travels as bf16 (fp32 accumulation by the
+        # owner, fp32 master update); default fp32 (reference parity)
+        self.grad_dtype = env.get_str("DAMD_GRAD_DTYPE", "fp32").lower()
+        if self.grad_dtype not in ("fp32", "bf16"):
+            raise ValueError("DAMD_GRAD_DTYPE must be fp32 or bf16")
+        if self.world > 1 and mode != "rccl":
             from ..parallel.communicator import make_peer_allreduce
 
             # in-kernel wait deadline: the collective watchdog's when one is set, so a missing
             # peer costs at most that much GPU spinning per wait
             wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
-            n64 = 2 * NCONV
-            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0,
-                                            C.PeerAllreduce.message_words(C.convnet_grad_count(self.PP), n64),
+            want_sharded = mode in ("auto", "sharded") and self.world <= 8
+            if want_sharded:
+                NU = 4 * NS
+                cap = max(self.world * NU * 2048, 347648 + 2 * 8 * 1408 + 16384 + FEAT * HID // 2)
+            else:
+                cap = C.PeerAllreduce.message_words(C.convnet_grad_count(self.PP), 2 * NCONV)
+            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, cap,
                                             blocks=env.get_int("DAMD_PEER_BLOCKS", 64),
                                             timeout_s=wd if wd > 0 else 60.0)
-            if self.peer is None and mode == "xgmi":
-                raise RuntimeError("DAMD_ALLREDUCE=xgmi but the peer-to-peer all-reduce is unavailable")
+            if self.peer is None and mode in ("xgmi", "sharded"):
+                raise RuntimeError(f"DAMD_ALLREDUCE={mode} but the xGMI peer mapping is unavailable")
+            if self.peer is not None and want_sharded:
+                self.trainer.set_sharded(self.peer, self.hred.data_ptr(), int(self.grad_dtype == "bf16"))
+                self.sharded = True
+                # ranks sharing one device (the 1-GPU rehearsal of a multi-GPU run): each
+                # rank's step stream gets its own CUs -- the in-kernel waits of one rank must
+                # not hold the CUs another rank needs to publish what they wait for
+                ndev = max(1, torch.cuda.device_count())
+                share = [q for q in range(self.world) if q % ndev == (dev.index or 0)]
+                if len(share) > 1:
+                    self.trainer.restrict_cus(share.index(self.rank), len(share))
+                # every rank's flags are zero before any rank's first step writes into them
+                strategy.communicator.barrier()
         # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
         # time, the gradient/metric buffer all-reduced through the host between steps
         self.host_collective = self.world > 1 and native is None and self.peer is None
         self.allreduce_kind = ("none" if self.world == 1 and not force else
+                               "xgmi-sharded" if self.sharded else
                                "xgmi-peer" if self.peer is not None else
                                "rccl" if native is not None else "host-gloo")
-        if self.peer is not None:
+        if self.peer is not None and not self.sharded:
             # folded (default): bwd writes its gradient straight into the peer kernel's `in`
             # staging and fwd / flush read the reduced gradient from its `out`, so the peer
             # kernel only exchanges (no copy-in / copy-out passes over the 1.39 MB message)
             self.trainer.set_peer(self.peer, fold=env.get_bool("DAMD_PEER_FOLD", True))
-        elif native is not None:
+        elif self.peer is None and native is not None:
             self.trainer.set_comm(native)
         if self.world > 1:
-            dlog.info("fused ConvNet engine: gradient all-reduce via %s",
-                      "xGMI peer-to-peer kernel" if self.peer is not None else
-                      ("RCCL" if native is not None else "host (gloo)"))
+            dlog.info("fused ConvNet engine: gradient exchange via %s",
+                      {"xgmi-sharded": "the step kernels (sharded xGMI exchange)",
+                       "xgmi-peer": "xGMI peer-to-peer all-reduce kernel", "rccl": "RCCL",
+                       "host-gloo": "host (gloo)"}[self.allreduce_kind])
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph_steps = max(1, env.get_int("DAMD_GRAPH_STEPS", 20))
         self.watchdog_s = env.get_float("DAMD_WATCHDOG_S", 0.0)

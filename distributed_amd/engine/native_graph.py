@@ -458,6 +458,7 @@ class NativeGraphEngine(Engine):
         self.K, self.Kp = K, _pad8(K)
         self.logits = torch.zeros(self.B, self.Kp, dtype=torch.float32, device=dev)
         self.dlogits = torch.zeros(self.B, self.Kp, dtype=torch.bfloat16, device=dev)
+        self.xent_rows = H.xent_rows(self.B, dev)  # fixed-order loss / metric sums
         last.attrs["logits"] = True
         # per-node scratch
         self.st_ident = torch.cat([torch.zeros(1, 1), torch.ones(1, 1), torch.ones(1, 1), torch.zeros(1, 1)])
@@ -488,6 +489,8 @@ class NativeGraphEngine(Engine):
                 ws = max(ws, fplan["ws"], H.conv_dgrad_plan(xshape, wshape, l.strides, l.padding)["ws"])
                 if nd.attrs.get("stats"):
                     nd.attrs["stats_buf"] = torch.zeros(fplan["stats_T"], 2, cout, device=dev)
+                if l.use_bias:  # bias gradient = column sums of dy, fixed order
+                    ws = max(ws, H.colsum_workspace_elems(int(np.prod(nd.out.shape[:-1])), cout))
                 if _act_name(l) != "linear":
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
             elif k == "BatchNormalization":
@@ -505,7 +508,8 @@ class NativeGraphEngine(Engine):
                 l = nd.layer
                 kin, units = l.kernel.shape
                 ws = max(ws, H.wgrad_workspace_elems(kin, _pad8(units), self.B),
-                         H.dense_workspace_elems(self.B, _pad8(units), kin))
+                         H.dense_workspace_elems(self.B, _pad8(units), kin),
+                         H.colsum_workspace_elems(self.B, units))
                 if nd.attrs.get("logits") and units % 8:
                     up = _pad8(units)
                     nd.attrs["w_pad"] = torch.zeros(kin, up, dtype=torch.bfloat16, device=dev)
@@ -778,7 +782,7 @@ class NativeGraphEngine(Engine):
         for nd in live:
             getattr(self, "_fwd_" + nd.kind)(nd)
         H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:],
-                       ctrl=self.ctrl)
+                       ctrl=self.ctrl, rows=self.xent_rows)
         self._mark("forward")
         for t in self._all_tensors():
             t.root().written = False
@@ -972,7 +976,7 @@ class NativeGraphEngine(Engine):
             self._act_bwd(nd, dy, y.buf, nd.attrs["dz"])
             dy = nd.attrs["dz"]
         if l.use_bias:
-            H.colsum(dy, self.gviews[id(l.bias)])
+            H.colsum(dy, self.gviews[id(l.bias)], workspace=self.gemm_ws)
         if nd.attrs.get("stem4"):
             kh, kw, cin, cout = l.kernel.shape
             dwp = nd.attrs["dw_pad"]
@@ -1163,11 +1167,7 @@ class NativeGraphEngine(Engine):
             dy = nd.attrs["dz"]
         units = l.units
         if l.use_bias:
-            if dy.shape[1] != units:
-                self.C.colsum(dy.data_ptr(), 0, dy.shape[0], units, dy.shape[1], self.gviews[id(l.bias)].data_ptr(),
-                              H.stream_handle())
-            else:
-                H.colsum(dy, self.gviews[id(l.bias)])
+            H.colsum(dy, self.gviews[id(l.bias)], workspace=self.gemm_ws, M=dy.shape[0], N=units, ld=dy.shape[1])
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
             H.dense_wgrad(x2, dy, dwp, workspace=self.gemm_ws, accumulate=False)

@@ -135,7 +135,8 @@ class NativeInference(NativeGraphEngine):
                            self._bufs["out"].data_ptr(), s)
             C.step_fold(self.ctrl.data_ptr(), 0, s)
         else:
-            H.softmax_xent(self.logits, self.labels, self.K, 1.0 / B, self.dlogits, self.tail, ctrl=self.ctrl)
+            H.softmax_xent(self.logits, self.labels, self.K, 1.0 / B, self.dlogits, self.tail, ctrl=self.ctrl,
+                           rows=self.xent_rows)
             C.step_fold(self.ctrl.data_ptr(), self.tail.data_ptr(), s)
 
     def _stage(self, x, y=None):

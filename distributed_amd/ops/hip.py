@@ -844,18 +844,38 @@ def add_bf16(a, b, out):
     _C().add_bf16(_ptr(a), _ptr(b), _ptr(out), a.numel(), stream_handle())
 
 
-def colsum(x, out):
-    M, N = x.shape[0], x.shape[-1]
-    M = x.numel() // N
-    _C().colsum(_ptr(x), int(x.dtype == torch.float32), M, N, N, _ptr(out), stream_handle())
+def colsum_workspace_elems(M: int, N: int) -> int:
+    """fp32 workspace floats colsum needs for an [M][N] input (0: one pass, no workspace)."""
+    sp = _C().colsum_splits(M, N)
+    return sp * N if sp > 1 else 0
 
 
-def softmax_xent(logits, labels, K, scale, dlogits, tail, ctrl=None):
+def colsum(x, out, workspace=None, M=None, N=None, ld=None):
+    """out[n] += sum over rows of x (bf16 or fp32) in a fixed order (no float atomics)."""
+    N = N or x.shape[-1]
+    ld = ld or N
+    M = M or x.numel() // ld
+    need = colsum_workspace_elems(M, N)
+    if need and (workspace is None or workspace.numel() < need):
+        workspace = torch.empty(need, dtype=torch.float32, device=x.device)  # (eager callers only)
+    _C().colsum(_ptr(x), int(x.dtype == torch.float32), M, N, ld, _ptr(out), stream_handle(),
+                _ptr(workspace) if need else 0)
+
+
+def xent_rows(B: int, device) -> torch.Tensor:
+    """softmax_xent's per-row scratch: 3 B floats + the arrival counter (zeroed once)."""
+    return torch.zeros(3 * B + 1, dtype=torch.float32, device=device)
+
+
+def softmax_xent(logits, labels, K, scale, dlogits, tail, ctrl=None, rows=None):
     """ctrl (the engine's device control block) makes the scale 1 / real rows of the global
-    batch; labels < 0 mark padding rows of a short final batch."""
+    batch; labels < 0 mark padding rows of a short final batch.  The loss / correct / count
+    sums are formed in a fixed row order (``rows``: :func:`xent_rows` scratch)."""
     B, ld = logits.shape
+    if rows is None:
+        rows = xent_rows(B, logits.device)  # (eager callers only: engines pass their own)
     _C().softmax_xent(_ptr(logits), ld, _ptr(labels), B, K, float(scale), _ptr(ctrl), _ptr(dlogits), _ptr(tail),
-                      stream_handle())
+                      _ptr(rows), stream_handle())
 
 
 def sgd_flat(P, G, V, Pb, lr, momentum=0.0, nesterov=False):

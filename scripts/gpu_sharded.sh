@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round-4 check of the sharded multi-rank MNIST step + determinism work: the peer / sharded
+# exchange tests (ranks sharing one GPU), the N=2 rehearsal bench sharded vs the standalone
+# peer kernel, the fused-engine and native-graph GPU tests, the driver's 1-GPU bench.
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_peer_allreduce_gpu.py -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/peer.log 2>&1
+rc=$?; echo "peer rc=$rc"; grep -E "PASS|FAIL|ERROR|passed|failed" gpurun_out/peer.log | tail -12
+if [ $rc -ne 0 ]; then tail -50 gpurun_out/peer.log; exit $rc; fi
+timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 200 --warmup 20 > gpurun_out/share2.log 2>&1
+rc=$?; echo "share2 rc=$rc"; tail -2 gpurun_out/share2.log; [ $rc -ne 0 ] && exit $rc
+DAMD_ALLREDUCE=xgmi timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 2 --steps 200 --warmup 20 > gpurun_out/share2x.log 2>&1
+rc=$?; echo "share2x rc=$rc"; tail -1 gpurun_out/share2x.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/b1.log 2>&1
+rc=$?; echo "b1 rc=$rc"; tail -1 gpurun_out/b1.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 700 python -u -m pytest tests/test_fused_convnet_gpu.py tests/test_native_infer_gpu.py tests/test_hip_ops_gpu.py tests/test_native_graph_gpu.py tests/test_native_layers_gpu.py -q -m gpu -p no:cacheprovider --timeout 150 --timeout-method thread > gpurun_out/gpu_rest.log 2>&1
+rc=$?; echo "rest rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/gpu_rest.log | tail -15
+exit $rc

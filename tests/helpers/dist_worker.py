@@ -49,6 +49,7 @@ def main():
         eng = getattr(model, "_engine", None)
         json.dump({"history": h.history, "world": num_workers, "rank": rank,
                    "engine": getattr(eng, "name", None),
+                   "exchange": getattr(eng, "allreduce_kind", None),
                    "iterations": int(model.optimizer.iterations)}, f)
     if rank == 0:
         np.savez(os.path.join(out, "init0.npz"), *init)

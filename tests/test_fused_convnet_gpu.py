@@ -344,7 +344,7 @@ def test_final_graph_equals_run_then_flush(monkeypatch):
     assert res[0][1]["loss"] == res[1][1]["loss"] and res[0][1]["accuracy"] == res[1][1]["accuracy"]
 
 
-@pytest.mark.parametrize("where", ["w1", "conv"])
+@pytest.mark.parametrize("where", ["w1", "conv", "b1"])
 def test_nonfinite_weight_reports_nan_loss(where, monkeypatch):
     """the fixed-point cross-block sums cannot carry NaN / inf, so a non-finite
     value raises the sticky ctrl.bad flag and the loss reads NaN (as the fp32 engines show
@@ -357,8 +357,10 @@ def test_nonfinite_weight_reports_nan_loss(where, monkeypatch):
     ws = m.get_weights()
     if where == "w1":
         ws[2][7, 3] = np.nan
+    elif where == "conv":
+        ws[0][1, 1, 0, 5] = np.inf  # the conv's ReLU (fmaxf) alone would map the NaN products to 0
     else:
-        ws[0][1, 1, 0, 5] = np.inf
+        ws[3][5] = np.nan           # as would the head's ReLU for a NaN b1
     m.set_weights(ws)
     h = m.fit(x, y, batch_size=64, epochs=2, steps_per_epoch=2, verbose=0,
               callbacks=[tf.keras.callbacks.TerminateOnNaN()])

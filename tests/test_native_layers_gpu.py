@@ -146,23 +146,24 @@ def test_native_optimizers_track_reference(name):
     # above.  epsilon 1e-2, not 1e-7: with a tiny epsilon Adam / RMSprop move every weight
     # by ~lr * sign(g), so weights whose gradient is ~0 follow the sign of the bf16 vs fp32
     # rounding noise (measured cos 0.885 at 1e-7, 0.926 at 1e-3 after 10 steps)
-    opt = _opt_cases(eps=1e-2)[name]
+    # the bounds must hold for any initial draw: three unpinned inits in one process
     x, y = _data(640, (28, 28, 1), 10, seed=3)
-    tf.keras.backend.clear_session()
-    tf.set_seed(11)  # a fixed init: the tolerances below are for one draw, not for every draw
-    init = _mnist().get_weights()
-    wn, hn, en, on = _train(_mnist, x, y, init, 64, 10, native=True, optimizer=opt)
-    wr, hr, er, orf = _train(_mnist, x, y, init, 64, 10, native=False, device="cpu", optimizer=opt)
-    assert en == "native_graph" and er == "generic"
-    assert on.iterations == orf.iterations == 10
-    np.testing.assert_allclose(hn["loss"], hr["loss"], rtol=2e-2)
-    cos_min, rel_max = 0.93, 0.4
-    _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=cos_min, rel_max=rel_max)
-    # the slots come back to the Keras optimizer in its dense (unpadded) layout
-    for s in orf.slot_names():
-        a, b = on.slots[s].cpu().double(), orf.slots[s].cpu().double()
-        assert a.shape == b.shape
-        assert float(a @ b / (a.norm() * b.norm() + 1e-30)) > 0.9, s
+    for rep in range(3):
+        opt = _opt_cases(eps=1e-2)[name]
+        tf.keras.backend.clear_session()
+        init = _mnist().get_weights()
+        wn, hn, en, on = _train(_mnist, x, y, init, 64, 10, native=True, optimizer=opt)
+        wr, hr, er, orf = _train(_mnist, x, y, init, 64, 10, native=False, device="cpu", optimizer=opt)
+        assert en == "native_graph" and er == "generic"
+        assert on.iterations == orf.iterations == 10
+        np.testing.assert_allclose(hn["loss"], hr["loss"], rtol=2e-2)
+        cos_min, rel_max = 0.9, 0.45
+        _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=cos_min, rel_max=rel_max)
+        # the slots come back to the Keras optimizer in its dense (unpadded) layout
+        for s in orf.slot_names():
+            a, b = on.slots[s].cpu().double(), orf.slots[s].cpu().double()
+            assert a.shape == b.shape
+            assert float(a @ b / (a.norm() * b.norm() + 1e-30)) > 0.85, s
 
 
 def _act_pool_model():
@@ -211,12 +212,11 @@ def test_native_dropout_trains_and_rate0_is_identity():
     w0, h0, e0 = _train(lambda: _dropout_model(0.0), x, y, init, 64, 5, native=True, lr=0.05)
     w1, h1, e1 = _train(_mnist, x, y, init, 64, 5, native=True, lr=0.05)
     assert e0 == e1 == "native_graph"
-    # (the conv bias colsum adds fp32 partials atomically in arrival order: after 5 SGD
-    # steps at lr 0.05 that is usually <= ~2e-8 absolute on weights of ~1e-2, but an
-    # order-dependent last bit that flips a bf16 activation rounding has been seen as
-    # 2.1e-7 on 3 of 346,112 elements)
+    # identical plans, and every reduction of the native step is in a fixed order (the
+    # bias column sums and the loss / metric sums included): bitwise the same run
     for a, b in zip(w0, w1):
-        np.testing.assert_allclose(a, b, rtol=1e-5, atol=1e-6)
+        np.testing.assert_array_equal(a, b)
+    assert h0["loss"] == h1["loss"]
     # rate 0.4: trains (loss falls over two epochs' worth of steps), differs from rate 0
     w2, h2, e2 = _train(lambda: _dropout_model(0.4), x, y, init, 64, 10, native=True, lr=0.05, momentum=0.9)
     assert e2 == "native_graph"
