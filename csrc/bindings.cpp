@@ -50,6 +50,8 @@ class ConvNetTrainer : public StepExecutor {
     b_.hacc = P_<long long>(g("hacc"));
     b_.hconv = P_<long long>(g("hconv"));
     b_.calt = P_<float>(g("calt"));
+    b_.ppb = bufs.contains("ppb") ? (int)g("ppb") : PP;
+    if (b_.ppb < 1 || b_.ppb > 4) throw std::invalid_argument("bwd positions per slice must be in [1,4]");
     HIP_CHECK(convnet2_set_lds_limits());
   }
   // Phase timing: k eager steps of the 2-launch step with HIP events
@@ -115,7 +117,7 @@ class ConvNetTrainer : public StepExecutor {
   // hred: [2][320] int64 (the conv-gradient sums convnet2_launch_gather writes for flush)
   void set_sharded(PeerAllreduce* p, uintptr_t hred, int gbf16) {
     if (!p || p->world() < 2 || p->world() > kXMaxRanks) throw std::invalid_argument("sharded step: 2..8 ranks");
-    const int NU = 4 * convnet_num_slices(PP_);
+    const int NU = 4 * convnet_num_slices(b_.ppb);
     if (p->capacity() < convnet_xin_floats(p->world(), NU) || p->capacity() < convnet_xout_floats(NU))
       throw std::invalid_argument("sharded step: peer staging too small");
     const PeerArgs& a = p->args();
@@ -130,6 +132,7 @@ class ConvNetTrainer : public StepExecutor {
     x.world = p->world();
     x.rank = p->rank();
     x.gbf16 = gbf16;
+    x.ppb = b_.ppb;
     xa_ = x;
     set_peer(p);
     sharded_ = true;
@@ -169,6 +172,7 @@ class ConvNetTrainer : public StepExecutor {
   bool run_final(int k) { return StepExecutor::run_final(k); }
   bool warm_final(int k) { return StepExecutor::warm_final(k); }
   int num_slices() const { return convnet_num_slices(PP_); }
+  int num_slices_bwd() const { return convnet_num_slices(b_.ppb); }
   int batch() const { return B_; }
 
  protected:
@@ -271,6 +275,14 @@ PYBIND11_MODULE(_C, m) {
       .def("set_timeout", &PeerAllreduce::set_timeout)
       .def_property_readonly("ready", &PeerAllreduce::ready)
       .def_property_readonly("capacity", &PeerAllreduce::capacity)
+      // diagnostics: n 32-bit words of this rank's `out` staging from word `off` (synchronizes)
+      .def("peek_out",
+           [](PeerAllreduce& p, long off, long n) {
+             std::vector<uint32_t> v((size_t)n);
+             HIP_CHECK(hipDeviceSynchronize());
+             HIP_CHECK(hipMemcpy(v.data(), p.out_local() + off, (size_t)n * 4, hipMemcpyDeviceToHost));
+             return v;
+           })
       .def_property_readonly("world", &PeerAllreduce::world)
       .def_property_readonly("rank", &PeerAllreduce::rank);
 
@@ -303,6 +315,7 @@ PYBIND11_MODULE(_C, m) {
       .def("invalidate_graphs", &ConvNetTrainer::invalidate_graphs)
       .def_property_readonly("num_graphs", &ConvNetTrainer::num_graphs)
       .def_property_readonly("num_slices", &ConvNetTrainer::num_slices)
+      .def_property_readonly("num_slices_bwd", &ConvNetTrainer::num_slices_bwd)
       .def_property_readonly("batch", &ConvNetTrainer::batch)
       .def_property_readonly("stream", [](ConvNetTrainer& t) { return reinterpret_cast<uintptr_t>(t.stream()); });
 

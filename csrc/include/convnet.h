@@ -27,6 +27,7 @@ struct XArgs {
   unsigned long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
   int world, rank;          // world <= 1: not sharded
   int gbf16;                // DAMD_GRAD_DTYPE=bf16: partials and reduced units travel as bf16
+  int ppb;                  // pooled positions per bwd slice (units are 4 per bwd slice)
 };
 constexpr long kXG16 = kXFlags + 16384;  // out: bf16 reduced dW1 [5408][64] (DAMD_GRAD_DTYPE=bf16)
 // floats of `out` the exchange needs for nunits units (<= 909 units: the flag area)
@@ -57,6 +58,10 @@ struct ConvNetBuffers {
   // Then Gr = this rank's gradient staging and hconv_r = the conv-gradient sums that
   // convnet2_launch_gather fills for flush / the host
   const XArgs* xa;
+  // pooled positions per slice of the backward kernel (0: the forward's PP).  The forward
+  // runs 4 image groups per slice (a 228-block grid at PP 3); the backward has one block per
+  // slice, so a finer slicing spreads its dW1 / dP / conv-gradient work over more CUs
+  int ppb;
 };
 constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;

@@ -66,7 +66,9 @@ struct Ctrl {
   int   xcnt2;              // 22 xcnt as seen by the step's bwd (set by its fwd)
   int   ticket;             // 23 arrival ticket of the sharded bwd (its last block publishes the
                             //    rank's small-gradient message)
-  int   pad[8];
+  int   pend2;              // 24 `pending` as seen by the step's fwd (set by it): bwd folds the
+                            //    previous step's metric tail only when there was one
+  int   pad[7];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

@@ -100,8 +100,9 @@ hipError_t logits_store(const float* logits, int ld, int K, int B, const Ctrl* c
 hipError_t step_fold(Ctrl* ctrl, float* tail, hipStream_t s);
 // out = a + b (bf16)
 hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n, hipStream_t s);
-// fp32 -> bf16
+// fp32 -> bf16, bf16 -> fp32
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t s);
+hipError_t cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t s);
 // uint8 (k) -> bf16(k * scale)
 hipError_t cast_u8_bf16(const uint8_t* x, float scale, uint16_t* y, long n, hipStream_t s);
 // out[n] += sum_m x[m][n]  (x bf16 or fp32, [M][ld]) in a fixed order; when

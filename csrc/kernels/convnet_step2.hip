@@ -159,6 +159,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     ctrl->cur2 = c.cursor;
     ctrl->par2 = par;
     ctrl->xcnt2 = c.xcnt;
+    ctrl->pend2 = c.pending;
   }
   const bool pend = c.pending != 0;
   const long row_base = (long)c.cursor * c.global_batch + c.row0 + img0;
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   if (sh && pend) {
     const int ps = xe & 1;
     float* xo = xa.out[xa.rank];
-    if (tid < xa.world) x_wait(xa, x_sflag(xo, 4 * gridDim.x, ps, tid), xe, XW_SMALL);
+    if (tid < xa.world) x_wait(xa, x_sflag(xo, 4 * ((NPOS + xa.ppb - 1) / xa.ppb), ps, tid), xe, XW_SMALL);
     __syncthreads();
     long long q = 0;
     float g = 0.f;
@@ -323,7 +324,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     // sharded: the slice's reduced dW1 arrives as 4 units (2 halves each) from their owners,
     // pushed at the end of every owner's bwd -- waited for only now, after the conv
     if (pend) {
-      if (tid < 8) x_wait(xa, x_gflag(xa.out[xa.rank], 4 * gridDim.x, 4 * s + (tid >> 1), tid & 1), xe, XW_UNIT);
+      // units of the bwd slices covering this slice's rows, 2 halves each
+      const int sb0 = p0 / xa.ppb, nunits = 4 * ((p1 - 1) / xa.ppb - sb0 + 1), NUb = 4 * ((NPOS + xa.ppb - 1) / xa.ppb);
+      if (tid < 2 * nunits) x_wait(xa, x_gflag(xa.out[xa.rank], NUb, 4 * sb0 + (tid >> 1), tid & 1), xe, XW_UNIT);
       __syncthreads();
       if (xa.gbf16) {
         const uint2* R2 = reinterpret_cast<const uint2*>(xa.out[xa.rank] + kXG16) + p0 * 32 * HID / 4;
@@ -893,7 +896,10 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       const int m = ae - NSMALL;  // 0 loss, 1 correct, 2 count
       float* accp = m == 0 ? &ctrl->acc_loss : (m == 1 ? &ctrl->acc_correct : &ctrl->acc_count);
       const float old = m == 0 ? c.acc_loss : (m == 1 ? c.acc_correct : c.acc_count);
-      if (!sh) *accp = old + ag_old;  // fold the previous step's all-reduced metric into the epoch total
+      // fold the previous step's all-reduced metric into the epoch total -- if there is one
+      // not yet folded: none before the first step, none right after a flush (which folded
+      // it), and the staging may hold anything then (the peer self-test's values)
+      if (!sh) *accp = c.pend2 ? old + ag_old : old;
       // (a non-finite / out-of-range fixed-point input so far: the loss is NaN from now on)
       G[OFF_LOSS + m] = m == 0 && c.bad ? __builtin_nanf("") : m < 2 ? tot : (float)max(0, min(B, gcount - c.row0));
     }
@@ -915,7 +921,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 // =================================================================================
 // G / hconv: the reduced gradient (the peer all-reduce's `out` when it is folded into the
 // step, see ConvNetBuffers::Gr); hconv_w: the buffer bwd adds into (both parities cleared)
-__global__ __launch_bounds__(256) void flush(float* __restrict__ P, const float* __restrict__ G, float* __restrict__ V,
+__global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
                                              const float* __restrict__ W1alt, const float* __restrict__ V1alt,
                                              long long* __restrict__ hconv, const float* __restrict__ calt,
                                              long long* __restrict__ hacc, int B, int eager,
@@ -950,10 +956,14 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, const float*
     }
     else hacc[i - 2 * NCONV] = 0;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && pend) {  // (G is read only while an update is pending)
+  if (blockIdx.x == 0 && threadIdx.x == 0 && pend) {
     ctrl->acc_loss = c.acc_loss + G[OFF_LOSS];
     ctrl->acc_correct = c.acc_correct + G[OFF_CORR];
     ctrl->acc_count = c.acc_count + G[OFF_CNT];
+    // the metric tail is folded: the next bwd's fold of "the previous step's metric" (world 1
+    // / the standalone all-reduce) must add nothing (the gradient itself is never re-read:
+    // the next fwd applies no update)
+    G[OFF_LOSS] = G[OFF_CORR] = G[OFF_CNT] = 0.f;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1059,9 +1069,12 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
                      b.hconv_r ? b.hconv_r : b.hconv, xargs(b));
 }
 
+static int ppb_of(const ConvNetBuffers& b, int PP) { return b.ppb > 0 ? b.ppb : PP; }
+
 template <bool U8>
-static void launch2_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
+static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st) {
   using namespace convnet;
+  const int PP = ppb_of(b, PPf);
   const int NS = convnet_num_slices(PP);
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
@@ -1084,7 +1097,8 @@ hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream
 
 hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   if (!b.hacc || !b.hconv || !b.calt) return hipErrorInvalidValue;
-  if (convnet2_bwd_lds(PP) > 160 * 1024) return hipErrorInvalidValue;
+  if (convnet2_bwd_lds(ppb_of(b, PP)) > 160 * 1024) return hipErrorInvalidValue;
+  if (b.xa && b.xa->ppb != ppb_of(b, PP)) return hipErrorInvalidValue;
   if (b.x_u8) launch2_bwd<true>(b, B, PP, st);
   else launch2_bwd<false>(b, B, PP, st);
   return hipGetLastError();
@@ -1097,8 +1111,9 @@ hipError_t convnet2_launch_step(const ConvNetBuffers& b, int B, int PP, hipStrea
 
 hipError_t convnet2_launch_gather(const ConvNetBuffers& b, int PP, hipStream_t st) {
   if (!b.xa || b.xa->world < 2 || !b.hconv_r) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(convnet2::sh_gather, dim3(57), dim3(512), 0, st, b.ctrl, *b.xa, b.hconv_r, convnet_num_slices(PP),
-                     PP);
+  const int ppb = ppb_of(b, PP);
+  hipLaunchKernelGGL(convnet2::sh_gather, dim3(57), dim3(512), 0, st, b.ctrl, *b.xa, b.hconv_r, convnet_num_slices(ppb),
+                     ppb);
   return hipGetLastError();
 }
 

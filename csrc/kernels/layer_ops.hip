@@ -1227,6 +1227,10 @@ __global__ __launch_bounds__(NT) void cast_f32_bf16_k(const float* x, uint16_t* 
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) y[i] = f2bf(x[i]);
 }
 
+__global__ __launch_bounds__(NT) void cast_bf16_f32_k(const uint16_t* x, float* y, long n) {
+  for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT) y[i] = bf2f(x[i]);
+}
+
 __global__ __launch_bounds__(NT) void cast_u8_bf16_k(const uint8_t* x, float scale, uint16_t* y, long n) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < n; i += (long)gridDim.x * NT)
     y[i] = f2bf((float)x[i] * scale);
@@ -1886,6 +1890,11 @@ hipError_t add_bf16(const uint16_t* a, const uint16_t* b, uint16_t* out, long n,
 
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, long n, hipStream_t s) {
   hipLaunchKernelGGL(cast_f32_bf16_k, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t cast_bf16_f32(const uint16_t* x, float* y, long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_k, dim3(grid_for(n)), dim3(NT), 0, s, x, y, n);
   return hipGetLastError();
 }
 

@@ -255,6 +255,9 @@ void register_kernel_ops(py::module_& m) {
   m.def("add_bf16", [](U a, U b, U o, long n, U s) {
     check(damd::add_bf16(P_<const u16>(a), P_<const u16>(b), P_<u16>(o), n, P_<ihipStream_t>(s)), "add_bf16");
   });
+  m.def("cast_bf16_f32", [](U x, U y, long n, U s) {
+    check(damd::cast_bf16_f32(P_<const u16>(x), P_<float>(y), n, P_<ihipStream_t>(s)), "cast_bf16_f32");
+  });
   m.def("cast_f32_bf16", [](U x, U y, long n, U s) {
     check(damd::cast_f32_bf16(P_<const float>(x), P_<u16>(y), n, P_<ihipStream_t>(s)), "cast_f32_bf16");
   });

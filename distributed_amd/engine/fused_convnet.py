@@ -29,7 +29,7 @@ NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
 (C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
- C_FLUSHT, C_PEND, C_PAR2, C_BAD, C_XCNT, C_XCNT2, C_TICKET) = range(24)
+ C_FLUSHT, C_PEND, C_PAR2, C_BAD, C_XCNT, C_XCNT2, C_TICKET, C_PEND2) = range(25)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -91,6 +91,14 @@ class FusedConvNetEngine(Engine):
         self.PP = env.get_int("DAMD_PP", 3)
         if not 1 <= self.PP <= 4:
             raise ValueError("DAMD_PP must be in [1, 4]")
+        # the backward kernel's own slicing (one block per slice): finer slices spread its
+        # post-head work (dW1 / dP MFMAs, pool / ReLU backward, conv gradient) over more CUs.
+        # rocprofv3 bwd duration, B=64: 13.32 us (1 position, 169 blocks), 12.53 us (2, 85),
+        # 13.16 us (3, 57): more blocks also mean more same-address conv-gradient atomics
+        # and redundant heads, so 2 is the default
+        self.PPB = env.get_int("DAMD_PP_BWD", 2)
+        if not 1 <= self.PPB <= 4:
+            raise ValueError("DAMD_PP_BWD must be in [1, 4]")
         NS = C.convnet_num_slices(self.PP)
         f32 = dict(dtype=torch.float32, device=dev)
         BP = (B + 63) // 64 * 64  # padded batch pitch of the feature-major buffers
@@ -130,7 +138,8 @@ class FusedConvNetEngine(Engine):
                     ctrl=self.ctrl.data_ptr(),
                     pooled=self.pooled.data_ptr(), code=self.code.data_ptr(), w1alt=self.w1alt.data_ptr(),
                     v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr(),
-                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr())
+                    hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr(),
+                    ppb=self.PPB)
         # world 1 (no gradient all-reduce): bwd applies the W1 update itself as soon as it
         # has the slice's gradient, and fwd reads only the bf16 copy (DAMD_EAGER_W1=0: the
         # deferred update in fwd, as with an all-reduce between the launches)
@@ -155,20 +164,21 @@ class FusedConvNetEngine(Engine):
         #       owners over xGMI, owners reduce in rank order and push the reduced units back;
         #       the small gradients + metrics travel as one message per rank.  No extra launch.
         #   xgmi -- the standalone two-shot peer all-reduce kernel after bwd (folded staging)
-        #   rccl -- RCCL inside the captured step
+        #   rccl -- RCCL inside the captured step; off -- no device transport (RCCL if the
+        #       communicator has one, else the host-staged gloo all-reduce between steps)
         # Both peer modes need every rank to map every peer (one node); else RCCL.
         self.peer = None
         self.sharded = False
         self.hred = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)  # sharded: conv sums for flush
         mode = env.get_str("DAMD_ALLREDUCE", "auto").lower()
-        if mode not in ("auto", "sharded", "xgmi", "rccl"):
-            raise ValueError("DAMD_ALLREDUCE must be auto, sharded, xgmi or rccl")
+        if mode not in ("auto", "sharded", "xgmi", "rccl", "off"):
+            raise ValueError("DAMD_ALLREDUCE must be auto, sharded, xgmi, rccl or off")
         # DAMD_GRAD_DTYPE=bf16: the exchanged dW1 travels as bf16 (fp32 accumulation by the
         # owner, fp32 master update); default fp32 (reference parity)
         self.grad_dtype = env.get_str("DAMD_GRAD_DTYPE", "fp32").lower()
         if self.grad_dtype not in ("fp32", "bf16"):
             raise ValueError("DAMD_GRAD_DTYPE must be fp32 or bf16")
-        if self.world > 1 and mode != "rccl":
+        if self.world > 1 and mode not in ("rccl", "off"):
             from ..parallel.communicator import make_peer_allreduce
 
             # in-kernel wait deadline: the collective watchdog's when one is set, so a missing
@@ -176,7 +186,7 @@ class FusedConvNetEngine(Engine):
             wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
             want_sharded = mode in ("auto", "sharded") and self.world <= 8
             if want_sharded:
-                NU = 4 * NS
+                NU = 4 * C.convnet_num_slices(self.PPB)
                 cap = max(self.world * NU * 2048, 347648 + 2 * 8 * 1408 + 16384 + FEAT * HID // 2)
             else:
                 cap = C.PeerAllreduce.message_words(C.convnet_grad_count(self.PP), 2 * NCONV)
@@ -193,7 +203,11 @@ class FusedConvNetEngine(Engine):
                 # not hold the CUs another rank needs to publish what they wait for
                 ndev = max(1, torch.cuda.device_count())
                 share = [q for q in range(self.world) if q % ndev == (dev.index or 0)]
-                if len(share) > 1:
+                # (two ranks need no split: one rank's waiting forward leaves the other's
+                # 57-169-block backward enough CUs to finish -- measured 44.7 us/step shared
+                # vs 78 us with halved CUs; from three ranks on, the waiting forwards of two
+                # ranks can hold every CU)
+                if len(share) > 2 and env.get_bool("DAMD_SHARED_CU_SPLIT", True):
                     self.trainer.restrict_cus(share.index(self.rank), len(share))
                 # every rank's flags are zero before any rank's first step writes into them
                 strategy.communicator.barrier()

@@ -259,17 +259,44 @@ class NativeGraphEngine(Engine):
         self._write_hparams()
         force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)  # exercise the RCCL path at world 1
         self.native_comm = strategy.communicator.native if (self.world > 1 or force) else None
-        self.host_collective = self.world > 1 and self.native_comm is None
-        self.allreduce_kind = ("none" if self.native_comm is None and self.world == 1 else
-                               "rccl-bucketed" if self.native_comm is not None else "host-gloo")
-        self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
+        self.peer = None  # native xGMI peer all-reduce as the bucket transport (set below)
+        # DAMD_GRAD_DTYPE=bf16: the RCCL buckets carry bf16 gradients (half the ring traffic;
+        # the metric tail stays fp32, the master update fp32); default fp32 (reference parity)
+        self.grad_bf16 = env.get_str("DAMD_GRAD_DTYPE", "fp32").lower() == "bf16"
         self.graph = None
         self._phase_events = None  # phase_times(): (name, event) marks of an eager step
         self.feed = None
         self._plan()
         self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0))
+        # bucket transport at world > 1 (DAMD_ALLREDUCE): RCCL (auto, when the RCCL
+        # communicator exists), or the native xGMI peer all-reduce over IPC-mapped staging
+        # (xgmi; auto without RCCL, e.g. ranks sharing one GPU in a rehearsal) -- both on the
+        # side stream, overlapped with the rest of backward, inside the captured step
+        mode = env.get_str("DAMD_ALLREDUCE", "auto").lower()
+        if self.world > 1 and (mode == "xgmi" or (mode == "auto" and self.native_comm is None)):
+            from ..parallel.communicator import make_peer_allreduce
+
+            cap = max(b["hi"] - b["lo"] for b in self._buckets)
+            wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
+            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, cap,
+                                            blocks=env.get_int("DAMD_PEER_BLOCKS", 64), timeout_s=wd if wd > 0 else 60.0)
+            if self.peer is None and mode == "xgmi":
+                raise RuntimeError("DAMD_ALLREDUCE=xgmi but the xGMI peer mapping is unavailable")
+        if self.peer is not None and self.grad_bf16:
+            dlog.warning("DAMD_GRAD_DTYPE=bf16 applies to the RCCL buckets; the peer transport reduces fp32")
+            self.grad_bf16 = False
+        self.host_collective = self.world > 1 and self.native_comm is None and self.peer is None
+        self.allreduce_kind = ("none" if self.native_comm is None and self.peer is None else
+                               "xgmi-peer-bucketed" if self.peer is not None else
+                               "rccl-bucketed-bf16" if self.grad_bf16 else "rccl-bucketed")
+        if self.host_collective:
+            self.allreduce_kind = "host-gloo"
+        self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
+        self.g16 = (torch.zeros(self.nparam, dtype=torch.bfloat16, device=dev)
+                    if self.grad_bf16 and self.native_comm is not None else None)
         # created up front: no stream creation while a graph is being captured
-        self._comm_stream = torch.cuda.Stream(dev) if self.native_comm is not None else None
+        self._comm_stream = (torch.cuda.Stream(dev) if (self.native_comm is not None or self.peer is not None)
+                             else None)
         opt._iter_source = self._iterations
         torch.cuda.synchronize(dev)
         dlog.info("native graph engine: %d nodes, %d params, %.1f MB planned activations", len(self.nodes), n,
@@ -634,8 +661,25 @@ class NativeGraphEngine(Engine):
             b["left"] = set(b["vars"])
             b["sent"] = False
 
+    def _reduce_bucket(self, b, st: int):
+        """SUM all-reduce of G[lo:hi] on stream ``st`` by the configured transport."""
+        lo, hi = b["lo"], b["hi"]
+        gp = self.G.data_ptr()
+        if self.peer is not None:
+            self.peer.allreduce(gp + 4 * lo, hi - lo, st)
+        elif self.g16 is not None:
+            n = min(hi, self.nparam) - lo  # the parameter part travels as bf16 ...
+            g16 = self.g16.data_ptr() + 2 * lo
+            self.C.cast_f32_bf16(gp + 4 * lo, g16, n, st)
+            self.native_comm.allreduce(g16, g16, n, 1, 0, st)
+            self.C.cast_bf16_f32(g16, gp + 4 * lo, n, st)
+            if hi > self.nparam:  # ... the metric tail (counts, sums) as fp32
+                self.native_comm.allreduce(gp + 4 * self.nparam, gp + 4 * self.nparam, hi - self.nparam, 0, 0, st)
+        else:
+            self.native_comm.allreduce(gp + 4 * lo, gp + 4 * lo, hi - lo, 0, 0, st)
+
     def _bucket_progress(self, nd, final=False):
-        if self.native_comm is None:
+        if self.native_comm is None and self.peer is None:
             return
         done = set(self._writes.get(id(nd), ())) if nd is not None else set()
         main = torch.cuda.current_stream(self.device)
@@ -647,8 +691,7 @@ class NativeGraphEngine(Engine):
                 continue
             cs = self._comm_stream
             cs.wait_stream(main)
-            self.native_comm.allreduce(self.G.data_ptr() + 4 * b["lo"], self.G.data_ptr() + 4 * b["lo"],
-                                       b["hi"] - b["lo"], 0, 0, cs.cuda_stream)
+            self._reduce_bucket(b, cs.cuda_stream)
             b["sent"] = True
         if final:
             main.wait_stream(self._comm_stream)
@@ -1253,8 +1296,13 @@ class NativeGraphEngine(Engine):
         torch.cuda.synchronize(self.device)
         self.graph = g
 
+    def _check_peer(self):
+        if self.peer is not None and self.peer.status():
+            raise RuntimeError("xGMI peer all-reduce: a wait for a peer timed out (peer missing or wedged)")
+
     def metrics(self):
         torch.cuda.synchronize(self.device)
+        self._check_peer()
         c = self.ctrl.cpu().tolist()
         loss, corr, cnt = _i2f(c[C_AL]), _i2f(c[C_AC]), _i2f(c[C_AN])
         d = max(cnt, 1.0)
@@ -1280,6 +1328,7 @@ class NativeGraphEngine(Engine):
 
     def sync(self):
         torch.cuda.synchronize(self.device)
+        self._check_peer()  # never hand out weights built from a timed-out (partial) reduction
 
     def after_external_write(self):
         # the forward/backward GEMMs read the bf16 shadow Pb: re-derive it from the

@@ -33,7 +33,7 @@ def main():
     eng.sync()
     st = eng.stamps.cpu().numpy()
     NS = eng.trainer.num_slices
-    grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, NS)}
+    grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, eng.trainer.num_slices_bwd)}
     names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued"],
              "bwd": ["start", "loads staged", "head done", "mfma", "convgrad", "end", "h", "softmax", "dh"]}
     t0 = None

@@ -25,20 +25,32 @@ def main():
     batch_size = per * num_workers
     # different seed per worker: the initial-value broadcast must make replicas equal
     tf.set_seed(100 + rank)
-    mnist = tf.keras.datasets.mnist
-    (x_train, y_train), _ = mnist.load_data()
-    x_train = x_train[:rows].reshape(rows, 28, 28, 1) / 255.0
-    y_train = y_train[:rows]
-    with strategy.scope():
-        model = tf.keras.Sequential([
-            tf.keras.layers.Conv2D(32, 3, activation='relu', input_shape=(28, 28, 1)),
-            tf.keras.layers.MaxPooling2D(),
-            tf.keras.layers.Flatten(),
-            tf.keras.layers.Dense(64, activation='relu'),
-            tf.keras.layers.Dense(10)
-        ])
-        model.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
-                      optimizer=tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9), metrics=['accuracy'])
+    if os.environ.get("DAMD_TEST_MODEL") == "resnet_small":
+        # a small residual net (BN, projection shortcuts): the native graph engine's plan
+        # with several gradient buckets (DAMD_BUCKET_MB) reduced while backward runs
+        rng = np.random.default_rng(5)
+        x_train = (rng.integers(0, 256, size=(rows, 32, 32, 3)) / 255.0).astype(np.float32)
+        y_train = rng.integers(0, 10, size=rows).astype(np.int64)
+        with strategy.scope():
+            model = tf.models.resnet18(classes=10, input_shape=(32, 32, 3), widths=(16, 32, 32, 64),
+                                       blocks=(1, 1, 1, 1))
+            model.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                          optimizer=tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9), metrics=['accuracy'])
+    else:
+        mnist = tf.keras.datasets.mnist
+        (x_train, y_train), _ = mnist.load_data()
+        x_train = x_train[:rows].reshape(rows, 28, 28, 1) / 255.0
+        y_train = y_train[:rows]
+        with strategy.scope():
+            model = tf.keras.Sequential([
+                tf.keras.layers.Conv2D(32, 3, activation='relu', input_shape=(28, 28, 1)),
+                tf.keras.layers.MaxPooling2D(),
+                tf.keras.layers.Flatten(),
+                tf.keras.layers.Dense(64, activation='relu'),
+                tf.keras.layers.Dense(10)
+            ])
+            model.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                          optimizer=tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9), metrics=['accuracy'])
     init = [w.copy() for w in model.get_weights()]
     if os.environ.get("DAMD_TEST_INIT_FROM"):
         init = [a for a in np.load(os.environ["DAMD_TEST_INIT_FROM"]).values()]
