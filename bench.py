@@ -248,6 +248,9 @@ def main():
             "final_epoch_loss": round(m.get("loss", float("nan")), 4),
             # how the per-step gradient all-reduce ran, and how many ranks RCCL itself counts
             "allreduce": getattr(engine, "allreduce_kind", "none"),
+            # dtype of the exchanged gradient (DAMD_GRAD_DTYPE; fp32 = reference parity)
+            "grad_dtype": ("bf16" if (getattr(engine, "grad_dtype", "fp32") == "bf16"
+                                      or getattr(engine, "grad_bf16", False)) and n > 1 else "fp32"),
             "rccl_ranks": _rccl_ranks(comm),
         }
         if phases is not None:

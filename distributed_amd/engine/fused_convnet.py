@@ -211,6 +211,10 @@ class FusedConvNetEngine(Engine):
                     self.trainer.restrict_cus(share.index(self.rank), len(share))
                 # every rank's flags are zero before any rank's first step writes into them
                 strategy.communicator.barrier()
+        if self.grad_dtype == "bf16" and not self.sharded:
+            if self.world > 1:
+                dlog.warning("DAMD_GRAD_DTYPE=bf16 applies to the sharded exchange only; exchanging fp32")
+            self.grad_dtype = "fp32"
         # host-collective mode (DAMD_COMM=gloo, e.g. several ranks on one GPU): one step at a
         # time, the gradient/metric buffer all-reduced through the host between steps
         self.host_collective = self.world > 1 and native is None and self.peer is None
