@@ -56,6 +56,23 @@ class Engine:
     def sync(self):
         pass
 
+    def completion_event(self):
+        """An event that completes when the work enqueued so far has finished on the device
+        (the watchdog beats on it), or None on the CPU: the host loop itself is the work."""
+        if getattr(self.device, "type", "cpu") != "cuda":
+            return None
+        import torch
+
+        ev = torch.cuda.Event()
+        ev.record(self._work_stream())
+        return ev
+
+    def _work_stream(self):
+        """The stream the engine's step work is enqueued on."""
+        import torch
+
+        return torch.cuda.current_stream(self.device)
+
     def phase_times(self, n_steps: int) -> dict:
         """Mean milliseconds per step of the step's phases (forward / backward / all-reduce /
         optimizer) over ``n_steps`` real training steps run eagerly with timing points between

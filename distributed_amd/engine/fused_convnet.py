@@ -181,9 +181,11 @@ class FusedConvNetEngine(Engine):
         if self.world > 1 and mode not in ("rccl", "off"):
             from ..parallel.communicator import make_peer_allreduce
 
-            # in-kernel wait deadline: the collective watchdog's when one is set, so a missing
-            # peer costs at most that much GPU spinning per wait
-            wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
+            # in-kernel wait deadline: the collective watchdog's (its default included), so a
+            # missing peer is reported by the kernel's status word no later than the watchdog
+            from ..utils.watchdog import deadline_for
+
+            wd = deadline_for(self.world)
             want_sharded = mode in ("auto", "sharded") and self.world <= 8
             if want_sharded:
                 NU = 4 * C.convnet_num_slices(self.PPB)
@@ -445,6 +447,12 @@ class FusedConvNetEngine(Engine):
     def after_external_write(self):
         self._refresh_w1bf()
         self._ctrl_write({C_BAD: 0})  # new weights: a past overflow no longer applies
+
+    def _work_stream(self):
+        # the step kernels run on the trainer's own HIP stream
+        if getattr(self, "_ext_stream", None) is None:
+            self._ext_stream = torch.cuda.ExternalStream(self.trainer.stream, device=self.device)
+        return self._ext_stream
 
     def sync(self):
         # host readers (get_weights, checkpoints, callbacks) see the trained values: the

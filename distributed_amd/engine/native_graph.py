@@ -277,7 +277,9 @@ class NativeGraphEngine(Engine):
             from ..parallel.communicator import make_peer_allreduce
 
             cap = max(b["hi"] - b["lo"] for b in self._buckets)
-            wd = env.get_float("DAMD_WATCHDOG_S", 0.0)
+            from ..utils.watchdog import deadline_for
+
+            wd = deadline_for(self.world)  # in-kernel wait deadline = the watchdog's
             self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, cap,
                                             blocks=env.get_int("DAMD_PEER_BLOCKS", 64), timeout_s=wd if wd > 0 else 60.0)
             if self.peer is None and mode == "xgmi":

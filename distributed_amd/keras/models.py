@@ -278,9 +278,13 @@ class Model(L.Layer):
                     done += k
                     global_step += k
                     if watchdog is not None:
-                        # the host loop is alive; a hang inside a collective or a device wait
-                        # stops these beats (the next host sync blocks)
-                        watchdog.beat(f"epoch {epoch + 1} step {done}")
+                        # beat when the chunk's DEVICE work completes (an event behind it),
+                        # not when the host has merely enqueued it
+                        ev = engine.completion_event()
+                        if ev is None:
+                            watchdog.beat(f"epoch {epoch + 1} step {done}")
+                        else:
+                            watchdog.beat_when_done(ev, f"epoch {epoch + 1} step {done}")
                     if per_hook or (verbose == 1 and time.time() - last_ui > refresh_s):
                         logs = self._public(engine.metrics())
                         logs["seen"] = min(done * batch_size, n) if steps_per_epoch is None else done * batch_size

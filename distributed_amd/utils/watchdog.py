@@ -4,10 +4,12 @@ Reference behaviour: "ModelCheckpoint callback is not provided. Workers will nee
 restart training if any fails" (README.md:400) -- TF has no way out of a collective whose
 peer died.  Here (SURVEY.md §5 failure detection):
 
-* ``fit`` arms the watchdog for the whole training loop and beats it after every
-  completed chunk of steps (each chunk ends at a host sync point, so a beat means the
-  device work -- kernels, RCCL / xGMI all-reduces -- and the host collectives of that chunk
-  finished);
+* ``fit`` arms the watchdog for the whole training loop; after enqueuing each chunk of
+  steps it hands the watchdog a device event recorded behind that chunk
+  (:meth:`Watchdog.beat_when_done`), and the watchdog thread beats when the event
+  COMPLETES -- so a beat means the chunk's device work (kernels, RCCL / xGMI exchanges)
+  finished, not merely that the host enqueued it, and a wedged collective is detected one
+  deadline after the last completed chunk;
 * a daemon thread checks the age of the last beat; past the deadline it logs which phase
   was stuck, aborts the registered communicators (``ncclCommAbort`` wakes a device-side
   RCCL wait, the peer kernel's bounded waits expire on their own) and ends the process with
@@ -44,6 +46,8 @@ class Watchdog:
         self._armed = False
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
+        self._pending: List[tuple] = []  # (event, phase) in enqueue order
+        self._lock = threading.Lock()
         self.fired = False
 
     # --- control ---------------------------------------------------------------------
@@ -64,6 +68,26 @@ class Watchdog:
         self._last = time.monotonic()
         if phase is not None:
             self._phase = phase
+
+    def beat_when_done(self, event, phase: str) -> None:
+        """Beat when ``event`` (anything with ``query() -> bool``, e.g. a torch.cuda.Event
+        recorded behind a chunk of device work) completes; events complete in order."""
+        with self._lock:
+            self._pending.append((event, phase))
+
+    def _poll_events(self) -> None:
+        with self._lock:
+            while self._pending:
+                ev, phase = self._pending[0]
+                try:
+                    done = bool(ev.query())
+                except Exception:  # pragma: no cover - a destroyed / failed event counts as done
+                    done = True
+                if not done:
+                    break
+                self._pending.pop(0)
+                self._last = time.monotonic()
+                self._phase = phase
 
     def disarm(self) -> None:
         self._armed = False
@@ -87,6 +111,7 @@ class Watchdog:
         while not self._stop.wait(self.poll_s):
             if not self._armed:
                 continue
+            self._poll_events()
             age = time.monotonic() - self._last
             if age > self.deadline_s:
                 self._expire(age)

@@ -347,6 +347,40 @@ def test_watchdog_unit():
     wd.close()
 
 
+def test_watchdog_beats_on_device_completion_not_enqueue():
+    """A chunk whose device work never completes (a wedged collective: its event never
+    signals) stops the beats even though the host enqueued it; the watchdog fires one
+    deadline after the last COMPLETED chunk and names it."""
+    import time as _t
+
+    from distributed_amd.utils.watchdog import Watchdog
+
+    class Ev:  # stand-in for torch.cuda.Event: query() is True once the work finished
+        def __init__(self, done):
+            self.done = done
+
+        def query(self):
+            return self.done
+
+    fired = []
+    wd = Watchdog(0.5, on_expire=fired.append, poll_s=0.05)
+    wd.arm("start")
+    late = Ev(False)
+    wd.beat_when_done(Ev(True), "chunk 1")
+    wd.beat_when_done(late, "chunk 2")
+    _t.sleep(0.3)
+    late.done = True  # chunk 2 completes late but within the deadline: a beat
+    _t.sleep(0.3)
+    assert not fired and wd._phase == "chunk 2"
+    t0 = _t.monotonic()
+    wd.beat_when_done(Ev(False), "chunk 3")  # enqueued, never completes
+    while not fired and _t.monotonic() - t0 < 5:
+        _t.sleep(0.02)
+    assert fired and "'chunk 2'" in fired[0], fired
+    assert _t.monotonic() - t0 < 0.5 + 0.3  # deadline (from chunk 2's completion) + a poll
+    wd.close()
+
+
 @pytest.mark.timeout(200)
 def test_step_phases_include_the_allreduce_share(tmp_path):
     """bench.py --phases on 2 gloo ranks: forward / backward / all-reduce / optimizer times
