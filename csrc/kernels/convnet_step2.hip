@@ -591,7 +591,16 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     load_indep(chunk);
     load_dep(chunk);
   };
-  auto store_chunk = [&](int chunk) __attribute__((always_inline)) {
+  // what the head needs (b1 / W2 / b2, labels) and what only the MFMAs / conv gradient
+  // need (pooled tile, argmax codes, input rows): the single-chunk backward stores the
+  // latter while waves 0-3 run the logits / softmax, so the head does not wait for the
+  // input rows (the largest, last-issued loads)
+  auto store_head = [&]() __attribute__((always_inline)) {
+    spl[tid] = spv0;
+    if (tid + 512 < NSMALL) spl[tid + 512] = spv1;
+    if (tid < CH) ylds[tid] = yval ? ylab : -1;
+  };
+  auto store_body = [&]() __attribute__((always_inline)) {
     if (tid < K * 8) *reinterpret_cast<uint4*>(pt + (tid >> 3) * HP + (tid & 7) * 8) = pv0;
     if (tid + 512 < K * 8) *reinterpret_cast<uint4*>(pt + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = pv1;
     if (tid < CH * kc) {
@@ -599,14 +608,15 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cok ? cv : make_uint4(0u, 0u, 0u, 0u);
     }
     x_store<U8>(xst, xs, lut);
-    spl[tid] = spv0;
-    if (tid + 512 < NSMALL) spl[tid + 512] = spv1;
-    if (tid < CH) ylds[tid] = yval ? ylab : -1;
+  };
+  auto store_chunk = [&](int chunk) __attribute__((always_inline)) {
+    store_body();
+    store_head();
   };
   load_dep(0);
+  // (w1s is read only by the dP MFMAs, several barriers later)
   if (tid < n8) *reinterpret_cast<uint4*>(w1s + (tid >> 3) * HP + (tid & 7) * 8) = wv0;
   if (tid + 512 < n8) *reinterpret_cast<uint4*>(w1s + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = wv1;
-  lds_barrier();  // w1s / staging visible
 
   const int dn = wave & 3, dm0 = wave >> 2;
   const bool mom = c.momentum != 0.f;
@@ -645,7 +655,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       lds_barrier();
       load_chunk(chunk);
     }
-    store_chunk(chunk);
+    if (ONE) store_head();
+    else store_chunk(chunk);
     lds_barrier();
     stamp(sts, st, 1);
     // eager: the slice's fp32 masters / velocities for the update right after the dW1
@@ -679,6 +690,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     }
     lds_barrier();
     stamp(sts, st, 6);
+    if (ONE && wave >= 4) store_body();  // (waves 4-7 have no logits to compute)
     // logits on f32 MFMA (wave mt: rows 16 mt .. 16 mt + 15, 16 columns, 10 used), then
     // softmax-xent / accuracy / dz over each row's 16 lanes (DPP row reductions); the four
     // rows j of a lane are independent chains, interleaved
@@ -721,6 +733,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
         if (lr == 0) rc[r] = (valid && am[j] == y) ? 1.f : 0.f;
       }
     }
+    if (ONE && wave < 4) store_body();
     lds_barrier();
     stamp(sts, st, 7);
     // dh = (dz W2^T) * [h > 0] on f32 MFMA: 16 tiles of 16x16, two per wave, K = 10 (three
