@@ -53,6 +53,8 @@ int wgrad64_rows(int N, int Ho, int Wo, int kstep);
 // A_WGRAD3: K = wgrad3_rows (q space), k_per_split a multiple of 32, tiles 64x64 x 9 taps
 hipError_t wgrad3_launch(const GemmArgs& a, int epi, int splits, hipStream_t s);
 int wgrad3_rows(int N, int H, int W);
+hipError_t wgrad3_stamps_enable(int on);                              // diagnostics
+hipError_t wgrad3_stamps_read(unsigned long long* host, int blocks);  // [blocks][4]
 // A_CONV3 / A_DGRAD3: tile 1 -> BN 64 (256 x 64), 0 -> BN 128 (128 x 128); output rows per
 // block for an H x W image (0: not supported); stats partials = Nimg * ceil(H / rows)
 hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream_t s);

@@ -311,7 +311,14 @@ hipError_t launch3_epi(const GemmArgs& a, int epi, int R, hipStream_t s) {
 
 }  // namespace
 
-hipError_t conv3_stamps_enable(int on) { return hipMemcpyToSymbol(HIP_SYMBOL(g_c3_on), &on, sizeof(int)); }
+hipError_t conv3_stamps_enable(int on) {
+  if (on) {  // clear the previous launch's stamps (a smaller grid leaves stale rows otherwise)
+    static unsigned long long zeros[kC3StampBlocks][4];
+    const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_c3_st), zeros, sizeof(zeros));
+    if (e != hipSuccess) return e;
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_c3_on), &on, sizeof(int));
+}
 // [blocks][4] stamps of the last conv3_kernel launch (host copy; synchronizes)
 hipError_t conv3_stamps_read(unsigned long long* host, int blocks) {
   if (blocks > kC3StampBlocks) blocks = kC3StampBlocks;

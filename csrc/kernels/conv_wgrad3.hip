@@ -67,6 +67,18 @@ __device__ __forceinline__ const uint16_t* w3_src(const uint16_t* base, const QG
   return base + ((long)(n * g.H + r) * g.W + c) * C + ch0 + 8 * chunk;
 }
 
+// s_waitcnt vmcnt(min(ahead, S - 2)): the DMA issues this wave may leave in flight
+template <int S>
+__device__ __forceinline__ void w3_wait_vm(int ahead) {
+  if (S >= 8 && ahead >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (S >= 7 && ahead >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if (S >= 6 && ahead >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (S >= 5 && ahead >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if (S >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (S >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Wave t = tap t: the whole 64x64 tile, 16 MFMAs and 16 transposed reads per k-step.
 // Every read address is a per-lane constant (set up once: the swizzle of a ring row depends
 // on its row mod 16 only, and k-steps advance the ring by 32 rows) plus, for x, the ring
@@ -75,9 +87,17 @@ __device__ __forceinline__ const uint16_t* w3_src(const uint16_t* base, const QG
 // ~5.6 VALU per MFMA (SQ_INSTS_VALU / SQ_INSTS_MFMA), which bound it.  Waves 0-3 DMA the
 // x block, 4-7 the dy block (one 1-KB DMA each per k-step).  S-stage pipeline: issue(kt)
 // = x block kt+2D + dy step kt, S-1 issues in flight, counted vmcnt.
+// Diagnostics (wgrad3_stamps_enable): per block s_memrealtime at start, first k-step's
+// operands landed, k-loop done, end -> g_w3_st[block][4]
+constexpr int kW3StampBlocks = 4096;
+__device__ int g_w3_on;
+__device__ unsigned long long g_w3_st[kW3StampBlocks][4];
+
 template <int S, int EPI>
 __global__ __launch_bounds__(576) void wgrad3_kernel(GemmArgs a) {
-  constexpr int XB = 8 * 32 * 128, DB = S * 32 * 128;  // x ring: 2D + S <= 8 blocks
+  const bool stamps = g_w3_on != 0;
+  unsigned long long st0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, st1 = 0ull, st2 = 0ull;
+  constexpr int XB = (S <= 4 ? 8 : 16) * 32 * 128, DB = S * 32 * 128;  // x ring: 2D + S blocks (power of 2)
   __shared__ __attribute__((aligned(1024))) char smem[XB + DB];
   char* xring = smem;
   char* dyb = smem + XB;
@@ -157,18 +177,10 @@ __global__ __launch_bounds__(576) void wgrad3_kernel(GemmArgs a) {
   auto step = [&](auto stg, int kt) __attribute__((always_inline)) {
     constexpr int ST = decltype(stg)::value;
     const int ahead = min(nk - 1 - kt, S - 2);  // issues in flight beyond kt (1 DMA each)
-    if constexpr (S >= 4) {
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (S == 3) {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    w3_wait_vm<S>(ahead);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    if (stamps && kt == 0) st1 = __builtin_amdgcn_s_memrealtime();
     if (kt + S - 1 < nk) issue(kt + S - 1, (ST + S - 1) % S);
     const int blo = (kt * 4096 + xlo0) & rbm, bhi = (kt * 4096 + xhi0) & rbm;
     const char* dstg = dyb + ST * 4096;
@@ -188,9 +200,23 @@ __global__ __launch_bounds__(576) void wgrad3_kernel(GemmArgs a) {
     if constexpr (S > 1) if (kt + 1 < nk) step(std::integral_constant<int, 1>{}, kt + 1);
     if constexpr (S > 2) if (kt + 2 < nk) step(std::integral_constant<int, 2 % S>{}, kt + 2);
     if constexpr (S > 3) if (kt + 3 < nk) step(std::integral_constant<int, 3 % S>{}, kt + 3);
+    if constexpr (S > 4) if (kt + 4 < nk) step(std::integral_constant<int, 4 % S>{}, kt + 4);
+    if constexpr (S > 5) if (kt + 5 < nk) step(std::integral_constant<int, 5 % S>{}, kt + 5);
+    if constexpr (S > 6) if (kt + 6 < nk) step(std::integral_constant<int, 6 % S>{}, kt + 6);
+    if constexpr (S > 7) if (kt + 7 < nk) step(std::integral_constant<int, 7 % S>{}, kt + 7);
   }
+  if (stamps) st2 = __builtin_amdgcn_s_memrealtime();
   // wave tile: rows m = tap*Cin + ci0 .. +63, columns co0 .. +63
   tile::epilogue<64, 64, EPI>(a, acc, wave * Cin + ci0, co0, 0, 0, 0, wave, lane, nullptr);
+  if (stamps && threadIdx.x == 0) {
+    const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (b < kW3StampBlocks) {
+      g_w3_st[b][0] = st0;
+      g_w3_st[b][1] = st1;
+      g_w3_st[b][2] = st2;
+      g_w3_st[b][3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 int w3_env(const char* name, int dflt) {
@@ -202,7 +228,20 @@ int w3_env(const char* name, int dflt) {
 
 // pipeline depth (2..4): env DAMD_WGRAD3_STAGES.  3 measured best on the ResNet-18 step
 // once the LDS-DMA issue moved to inline asm (2.85 vs 2.89 ms/step with 2, 2.85 with 4)
-int w3_stages() { return std::min(4, std::max(2, w3_env("DAMD_WGRAD3_STAGES", 3))); }
+int w3_stages() { return std::min(8, std::max(2, w3_env("DAMD_WGRAD3_STAGES", 3))); }
+
+hipError_t wgrad3_stamps_enable(int on) {
+  if (on) {
+    static unsigned long long zeros[kW3StampBlocks][4];
+    const hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_w3_st), zeros, sizeof(zeros));
+    if (e != hipSuccess) return e;
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_w3_on), &on, sizeof(int));
+}
+hipError_t wgrad3_stamps_read(unsigned long long* host, int blocks) {
+  if (blocks > kW3StampBlocks) blocks = kW3StampBlocks;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_w3_st), (size_t)blocks * 4 * sizeof(unsigned long long));
+}
 int wgrad3_rows(int N, int H, int W) { return N * (H + 1) * (W + 1); }
 
 hipError_t wgrad3_launch(const GemmArgs& a, int epi, int splits, hipStream_t s) {
@@ -219,7 +258,14 @@ hipError_t wgrad3_launch(const GemmArgs& a, int epi, int splits, hipStream_t s) 
 #define W3_LAUNCH(S_)                                                                             \
   hipLaunchKernelGGL((epi == E_SLAB ? wgrad3_kernel<S_, E_SLAB> : wgrad3_kernel<S_, E_ATOMIC>), grid, \
                      dim3(576), 0, s, a)
-  if (st == 2) W3_LAUNCH(2); else if (st == 3) W3_LAUNCH(3); else W3_LAUNCH(4);
+  switch (st) {
+    case 2: W3_LAUNCH(2); break;
+    case 3: W3_LAUNCH(3); break;
+    case 4: W3_LAUNCH(4); break;
+    case 5:
+    case 6: W3_LAUNCH(6); break;
+    default: W3_LAUNCH(8); break;
+  }
 #undef W3_LAUNCH
   return hipGetLastError();
 }

@@ -873,22 +873,30 @@ __device__ __forceinline__ void quad_route8(const uint16_t* __restrict__ dpool, 
   const int cg = g.C / 8;
   float dw[2][2][8];
   uint32_t aw[2][2][2];
+  // the four windows are loaded unconditionally at clamped coordinates and the out-of-range
+  // ones neutralised after (a load under the edge branch cost its own round trip: the
+  // ResNet-18 stem's backward apply 66 -> 59 us)
+  uint4 dq[2][2];
+  uint2 aq[2][2];
+#pragma unroll
+  for (int wr = 0; wr < 2; ++wr) {
+#pragma unroll
+    for (int wc = 0; wc < 2; ++wc) {
+      const int oh = min(max(a - 1 + PT + wr, 0), g.Ho - 1), ow = min(max(b - 1 + PL + wc, 0), g.Wo - 1);
+      const long w = (((long)n * g.Ho + oh) * g.Wo + ow) * cg + c8;
+      dq[wr][wc] = reinterpret_cast<const uint4*>(dpool)[w];
+      aq[wr][wc] = reinterpret_cast<const uint2*>(arg)[w];
+    }
+  }
 #pragma unroll
   for (int wr = 0; wr < 2; ++wr) {
 #pragma unroll
     for (int wc = 0; wc < 2; ++wc) {
       const int oh = a - 1 + PT + wr, ow = b - 1 + PL + wc;
-      if ((unsigned)oh < (unsigned)g.Ho && (unsigned)ow < (unsigned)g.Wo) {
-        const long w = (((long)n * g.Ho + oh) * g.Wo + ow) * cg + c8;
-        unpack8(reinterpret_cast<const uint4*>(dpool)[w], dw[wr][wc]);
-        const uint2 av = reinterpret_cast<const uint2*>(arg)[w];
-        aw[wr][wc][0] = av.x;
-        aw[wr][wc][1] = av.y;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) dw[wr][wc][e] = 0.f;
-        aw[wr][wc][0] = aw[wr][wc][1] = 0xffffffffu;  // code 255 never matches a tap
-      }
+      const bool ok = (unsigned)oh < (unsigned)g.Ho && (unsigned)ow < (unsigned)g.Wo;
+      unpack8(dq[wr][wc], dw[wr][wc]);
+      aw[wr][wc][0] = ok ? aq[wr][wc].x : 0xffffffffu;  // code 255 never matches a tap
+      aw[wr][wc][1] = ok ? aq[wr][wc].y : 0xffffffffu;
     }
   }
 #pragma unroll

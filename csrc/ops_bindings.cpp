@@ -66,6 +66,12 @@ void register_kernel_ops(py::module_& m) {
     check(damd::conv3_stamps_read(v.data(), blocks), "conv3_stamps_read");
     return v;
   });
+  m.def("wgrad3_stamps_enable", [](int on) { check(damd::wgrad3_stamps_enable(on), "wgrad3_stamps_enable"); });
+  m.def("wgrad3_stamps_read", [](int blocks) {
+    std::vector<unsigned long long> v((size_t)blocks * 4);
+    check(damd::wgrad3_stamps_read(v.data(), blocks), "wgrad3_stamps_read");
+    return v;
+  });
   m.def("splitk_finish", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, uintptr_t R, int relu,
                             uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream, uintptr_t stats_acc) {
     check(damd::splitk_finish(P_<const float>(slab), splits, M, N, P_<const float>(bias), P_<const uint16_t>(R), relu,

@@ -1,0 +1,52 @@
+"""Distribution of the bf16-vs-fp32 update agreement over many initial draws, for the
+tolerance tests whose bounds must hold for ANY init (tests/test_native_layers_gpu.py
+test_native_optimizers_track_reference): per optimizer and weight tensor, the min cosine
+and max relative error of the native graph engine's 10-step weight update against the
+fp32 generic engine over SEEDS draws.  GPU box:
+    python scripts/sweep_tolerances.py [seeds] [opt names...]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import distributed_amd as tf  # noqa: E402
+from test_native_graph_gpu import _data, _mnist, _train  # noqa: E402
+from test_native_layers_gpu import _opt_cases  # noqa: E402
+
+
+def stats(init, wa, wb):
+    out = []
+    for w0, a, b in zip(init, wa, wb):
+        da, db = (a - w0).ravel().astype(np.float64), (b - w0).ravel().astype(np.float64)
+        nb = np.linalg.norm(db)
+        cos = float(da @ db / (np.linalg.norm(da) * nb + 1e-30))
+        out.append((cos, float(np.linalg.norm(da - db) / max(nb, 1e-30))))
+    return out
+
+
+def main():
+    seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    names = sys.argv[2:] or list(_opt_cases())
+    names_w = ["k", "b", "k1", "b1", "k2", "b2"]
+    x, y = _data(640, (28, 28, 1), 10, seed=3)
+    for name in names:
+        rows = []
+        for s in range(seeds):
+            tf.set_seed(1000 + s)
+            tf.keras.backend.clear_session()
+            init = _mnist().get_weights()
+            opt = _opt_cases(eps=1e-2)[name]
+            wn, hn, en, _ = _train(_mnist, x, y, init, 64, 10, native=True, optimizer=opt)
+            wr, hr, er, _ = _train(_mnist, x, y, init, 64, 10, native=False, device="cpu", optimizer=opt)
+            rows.append(stats(init, wn, wr))
+        a = np.array(rows)  # [seed][tensor][cos, rel]
+        print(f"{name}: " + "  ".join(f"{nm} cos min {a[:, i, 0].min():.4f} med {np.median(a[:, i, 0]):.4f} "
+                                      f"rel max {a[:, i, 1].max():.3f}" for i, nm in enumerate(names_w)), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -72,7 +72,9 @@ def _data(n, shape, classes, seed=0):
     return x, y
 
 
-def _compare_updates(init, wa, wb, names, cos_min=0.98, rel_max=0.08):
+def _compare_updates(init, wa, wb, names, cos_min=0.98, rel_max=0.08, idx=None):
+    if idx is not None:  # compare only the tensors at these positions
+        init, wa, wb = [init[i] for i in idx], [wa[i] for i in idx], [wb[i] for i in idx]
     for w0, a, b, nm in zip(init, wa, wb, names):
         da, db = (a - w0).ravel().astype(np.float64), (b - w0).ravel().astype(np.float64)
         nb = np.linalg.norm(db)
