@@ -206,8 +206,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       const int n = n0 + t;
       if (n < a.N) {
         if (a.stats_acc) {
-          unsafeAtomicAdd(a.stats_acc + n, (double)s);
-          unsafeAtomicAdd(a.stats_acc + a.N + n, (double)q);
+          double* acc = a.stats_acc + (size_t)(a.stats_reps > 1 ? tm % a.stats_reps : 0) * 2 * a.N;
+          unsafeAtomicAdd(acc + n, (double)s);
+          unsafeAtomicAdd(acc + a.N + n, (double)q);
         } else {
           float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
           st[n] = s;

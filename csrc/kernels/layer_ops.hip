@@ -99,30 +99,60 @@ __device__ __forceinline__ void reduce_partials8(const float* __restrict__ part,
 // accumulators into LDS (s: [4][C] for the forward, [3][C] for the backward); block 0 also
 // publishes them (st / co), updates the moving statistics and adds dgamma / dbeta.  The
 // returned pointer replaces st / co in the kernel body (global when acc is null).
+// The replicas acc[r][2][C] are summed in replica order.
+__device__ __forceinline__ void acc_sums(const double* acc, int reps, int C, int c, double& s, double& q) {
+  s = acc[c];
+  q = acc[C + c];
+  for (int r = 1; r < reps; ++r) {
+    s += acc[(size_t)r * 2 * C + c];
+    q += acc[(size_t)r * 2 * C + C + c];
+  }
+}
+// coefficients of channel c (mean, invstd, scale, shift); pub: also published to st and
+// the moving statistics (one thread per channel of the whole grid)
+__device__ __forceinline__ void bn_fin_sums(const BNFin& f, int C, int c, double s, double q, bool pub, float& m,
+                                            float& inv, float& sc, float& sh) {
+  const double mean = s / (double)f.count;
+  double var = q / (double)f.count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  m = (float)mean;
+  const float v = (float)var;
+  inv = rsqrtf(v + f.eps);
+  const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
+  sc = g * inv;
+  sh = b - m * sc;
+  if (pub) {
+    f.st[c] = m;
+    f.st[C + c] = inv;
+    f.st[2 * C + c] = sc;
+    f.st[3 * C + c] = sh;
+    if (f.rmean) {
+      f.rmean[c] = f.rmean[c] * f.mom + m * (1.f - f.mom);
+      f.rvar[c] = f.rvar[c] * f.mom + v * (1.f - f.mom);
+    }
+  }
+}
+// backward coefficients of channel c: dx = a dz + b + cc xhat; pub: co, dgamma, dbeta
+__device__ __forceinline__ void bn_bwd_fin_sums(const BNBwdFin& f, int C, int c, double s, double q,
+                                                const float* st, bool pub, float& a, float& b, float& cc) {
+  const float db = (float)s, dg = (float)q;
+  a = st[2 * C + c];
+  b = -a * db / f.count;
+  cc = -a * dg / f.count;
+  if (pub) {
+    if (f.dbeta) f.dbeta[c] += db;
+    if (f.dgamma) f.dgamma[c] += dg;
+    f.co[c] = a;
+    f.co[C + c] = b;
+    f.co[2 * C + c] = cc;
+  }
+}
 __device__ __forceinline__ const float* bn_fin_prologue(const BNFin& f, int C, float* s, const float* st) {
   if (f.acc == nullptr) return st;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const double mean = f.acc[c] / (double)f.count;
-    double var = f.acc[C + c] / (double)f.count - mean * mean;
-    if (var < 0.0) var = 0.0;
-    const float m = (float)mean, v = (float)var;
-    const float inv = rsqrtf(v + f.eps);
-    const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
-    const float sc = g * inv, sh = b - m * sc;
-    s[c] = m;
-    s[C + c] = inv;
-    s[2 * C + c] = sc;
-    s[3 * C + c] = sh;
-    if (blockIdx.x == 0) {
-      f.st[c] = m;
-      f.st[C + c] = inv;
-      f.st[2 * C + c] = sc;
-      f.st[3 * C + c] = sh;
-      if (f.rmean) {
-        f.rmean[c] = f.rmean[c] * f.mom + m * (1.f - f.mom);
-        f.rvar[c] = f.rvar[c] * f.mom + v * (1.f - f.mom);
-      }
-    }
+    double a, b;
+    acc_sums(f.acc, f.reps, C, c, a, b);
+    bn_fin_sums(f, C, c, a, b, blockIdx.x == 0, s[c], s[C + c], s[2 * C + c], s[3 * C + c]);
   }
   __syncthreads();
   return s;
@@ -131,28 +161,20 @@ __device__ __forceinline__ const float* bn_bwd_fin_prologue(const BNBwdFin& f, i
                                                             const float* co) {
   if (f.acc == nullptr) return co;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float db = (float)f.acc[c], dg = (float)f.acc[C + c];
-    const float a = st[2 * C + c];
-    s[c] = a;
-    s[C + c] = -a * db / f.count;
-    s[2 * C + c] = -a * dg / f.count;
-    if (blockIdx.x == 0) {
-      if (f.dbeta) f.dbeta[c] += db;
-      if (f.dgamma) f.dgamma[c] += dg;
-      f.co[c] = s[c];
-      f.co[C + c] = s[C + c];
-      f.co[2 * C + c] = s[2 * C + c];
-    }
+    double a, b;
+    acc_sums(f.acc, f.reps, C, c, a, b);
+    bn_bwd_fin_sums(f, C, c, a, b, st, blockIdx.x == 0, s[c], s[C + c], s[2 * C + c]);
   }
   __syncthreads();
   return s;
 }
-// per-block (fp32, fixed order) partial of channel ch -> the fp64 accumulator or the
-// partials row of this block
-__device__ __forceinline__ void put_partial(float* part, double* acc, int C, int ch, float a, float b) {
+// per-block (fp32, fixed order) partial of channel ch -> replica blockIdx.x % reps of the
+// fp64 accumulator, or the partials row of this block
+__device__ __forceinline__ void put_partial(float* part, double* acc, int reps, int C, int ch, float a, float b) {
   if (acc) {
-    unsafeAtomicAdd(acc + ch, (double)a);
-    unsafeAtomicAdd(acc + C + ch, (double)b);
+    double* r = acc + (size_t)(blockIdx.x % reps) * 2 * C;
+    unsafeAtomicAdd(r + ch, (double)a);
+    unsafeAtomicAdd(r + C + ch, (double)b);
   } else {
     part[(size_t)blockIdx.x * 2 * C + ch] = a;
     part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
@@ -220,20 +242,40 @@ __global__ __launch_bounds__(NT) void bn_apply_k(const uint16_t* __restrict__ x,
   }
 }
 
-// Row-mapped apply kernels (no in-consumer finalize): thread t keeps channel group
-// t % (C/8) for the whole launch, so its per-channel coefficients are loaded once into
-// registers instead of once per 16-byte data vector (the flat kernels above fetched 2-7
-// coefficient vectors per data vector); BN_UNR rows per thread in flight.  Same arithmetic,
-// bitwise equal output.  Measured on ResNet-18: backward apply 9.9 -> 8.8 us per launch,
-// forward apply unchanged (already at HBM rate); the same unrolling of bn_bwd_reduce_k's
-// row loop was slower (8.6 -> 9.5 us) and is not used.
+// Row-mapped apply kernels: thread t keeps channel group t % (C/8) for the whole launch,
+// so its per-channel coefficients are loaded once into registers instead of once per
+// 16-byte data vector (the flat kernels above fetched 2-7 coefficient vectors per data
+// vector); BN_UNR rows per thread in flight.  Same arithmetic, bitwise equal output.
+// Measured on ResNet-18: backward apply 9.9 -> 8.8 us per launch, forward apply unchanged
+// (already at HBM rate); the same unrolling of bn_bwd_reduce_k's row loop was slower
+// (8.6 -> 9.5 us) and is not used.  With the in-consumer finalize (BNFin / BNBwdFin) the
+// first batch of rows is requested before the prologue, so the data fetch overlaps the
+// accumulator read and the fp64 finalize instead of queueing behind them.
 constexpr int BN_UNR = 4;
-__global__ __launch_bounds__(NT) void bn_apply_rows_k(const uint16_t* __restrict__ x, const float* __restrict__ st,
-                                                      const uint16_t* __restrict__ r, const float* __restrict__ st2,
-                                                      int res_mode, int relu, uint16_t* __restrict__ y, long M, int C) {
-  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;
+__global__ __launch_bounds__(NT) void bn_apply_rows_k(const uint16_t* __restrict__ x, const float* st,
+                                                      const uint16_t* __restrict__ r, const float* st2,
+                                                      int res_mode, int relu, uint16_t* __restrict__ y, long M, int C,
+                                                      BNFin f1, BNFin f2) {
+  extern __shared__ float sfin[];  // in-consumer finalize: [4][C] (f1), then [4][C] (f2)
+  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;  // launcher: NT % cg == 0
   const int g = t % cg, rr = t / cg, c = g * 8;
-  if (rr >= rpi) return;
+  const long stride = (long)gridDim.x * rpi;
+  const uint4* x4 = reinterpret_cast<const uint4*>(x);
+  const uint4* r4 = reinterpret_cast<const uint4*>(r);
+  uint4* y4 = reinterpret_cast<uint4*>(y);
+  uint4 xq[BN_UNR], rq[BN_UNR];
+  auto load = [&](long row0) {
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = min(row0 + u * stride, M - 1);
+      xq[u] = x4[row * cg + g];
+      if (res_mode) rq[u] = r4[row * cg + g];
+    }
+  };
+  long row0 = (long)blockIdx.x * rpi + rr;
+  load(row0);
+  st = bn_fin_prologue(f1, C, sfin, st);
+  if (res_mode == 2) st2 = bn_fin_prologue(f2, C, sfin + 4 * C, st2);
   float sc[8], sh[8], sc2[8], sh2[8];
   ld8f(st + 2 * C + c, sc);
   ld8f(st + 3 * C + c, sh);
@@ -241,18 +283,8 @@ __global__ __launch_bounds__(NT) void bn_apply_rows_k(const uint16_t* __restrict
     ld8f(st2 + 2 * C + c, sc2);
     ld8f(st2 + 3 * C + c, sh2);
   }
-  const long stride = (long)gridDim.x * rpi;
-  const uint4* x4 = reinterpret_cast<const uint4*>(x);
-  const uint4* r4 = reinterpret_cast<const uint4*>(r);
-  uint4* y4 = reinterpret_cast<uint4*>(y);
-  for (long row0 = (long)blockIdx.x * rpi + rr; row0 < M; row0 += stride * BN_UNR) {
-    uint4 xq[BN_UNR], rq[BN_UNR];
-#pragma unroll
-    for (int u = 0; u < BN_UNR; ++u) {
-      const long row = min(row0 + u * stride, M - 1);
-      xq[u] = x4[row * cg + g];
-      if (res_mode) rq[u] = r4[row * cg + g];
-    }
+  for (bool first = true; row0 < M; row0 += stride * BN_UNR, first = false) {
+    if (!first) load(row0);
 #pragma unroll
     for (int u = 0; u < BN_UNR; ++u) {
       const long row = row0 + u * stride;
@@ -283,11 +315,29 @@ __global__ __launch_bounds__(NT) void bn_apply_rows_k(const uint16_t* __restrict
 __global__ __launch_bounds__(NT) void bn_bwd_apply_rows_k(const uint16_t* __restrict__ dy,
                                                           const uint16_t* __restrict__ y, int relu_mask,
                                                           const uint16_t* __restrict__ x, const float* __restrict__ st,
-                                                          const float* __restrict__ co, uint16_t* __restrict__ dx,
-                                                          long M, int C) {
-  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;
+                                                          const float* co, uint16_t* __restrict__ dx,
+                                                          long M, int C, BNBwdFin bf) {
+  extern __shared__ float sfin[];  // in-consumer finalize: [3][C]
+  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;  // launcher: NT % cg == 0
   const int g = t % cg, rr = t / cg, c = g * 8;
-  if (rr >= rpi) return;
+  const long stride = (long)gridDim.x * rpi;
+  const uint4* d4 = reinterpret_cast<const uint4*>(dy);
+  const uint4* x4 = reinterpret_cast<const uint4*>(x);
+  const uint4* y4 = reinterpret_cast<const uint4*>(y);
+  uint4* o4 = reinterpret_cast<uint4*>(dx);
+  uint4 dq[BN_UNR], xq[BN_UNR], yq[BN_UNR];
+  auto load = [&](long row0) {
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = min(row0 + u * stride, M - 1);
+      dq[u] = d4[row * cg + g];
+      xq[u] = x4[row * cg + g];
+      if (relu_mask == 1) yq[u] = y4[row * cg + g];
+    }
+  };
+  long row0 = (long)blockIdx.x * rpi + rr;
+  load(row0);
+  co = bn_bwd_fin_prologue(bf, C, st, sfin, co);
   float mean[8], inv[8], a[8], b[8], cc[8], sc[8], sh[8];
   ld8f(st + c, mean);
   ld8f(st + C + c, inv);
@@ -298,20 +348,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rows_k(const uint16_t* __rest
     ld8f(st + 2 * C + c, sc);
     ld8f(st + 3 * C + c, sh);
   }
-  const long stride = (long)gridDim.x * rpi;
-  const uint4* d4 = reinterpret_cast<const uint4*>(dy);
-  const uint4* x4 = reinterpret_cast<const uint4*>(x);
-  const uint4* y4 = reinterpret_cast<const uint4*>(y);
-  uint4* o4 = reinterpret_cast<uint4*>(dx);
-  for (long row0 = (long)blockIdx.x * rpi + rr; row0 < M; row0 += stride * BN_UNR) {
-    uint4 dq[BN_UNR], xq[BN_UNR], yq[BN_UNR];
-#pragma unroll
-    for (int u = 0; u < BN_UNR; ++u) {
-      const long row = min(row0 + u * stride, M - 1);
-      dq[u] = d4[row * cg + g];
-      xq[u] = x4[row * cg + g];
-      if (relu_mask == 1) yq[u] = y4[row * cg + g];
-    }
+  for (bool first = true; row0 < M; row0 += stride * BN_UNR, first = false) {
+    if (!first) load(row0);
 #pragma unroll
     for (int u = 0; u < BN_UNR; ++u) {
       const long row = row0 + u * stride;
@@ -340,7 +378,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
                                                       int relu_mask, const uint16_t* __restrict__ x,
                                                       const float* __restrict__ st, uint16_t* __restrict__ dz_out,
                                                       float* __restrict__ part, long M, int C, long rows_per_block,
-                                                      double* __restrict__ acc) {
+                                                      double* __restrict__ acc, int reps) {
   __shared__ float red[2][NT * 8];
   const int cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;  // rows per iteration
@@ -393,7 +431,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
       a += red[0][(q * cg + gg) * 8 + e];
       b += red[1][(q * cg + gg) * 8 + e];
     }
-    put_partial(part, acc, C, ch, a, b);
+    put_partial(part, acc, reps, C, ch, a, b);
   }
 }
 
@@ -783,7 +821,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_k(const uint16_t* __res
                                                            const uint8_t* __restrict__ arg, PoolGeo g,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ st,
                                                            float* __restrict__ part, long M, long rows_per_block,
-                                                           double* __restrict__ acc) {
+                                                           double* __restrict__ acc, int reps) {
   __shared__ float red[2][NT * 8];
   const int C = g.C, cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;
@@ -822,7 +860,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_k(const uint16_t* __res
       a += red[0][(q * cg + gg) * 8 + e];
       b += red[1][(q * cg + gg) * 8 + e];
     }
-    put_partial(part, acc, C, ch, a, b);
+    put_partial(part, acc, reps, C, ch, a, b);
   }
 }
 
@@ -928,7 +966,8 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_q_k(const uint16_t* __r
                                                              const uint8_t* __restrict__ arg, PoolGeo g,
                                                              const uint16_t* __restrict__ x,
                                                              const float* __restrict__ st, float* __restrict__ part,
-                                                             long nquad, long quads_per_block, double* __restrict__ acc) {
+                                                             long nquad, long quads_per_block, double* __restrict__ acc,
+                                                             int reps) {
   __shared__ float red[2][NT * 8];
   const int C = g.C, cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;
@@ -981,7 +1020,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_q_k(const uint16_t* __r
       sa += red[0][(q * cg + gg) * 8 + e];
       sb += red[1][(q * cg + gg) * 8 + e];
     }
-    put_partial(part, acc, C, ch, sa, sb);
+    put_partial(part, acc, reps, C, ch, sa, sb);
   }
 }
 
@@ -1686,10 +1725,21 @@ hipError_t bn_finalize(const float* part, int T, int C, float count, const float
 }
 
 // row-mapped apply kernels: about BN_UNR rows per thread (one batch of loads in flight)
-static int rows_grid(long M, int C) {
+static int rows_grid(long M, int C, int cap = 16384) {
   const long rpi = NT / (C / 8);
   long g = (M + rpi * BN_UNR - 1) / (rpi * BN_UNR);
-  return (int)(g < 1 ? 1 : (g > 16384 ? 16384 : g));
+  return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+// grid cap of a row-mapped consumer that finalizes in its prologue (env DAMD_BN_FIN_GRID):
+// every block pays the prologue, so fewer, longer-lived blocks.  ResNet-18 step: 2.707 ms
+// uncapped (1568 blocks on layer 1), 2.671 at 512, 2.665 at 768.
+static int fin_rows_cap() {
+  static int cap = [] {
+    const char* e = getenv("DAMD_BN_FIN_GRID");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 768;
+  }();
+  return cap;
 }
 
 // blocks of a consumer that finalizes in its prologue: every block pays one pass over the
@@ -1707,8 +1757,10 @@ hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const
   const size_t lds = (a.acc ? 4 * C * sizeof(float) : 0) + (b.acc ? 4 * C * sizeof(float) : 0);
   // (the f2 region starts at 4C: allocate it whenever f2 finalizes)
   const size_t lds2 = b.acc ? 8 * C * sizeof(float) : lds;
-  if (!a.acc && !b.acc && NT % (C / 8) == 0) {
-    hipLaunchKernelGGL(bn_apply_rows_k, dim3(rows_grid(M, C)), dim3(NT), 0, s, x, st, r, st2, res_mode, relu, y, M, C);
+  if (NT % (C / 8) == 0) {
+    hipLaunchKernelGGL(bn_apply_rows_k, dim3(rows_grid(M, C, (a.acc || b.acc) ? fin_rows_cap() : 16384)), dim3(NT),
+                       lds2, s, x, st, r, st2,
+                       res_mode, relu, y, M, C, a, b);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(bn_apply_k, dim3(grid_for(n8, NT, (a.acc || b.acc) ? FIN_GRID_CAP : 8192)), dim3(NT), lds2, s,
@@ -1724,11 +1776,12 @@ int bn_bwd_blocks(long M, int C) {
 }
 
 hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
-                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s, double* acc) {
-  if (C % 8 || C / 8 > NT || (!part && !acc)) return hipErrorInvalidValue;
+                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s, double* acc,
+                         int acc_reps) {
+  if (C % 8 || C / 8 > NT || (!part && !acc) || acc_reps < 1) return hipErrorInvalidValue;
   const long rows = (M + T - 1) / T;
   hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows,
-                     acc);
+                     acc, acc_reps);
   return hipGetLastError();
 }
 
@@ -1746,9 +1799,10 @@ hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, co
   const long n8 = M * C / 8;
   const BNBwdFin f = bf ? *bf : kNoBwdFin;
   if (f.acc && (!f.co || C > FIN_MAX_C)) return hipErrorInvalidValue;
-  if (!f.acc && NT % (C / 8) == 0) {
-    hipLaunchKernelGGL(bn_bwd_apply_rows_k, dim3(rows_grid(M, C)), dim3(NT), 0, s, dy, y, relu_mask, x, st, co, dx, M,
-                       C);
+  if (NT % (C / 8) == 0) {
+    hipLaunchKernelGGL(bn_bwd_apply_rows_k, dim3(rows_grid(M, C, f.acc ? fin_rows_cap() : 16384)), dim3(NT),
+                       f.acc ? 3 * C * sizeof(float) : 0, s, dy, y,
+                       relu_mask, x, st, co, dx, M, C, f);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(bn_bwd_apply_k, dim3(grid_for(n8, NT, f.acc ? FIN_GRID_CAP : 8192)), dim3(NT),
@@ -1794,18 +1848,19 @@ hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H,
 
 hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                               int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                              float* part, int T, hipStream_t s, double* acc) {
-  if (C % 8 || C / 8 > NT || (!part && !acc)) return hipErrorInvalidValue;
+                              float* part, int T, hipStream_t s, double* acc, int acc_reps) {
+  if (C % 8 || C / 8 > NT || (!part && !acc) || acc_reps < 1) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   const long M = (long)N * H * W, rows = (M + T - 1) / T;
   if (quad_pool_geo(g)) {
     const long nq = (long)N * Ho * Wo, qpb = (nq + T - 1) / T;
     auto k = g.pt ? (g.pl ? pool_bn_bwd_reduce_q_k<1, 1> : pool_bn_bwd_reduce_q_k<1, 0>)
                   : (g.pl ? pool_bn_bwd_reduce_q_k<0, 1> : pool_bn_bwd_reduce_q_k<0, 0>);
-    hipLaunchKernelGGL(k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, nq, qpb, acc);
+    hipLaunchKernelGGL(k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, nq, qpb, acc, acc_reps);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(pool_bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, M, rows, acc);
+  hipLaunchKernelGGL(pool_bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dpool, arg, g, x, st, part, M, rows, acc,
+                     acc_reps);
   return hipGetLastError();
 }
 

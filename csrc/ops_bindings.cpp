@@ -29,9 +29,11 @@ void register_kernel_ops(py::module_& m) {
       "gemm",
       [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,
          uintptr_t stats, uintptr_t R, int M, int N, int K, int lda, int ldb, int ldc, std::vector<int> geo, int kc,
-         int k_per_split, uintptr_t stream, int kstep, uintptr_t stats_acc, uintptr_t bnx, uintptr_t bnst) {
+         int k_per_split, uintptr_t stream, int kstep, uintptr_t stats_acc, uintptr_t bnx, uintptr_t bnst,
+         int stats_reps) {
         damd::GemmArgs a{};
         a.stats_acc = P_<double>(stats_acc);
+        a.stats_reps = stats_reps;
         a.bnx = P_<const uint16_t>(bnx);
         a.bnst = P_<const float>(bnst);
         a.A = P_<const void>(A);
@@ -56,7 +58,8 @@ void register_kernel_ops(py::module_& m) {
       py::arg("amode"), py::arg("bmode"), py::arg("epi"), py::arg("splits"), py::arg("tile"), py::arg("A"),
       py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("stats"), py::arg("R"), py::arg("M"), py::arg("N"), py::arg("K"),
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
-      py::arg("stream"), py::arg("kstep") = 0, py::arg("stats_acc") = 0, py::arg("bnx") = 0, py::arg("bnst") = 0);
+      py::arg("stream"), py::arg("kstep") = 0, py::arg("stats_acc") = 0, py::arg("bnx") = 0, py::arg("bnst") = 0,
+      py::arg("stats_reps") = 1);
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
   m.def("conv_gemm_kstep", &damd::conv_gemm_kstep);
   m.def("conv3_rows", &damd::conv3_rows);
@@ -73,13 +76,15 @@ void register_kernel_ops(py::module_& m) {
     return v;
   });
   m.def("splitk_finish", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, uintptr_t R, int relu,
-                            uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream, uintptr_t stats_acc) {
+                            uintptr_t stats, int rb, uintptr_t out, int ldc, uintptr_t stream, uintptr_t stats_acc,
+                            int stats_reps) {
     check(damd::splitk_finish(P_<const float>(slab), splits, M, N, P_<const float>(bias), P_<const uint16_t>(R), relu,
                               P_<float>(stats), rb, P_<uint16_t>(out), ldc, P_<ihipStream_t>(stream),
-                              P_<double>(stats_acc)),
+                              P_<double>(stats_acc), stats_reps),
           "splitk_finish");
   }, py::arg("slab"), py::arg("splits"), py::arg("M"), py::arg("N"), py::arg("bias"), py::arg("R"), py::arg("relu"),
-     py::arg("stats"), py::arg("rb"), py::arg("out"), py::arg("ldc"), py::arg("stream"), py::arg("stats_acc") = 0);
+     py::arg("stats"), py::arg("rb"), py::arg("out"), py::arg("ldc"), py::arg("stream"), py::arg("stats_acc") = 0,
+     py::arg("stats_reps") = 1);
   m.def("splitk_finish_f32", [](uintptr_t slab, int splits, int M, int N, uintptr_t bias, int relu, uintptr_t out,
                                 int ldc, uintptr_t stream) {
     check(damd::splitk_finish_f32(P_<const float>(slab), splits, M, N, P_<const float>(bias), relu, P_<float>(out),
@@ -126,17 +131,18 @@ void register_kernel_ops(py::module_& m) {
   auto mkfin = [](const std::vector<U>& p, const std::vector<float>& v) {
     damd::BNFin f{};
     if (p.empty()) return f;
-    if (p.size() != 6 || v.size() != 3) throw std::invalid_argument("fin: 6 pointers + [count, eps, momentum]");
+    if (p.size() != 6 || v.size() != 4) throw std::invalid_argument("fin: 6 pointers + [count, eps, momentum, reps]");
     f.acc = P_<const double>(p[0]); f.gamma = P_<const float>(p[1]); f.beta = P_<const float>(p[2]);
     f.st = P_<float>(p[3]); f.rmean = P_<float>(p[4]); f.rvar = P_<float>(p[5]);
-    f.count = v[0]; f.eps = v[1]; f.mom = v[2];
+    f.count = v[0]; f.eps = v[1]; f.mom = v[2]; f.reps = (int)v[3];
     return f;
   };
-  auto mkbfin = [](const std::vector<U>& p, float count) {
+  auto mkbfin = [](const std::vector<U>& p, float count, int reps) {
     damd::BNBwdFin f{};
     if (p.size() != 4) throw std::invalid_argument("bfin: [acc, dgamma, dbeta, co]");
     f.acc = P_<const double>(p[0]); f.dgamma = P_<float>(p[1]); f.dbeta = P_<float>(p[2]); f.co = P_<float>(p[3]);
     f.count = count;
+    f.reps = reps;
     return f;
   };
   m.def("bn_apply_fin", [mkfin](U x, U r, int res_mode, int relu, U y, long M, int C, std::vector<U> p1,
@@ -146,14 +152,15 @@ void register_kernel_ops(py::module_& m) {
                          P_<ihipStream_t>(s), &a, &b),
           "bn_apply_fin");
   });
-  m.def("bn_bwd_reduce_acc", [](U dy, U y, int relu_mask, U x, U st, U dz, U acc, int T, long M, int C, U s) {
+  m.def("bn_bwd_reduce_acc", [](U dy, U y, int relu_mask, U x, U st, U dz, U acc, int T, long M, int C, U s,
+                                int reps) {
     check(damd::bn_bwd_reduce(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
-                              P_<u16>(dz), nullptr, T, M, C, P_<ihipStream_t>(s), P_<double>(acc)),
+                              P_<u16>(dz), nullptr, T, M, C, P_<ihipStream_t>(s), P_<double>(acc), reps),
           "bn_bwd_reduce_acc");
   });
   m.def("bn_bwd_apply_fin", [mkbfin](U dy, U y, int relu_mask, U x, U st, U dx, long M, int C, std::vector<U> bp,
-                                     float count, U s) {
-    const damd::BNBwdFin f = mkbfin(bp, count);
+                                     float count, U s, int reps) {
+    const damd::BNBwdFin f = mkbfin(bp, count, reps);
     check(damd::bn_bwd_apply(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
                              f.co, P_<u16>(dx), M, C, P_<ihipStream_t>(s), &f),
           "bn_bwd_apply_fin");
@@ -166,17 +173,17 @@ void register_kernel_ops(py::module_& m) {
                                     g[9], g[10], g[11], P_<u16>(y), P_<uint8_t>(arg), P_<ihipStream_t>(s), &f),
           "bn_relu_maxpool_fwd_fin");
   });
-  m.def("pool_bn_bwd_reduce_acc", [](U dpool, U arg, std::vector<int> g, U x, U st, U acc, int T, U s) {
+  m.def("pool_bn_bwd_reduce_acc", [](U dpool, U arg, std::vector<int> g, U x, U st, U acc, int T, U s, int reps) {
     if (g.size() != 12) throw std::invalid_argument("pool geometry");
     check(damd::pool_bn_bwd_reduce(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
                                    g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st),
-                                   nullptr, T, P_<ihipStream_t>(s), P_<double>(acc)),
+                                   nullptr, T, P_<ihipStream_t>(s), P_<double>(acc), reps),
           "pool_bn_bwd_reduce_acc");
   });
   m.def("pool_bn_bwd_apply_fin", [mkbfin](U dpool, U arg, std::vector<int> g, U x, U st, U dx, std::vector<U> bp,
-                                          float count, U s) {
+                                          float count, U s, int reps) {
     if (g.size() != 12) throw std::invalid_argument("pool geometry");
-    const damd::BNBwdFin f = mkbfin(bp, count);
+    const damd::BNBwdFin f = mkbfin(bp, count, reps);
     check(damd::pool_bn_bwd_apply(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
                                   g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st), f.co,
                                   P_<u16>(dx), P_<ihipStream_t>(s), &f),

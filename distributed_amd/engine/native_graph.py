@@ -137,11 +137,12 @@ class NativeGraphEngine(Engine):
                  "AveragePooling2D", "GlobalAveragePooling2D", "Flatten", "Dense", "Dropout")
     ACTIVATIONS = ("linear", "relu", "sigmoid", "tanh")
     _weights_static = False  # True for an inference plan: padded weight copies made once per call
-    # DAMD_BN_FIN=1: BatchNorm statistics through fp64 accumulators finalized inside the
-    # consumer kernels (ops/hip.py BNFin): 40 fewer launches per ResNet-18 step, but every
-    # producer block adds into the same 2C addresses, and those same-address fp64 atomics
-    # serialise at the memory side (bn_bwd_reduce 8 -> 27 us): measured 3.13 vs 2.80
-    # ms/step, so the per-block partials + finalize kernels stay the default
+    # DAMD_BN_FIN (default on): BatchNorm statistics through fp64 accumulators finalized
+    # inside the consumer kernels (ops/hip.py BNFin): 40 fewer launches per ResNet-18 step.
+    # Same-address fp64 atomics serialise at the memory side (~18 ns each: with one
+    # accumulator bn_bwd_reduce took 8.6 -> 26 us, the step 3.02 ms), so the producers add
+    # into DAMD_BN_REPS (8) replicas (block b -> replica b % 8) that the consumers sum in
+    # order: 2.665 vs 2.712 ms/step with the partials + finalize launches (DAMD_BN_FIN=0).
     _bn_fin = True
 
     @staticmethod
@@ -563,19 +564,20 @@ class NativeGraphEngine(Engine):
         backward sums) in one buffer, cleared by the step's gather_batch launch; the conv
         producing a BN input accumulates into it from its epilogue."""
         bns = [nd for nd in self.nodes if nd.kind == "BatchNormalization" and not nd.attrs.get("dead")]
-        use = (self._bn_fin and env.get_bool("DAMD_BN_FIN", False)
+        use = (self._bn_fin and env.get_bool("DAMD_BN_FIN", True)
                and all(nd.out.shape[-1] <= H.FIN_MAX_C for nd in bns))
         self.bn_acc = None
         if not use or not bns:
             return
-        tot = sum(4 * nd.out.shape[-1] for nd in bns)
+        R = max(1, env.get_int("DAMD_BN_REPS", 8))
+        tot = sum(4 * R * nd.out.shape[-1] for nd in bns)
         self.bn_acc = torch.zeros(tot, dtype=torch.float64, device=self.device)
         o = 0
         for nd in bns:
             C = nd.out.shape[-1]
-            nd.attrs["acc_f"] = self.bn_acc[o:o + 2 * C]
-            nd.attrs["acc_b"] = self.bn_acc[o + 2 * C:o + 4 * C]
-            o += 4 * C
+            nd.attrs["acc_f"] = self.bn_acc[o:o + 2 * C * R].view(R, 2 * C)
+            nd.attrs["acc_b"] = self.bn_acc[o + 2 * C * R:o + 4 * C * R].view(R, 2 * C)
+            o += 4 * C * R
             if nd.attrs.get("stats_from_conv"):
                 self._producer(nd.inputs[0]).attrs["stats_buf"] = nd.attrs["acc_f"]
             l = nd.layer
@@ -594,7 +596,7 @@ class NativeGraphEngine(Engine):
         for bn in self.nodes:
             a = bn.attrs
             if (bn.kind != "BatchNormalization" or a.get("dead") or not a.get("relu") or a.get("stats_only")
-                    or a.get("pool") is not None or a.get("fin") is not None):
+                    or a.get("pool") is not None):
                 continue
             outs = bn.out.consumers
             if len(outs) != 1 or not outs[0].attrs.get("dead") or len(outs[0].out.consumers) != 1:
@@ -606,7 +608,9 @@ class NativeGraphEngine(Engine):
             plan = H.conv_dgrad_plan(bn.out.shape, tuple(l.kernel.shape), l.strides, l.padding)
             if plan["amode"] != H.A_DGRAD3:
                 continue
-            a["dgrad_part"] = torch.zeros(plan["stats_T"], 2, bn.out.shape[-1], device=self.device)
+            # with the in-consumer finalize the epilogue adds into the fp64 accumulator
+            a["dgrad_part"] = (a["acc_b"] if a.get("fin") is not None else
+                               torch.zeros(plan["stats_T"], 2, bn.out.shape[-1], device=self.device))
             conv.attrs["bnred"] = bn
 
     def _view_or_none(self, var):
@@ -917,7 +921,8 @@ class NativeGraphEngine(Engine):
         if fin is not None:
             if not nd.attrs.get("stats_from_conv"):  # sum / sum of squares of x into acc_f
                 self.C.bn_bwd_reduce_acc(x.buf.data_ptr(), 0, 0, x.buf.data_ptr(), self._ident(C).data_ptr(), 0,
-                                         nd.attrs["acc_f"].data_ptr(), nd.attrs["T"], M, C, H.stream_handle())
+                                         nd.attrs["acc_f"].data_ptr(), nd.attrs["T"], M, C, H.stream_handle(),
+                                         H.acc_reps(nd.attrs["acc_f"]))
             if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None:
                 return  # finalized and applied by the fused Add / MaxPool that consumes it
             H.bn_apply_fin(x.buf, nd.out.root().buf, fin, relu=nd.attrs.get("relu", False))
@@ -1066,15 +1071,16 @@ class NativeGraphEngine(Engine):
         ym = ymask.data_ptr() if relu else 0
         mode = (2 if mask_from_x else 1) if relu else 0
         dx, fin = self._grad_target(x)
+        fused = bn.attrs.get("dgrad_fused") and mode == 2 and dz_out is None
         if bn.attrs.get("fin") is not None and dx is not None:
             H.bn_bwd_fin(dy, ymask if relu else None, mode, x.buf, st, bn.attrs["acc_b"], co, dx,
                          dgamma=self.gviews[id(l.gamma)] if l.gamma is not None else None,
                          dbeta=self.gviews[id(l.beta)] if l.beta is not None else None,
-                         dz_out=dz_out if relu else None)
+                         dz_out=dz_out if relu else None, reduce=not fused)
             if fin:
                 fin()
             return
-        if bn.attrs.get("dgrad_fused") and mode == 2 and dz_out is None:
+        if fused:
             part = bn.attrs["dgrad_part"]  # written by the consuming conv's backprop-input epilogue
             Tn = part.shape[0]
         else:

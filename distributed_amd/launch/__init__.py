@@ -30,8 +30,10 @@ from typing import Any, Callable, List, Optional, Sequence
 from ..parallel.cluster import tf_config_json
 
 
-def free_port_base(n: int, host: str = "127.0.0.1", start: int = 20000, end: int = 60000) -> int:
-    """First base port such that [base, base+n) are all bindable right now."""
+def free_port_base(n: int, host: str = "127.0.0.1", start: int = 20000, end: int = 32000) -> int:
+    """First base port such that [base, base+n) are all bindable right now.  The range sits
+    below Linux's ephemeral ports (32768-60999), which outgoing connections of any process
+    may take between this check and the rank's bind."""
     import random
 
     rng = random.Random(os.getpid() ^ int(time.time() * 1000))

@@ -247,24 +247,31 @@ def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=(), ac
     _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw), stream_handle(), accumulate=int(accumulate))
 
 
+def acc_reps(acc):
+    """Replica count of an fp64 BatchNorm accumulator: [reps][2][C] (2-D [reps, 2C]) or a
+    single [2][C] (1-D).  Producer block b adds into replica b % reps (layer_ops.h BNFin)."""
+    return int(acc.shape[0]) if acc is not None and acc.dim() == 2 else 1
+
+
 def _stats_ptrs(stats):
-    """(partials pointer, fp64 accumulator pointer) of a stats argument: an fp32 [T][2][N]
-    partials tensor, or an fp64 [2][N] accumulator (BNFin: producers add, the consumer
-    finalizes)."""
+    """(partials pointer, fp64 accumulator pointer, replicas) of a stats argument: an fp32
+    [T][2][N] partials tensor, or an fp64 [2][N] / [reps][2N] accumulator (BNFin: producers
+    add, the consumer finalizes)."""
     if stats is None:
-        return 0, 0
+        return 0, 0, 1
     if stats.dtype == torch.float64:
-        return 0, _ptr(stats)
-    return _ptr(stats), 0
+        return 0, _ptr(stats), acc_reps(stats)
+    return _ptr(stats), 0, 1
 
 
 def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
          geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0, bnx=None, bnst=None):
     t = pick_tile(N) if tile is None else tile
     kps = k_per_split if k_per_split is not None else -(-K // BK) * BK
-    sp, sa = _stats_ptrs(stats)
+    sp, sa, reps = _stats_ptrs(stats)
     _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), sp, _ptr(R), M, N, K,
-              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep, stats_acc=sa, bnx=_ptr(bnx), bnst=_ptr(bnst))
+              lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep, stats_acc=sa, bnx=_ptr(bnx), bnst=_ptr(bnst),
+              stats_reps=reps)
 
 
 # ---- dense -------------------------------------------------------------------------------
@@ -414,17 +421,17 @@ def conv_fwd_stem4(x, w8, out, kernel_size, strides=(2, 2), padding="same", bias
     ws = _workspace(workspace, plan["ws"], x.device)
     gemm(x, w8, ws, amode=A_CONV64, bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=32)
-    sp, sa = _stats_ptrs(stats)
+    sp, sa, reps = _stats_ptrs(stats)
     _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), sp, FINISH_RB,
-                       _ptr(out), cout, stream_handle(), stats_acc=sa)
+                       _ptr(out), cout, stream_handle(), stats_acc=sa, stats_reps=reps)
 
 
 def _check_stats(stats, plan, cout, who):
     if stats is None:
         return
     if stats.dtype == torch.float64:
-        if stats.numel() != 2 * cout:
-            raise ValueError(f"{who}: an fp64 statistics accumulator has 2 x {cout} elements, got {stats.numel()}")
+        if stats.numel() != 2 * cout * acc_reps(stats) or stats.shape[-1] != 2 * cout:
+            raise ValueError(f"{who}: an fp64 statistics accumulator is [reps][2 x {cout}], got {tuple(stats.shape)}")
     elif stats.shape[0] != plan["stats_T"]:
         raise ValueError(f"{who}: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
 
@@ -540,9 +547,9 @@ def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, 
     ws = _workspace(workspace, plan["ws"], x.device)
     gemm(x, w, ws, amode=plan["amode"], bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,
          splits=plan["splits"], k_per_split=plan["kps"], tile=plan["tile"], geo=geo)
-    sp, sa = _stats_ptrs(stats)
+    sp, sa, reps = _stats_ptrs(stats)
     _C().splitk_finish(_ptr(ws), plan["splits"], M, cout, _ptr(bias), 0, int(relu), sp, FINISH_RB,
-                       _ptr(out), cout, stream_handle(), stats_acc=sa)
+                       _ptr(out), cout, stream_handle(), stats_acc=sa, stats_reps=reps)
 
 
 def _workspace(ws, need, device):
@@ -580,7 +587,8 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
     """dx [N,H,W,Cin] (+)= backprop-input of dy [N,Ho,Wo,Cout] through w.  ``bnred`` =
     (x, st, part): dx is the gradient of relu(BN(x)) (BN coefficients st [4][Cin]); when the
     direct kernel runs (conv_dgrad_plan stats_T rows) it also writes the BN-backward
-    partials (sum dz, sum dz * xhat per tile) into part [stats_T][2][Cin], replacing
+    partials (sum dz, sum dz * xhat per tile) into part [stats_T][2][Cin] (or adds them into
+    an fp64 accumulator [reps][2 Cin]), replacing
     bn_bwd_reduce.  Returns True when it did."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx.shape, w.shape, strides, padding)
     if s not in (1, 2):
@@ -595,7 +603,9 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
     geo = (h, wd, cout, ho, wo, kh, kw, s, pad)
     if bnred is not None and plan["amode"] == A_DGRAD3 and not accumulate:
         bx, bst, part = bnred
-        if part.shape[0] != plan["stats_T"] or tuple(bx.shape) != tuple(dx.shape):
+        fp64 = part.dtype == torch.float64  # an fp64 accumulator [reps][2 Cin] (BNBwdFin)
+        if ((part.shape[-1] != 2 * cin if fp64 else part.shape[0] != plan["stats_T"])
+                or tuple(bx.shape) != tuple(dx.shape)):
             raise ValueError("conv_dgrad: bnred partials / BN input do not match the plan")
         gemm(dy, w, dx, amode=A_DGRAD3, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_BF16 | E_BNRED, kc=cout,
              geo=geo, stats=part, tile=plan["tile"], bnx=bx, bnst=bst)
@@ -712,7 +722,8 @@ def pool_bn_bwd(dpool, arg, x, st, part, co, dx, pool, strides, padding, dgamma=
 
 # ---- BatchNorm with the finalize folded into the consumer kernel (layer_ops.h BNFin) ------
 # The producers (conv / dense GEMM epilogue with an fp64 `stats` tensor, split-K finish,
-# bn_bwd_reduce with `acc`) add their per-block partials into an fp64 [2][C] accumulator;
+# bn_bwd_reduce with `acc`) add their per-block partials into an fp64 [2][C] accumulator
+# (or [reps, 2C]: block b into replica b % reps, summed in order by the consumer);
 # the consumer derives the coefficients in its prologue, so neither bn_finalize nor
 # bn_bwd_finalize is launched.  The accumulators must be zero before the producers run
 # (the native graph engine clears them all in the step's gather_batch launch).
@@ -728,7 +739,7 @@ class BNFin:
     def __init__(self, acc, gamma, beta, st, rmean, rvar, count, eps, momentum):
         self.acc, self.st = acc, st
         self._p = [_ptr(acc), _ptr(gamma), _ptr(beta), _ptr(st), _ptr(rmean), _ptr(rvar)]
-        self._v = [float(count), float(eps), float(momentum)]
+        self._v = [float(count), float(eps), float(momentum), float(acc_reps(acc))]
 
     def args(self):
         return self._p, self._v
@@ -747,17 +758,20 @@ def bn_apply_fin(x, y, fin: BNFin, relu=False, r=None, fin2: Optional[BNFin] = N
     _C().bn_apply_fin(_ptr(x), _ptr(r), mode, int(relu), _ptr(y), M, C, p1, v1, p2, v2, stream_handle())
 
 
-def bn_bwd_fin(dy, y, relu_mask, x, st, acc, co, dx, dgamma=None, dbeta=None, dz_out=None):
+def bn_bwd_fin(dy, y, relu_mask, x, st, acc, co, dx, dgamma=None, dbeta=None, dz_out=None, reduce=True):
     """BN backward in two launches: bn_bwd_reduce adds sum(dz), sum(dz * xhat) into the fp64
-    accumulator acc [2][C]; bn_bwd_apply derives co, adds dgamma / dbeta (block 0) and
-    writes dx."""
+    accumulator acc [2][C] (reduce=False: a conv epilogue, E_BNRED, already did); bn_bwd_apply
+    derives co, adds dgamma / dbeta (block 0) and writes dx."""
     C = x.shape[-1]
     M = x.numel() // C
     T = _C().bn_bwd_blocks(M, C)
     s = stream_handle()
-    _C().bn_bwd_reduce_acc(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dz_out), _ptr(acc), T, M, C, s)
+    r = acc_reps(acc)
+    if reduce:
+        _C().bn_bwd_reduce_acc(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dz_out), _ptr(acc), T, M, C,
+                               s, r)
     _C().bn_bwd_apply_fin(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dx), M, C,
-                          [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s)
+                          [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s, r)
 
 
 def bn_relu_maxpool_fwd_fin(x, y, arg, pool, strides, padding, fin: BNFin):
@@ -772,9 +786,10 @@ def pool_bn_bwd_fin(dpool, arg, x, st, acc, co, dx, pool, strides, padding, dgam
     M = x.numel() // C
     T = _C().bn_bwd_blocks(M, C)
     s = stream_handle()
-    _C().pool_bn_bwd_reduce_acc(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(acc), T, s)
+    r = acc_reps(acc)
+    _C().pool_bn_bwd_reduce_acc(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(acc), T, s, r)
     _C().pool_bn_bwd_apply_fin(_ptr(dpool), _ptr(arg), g, _ptr(x), _ptr(st), _ptr(dx),
-                               [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s)
+                               [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s, r)
 
 
 def gap_fwd(x, y):

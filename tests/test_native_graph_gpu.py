@@ -388,6 +388,39 @@ def test_bn_backward_reduce_fused_into_dgrad_epilogue(monkeypatch):
         np.testing.assert_allclose(hf["loss"], hu["loss"], rtol=1e-5)
 
 
+@pytest.mark.parametrize("reps", ["1", "8"])
+def test_bn_finalize_in_consumer_matches_finalize_kernels(monkeypatch, reps):
+    """BatchNorm statistics through fp64 accumulators (DAMD_BN_FIN=1: producers -- conv
+    epilogues, split-K finish, the backprop-input E_BNRED epilogue, bn_bwd_reduce, the stem
+    pool -- add per-block partials into `reps` replicas, the apply kernels finalize in their
+    prologue) == the per-block partials + finalize launches, one step, three initial draws;
+    and two runs with it are bitwise equal (fp64 sums of fp32 partials: arrival order does
+    not change them)."""
+    from distributed_amd.ops import hip as H
+
+    def build():
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    monkeypatch.setenv("DAMD_BN_REPS", reps)
+    assert H.conv_dgrad_plan((32, 16, 16, 64), (3, 3, 64, 64), (1, 1), "same")["amode"] == H.A_DGRAD3
+    x, y = _data(64, (64, 64, 3), 10, seed=9)
+    for rep in range(3):
+        tf.keras.backend.clear_session()
+        init = build().get_weights()
+        wf, hf, ef = _train(build, x, y, init, 32, 1, native=True, extra_env={"DAMD_BN_FIN": "1"})
+        wk, hk, ek = _train(build, x, y, init, 32, 1, native=True, extra_env={"DAMD_BN_FIN": "0"})
+        assert ef == ek == "native_graph"
+        for a, b in zip(wf, wk):
+            np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-4)
+        np.testing.assert_allclose(hf["loss"], hk["loss"], rtol=1e-5)
+    w2, h2, _ = _train(build, x, y, init, 32, 2, native=True, momentum=0.9, extra_env={"DAMD_BN_FIN": "1"})
+    w3, h3, _ = _train(build, x, y, init, 32, 2, native=True, momentum=0.9, extra_env={"DAMD_BN_FIN": "1"})
+    for a, b in zip(w2, w3):
+        np.testing.assert_array_equal(a, b)
+    assert h2 == h3
+
+
 def test_resnet18_full_size_trains():
     x, y = _data(64, (224, 224, 3), 1000, seed=3)
     tf.keras.backend.clear_session()

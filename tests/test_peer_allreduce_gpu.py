@@ -26,8 +26,10 @@ def _env(out, **kw):
 @pytest.mark.parametrize("world,blocks", [(2, 64), (4, 16)])
 @pytest.mark.timeout(300)
 def test_peer_allreduce_bitwise(tmp_path, world, blocks):
+    # max_restarts=1: a new port range if the rendezvous port was taken (EADDRINUSE) in the
+    # window between free_port_base's check and the bind; a protocol failure fails twice
     res = launch.launch_script([os.path.join(ROOT, "tests", "helpers", "peer_worker.py")], nproc=world,
-                               env=_env(tmp_path, DAMD_PEER_BLOCKS=blocks), timeout=240)
+                               env=_env(tmp_path, DAMD_PEER_BLOCKS=blocks), timeout=240, max_restarts=1)
     assert res.ok, res.returncodes
     rs = [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
     for j in rs:
