@@ -198,42 +198,49 @@ def test_small_resnet_step_matches_bf16_emulated_reference():
     accumulation) against an fp32 re-execution with the same bf16 storage points: after
     one plain-SGD step every weight update must agree.
 
-    The agreement depends on the random init: a 1-ulp fp32 difference flips some bf16
-    roundings and the BN-backward cancellation amplifies them, so across inits the worst
-    layer's relative update error measured 0.01-0.23 (median layer 0.004-0.16) -- with
-    the register-staged and the LDS-DMA conv kernels alike (bitwise-equal outputs, see
-    test_conv_gemm_gpu.py).  Hence a fixed init and aggregate bounds; exact wiring checks
-    are the bitwise fused-vs-unfused tests."""
+    A 1-ulp fp32 difference (summation order) flips some bf16 roundings and the BN-backward
+    cancellation amplifies them.  Bounds from a 16-init sweep (scripts/sweep_emulated_ref.py,
+    round 4): loss error <= 2.2e-3 relative, worst layer's relative update error <= 0.156,
+    median layer <= 0.098, worst layer cosine >= 0.990, head <= 9.2e-3, whole update vector
+    cosine >= 0.9946 / relative error <= 0.104 -- so any init passes the bounds below (three
+    unpinned inits per run); exact wiring checks are the bitwise fused-vs-unfused tests."""
     x, y = _data(32, (32, 32, 3), 10, seed=4)
     os.environ["DAMD_FUSED"] = "0"
     try:
-        tf.keras.backend.clear_session()
-        tf.set_seed(2)
-        m = _small_resnet()
-        lr = 0.1
-        m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
-                  optimizer=tf.keras.optimizers.SGD(learning_rate=lr), metrics=["accuracy"])
-        e = m._get_engine(32, 32)
-        assert e.name == "native_graph"
-        e.bind(x, y)
-        e.start_epoch(0, False)
-        w0 = {id(v): v.value.detach().clone() for v in m.trainable_weights}
-        grads, ref_loss = _emulated_reference_grads(e, m, x, y, 32)
-        e.run(1)
-        e.sync()
-        met = e.metrics()
-        assert abs(met["loss"] - ref_loss) < 2e-3 * abs(ref_loss)
-        rels = []
-        for v in m.trainable_weights:
-            d_native = (v.value.detach() - w0[id(v)]).double().ravel()
-            d_ref = (-lr * grads[id(v)]).double().ravel()
-            nref = d_ref.norm().item()
-            rel = (d_native - d_ref).norm().item() / max(nref, 1e-12)
-            cos = float(d_native @ d_ref / max(d_native.norm().item() * nref, 1e-30))
-            assert cos > 0.97 and rel < 0.25, f"{v.name}: rel err {rel:.4f} cos {cos:.4f} (|d| {nref:.3e})"
-            rels.append(rel)
-        assert sorted(rels)[len(rels) // 2] < 0.1, rels
-        assert rels[-2] < 2e-2, rels  # the head (predictions kernel): no BN below it
+        for rep in range(3):
+            tf.keras.backend.clear_session()
+            seed = int.from_bytes(os.urandom(4), "little")  # a fresh draw, printed for replay
+            print(f"init seed {seed}")
+            tf.set_seed(seed)
+            m = _small_resnet()
+            lr = 0.1
+            m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                      optimizer=tf.keras.optimizers.SGD(learning_rate=lr), metrics=["accuracy"])
+            e = m._get_engine(32, 32)
+            assert e.name == "native_graph"
+            e.bind(x, y)
+            e.start_epoch(0, False)
+            w0 = {id(v): v.value.detach().clone() for v in m.trainable_weights}
+            grads, ref_loss = _emulated_reference_grads(e, m, x, y, 32)
+            e.run(1)
+            e.sync()
+            met = e.metrics()
+            assert abs(met["loss"] - ref_loss) < 5e-3 * abs(ref_loss)
+            rels, dn, dr = [], [], []
+            for v in m.trainable_weights:
+                d_native = (v.value.detach() - w0[id(v)]).double().ravel()
+                d_ref = (-lr * grads[id(v)]).double().ravel()
+                nref = d_ref.norm().item()
+                rel = (d_native - d_ref).norm().item() / max(nref, 1e-12)
+                cos = float(d_native @ d_ref / max(d_native.norm().item() * nref, 1e-30))
+                assert cos > 0.97 and rel < 0.3, f"{v.name}: rel err {rel:.4f} cos {cos:.4f} (|d| {nref:.3e})"
+                rels.append(rel)
+                dn.append(d_native)
+                dr.append(d_ref)
+            assert sorted(rels)[len(rels) // 2] < 0.15, rels
+            assert rels[-2] < 2e-2, rels  # the head (predictions kernel): no BN below it
+            a, b = torch.cat(dn), torch.cat(dr)
+            assert float(a @ b / (a.norm() * b.norm())) > 0.99 and float((a - b).norm() / b.norm()) < 0.15
     finally:
         os.environ.pop("DAMD_FUSED", None)
 
