@@ -1,0 +1,50 @@
+// BatchNorm statistics finalize from the fp64 accumulators (layer_ops.h BNFin), shared by
+// the consumers that finalize in their prologue: the apply kernels (layer_ops.hip) and the
+// direct conv that normalises its input on load (conv3x3.hip, GemmArgs::bnin).  One
+// definition, so every consumer derives bitwise the same coefficients.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "layer_ops.h"
+
+namespace damd {
+
+// The replicas acc[r][2][C] are summed in replica order.
+__device__ inline void acc_sums(const double* acc, int reps, int C, int c, double& s, double& q) {
+  s = acc[c];
+  q = acc[C + c];
+  for (int r = 1; r < reps; ++r) {
+    s += acc[(size_t)r * 2 * C + c];
+    q += acc[(size_t)r * 2 * C + C + c];
+  }
+}
+// coefficients of channel c (mean, invstd, scale, shift); pub: also published to st and
+// the moving statistics (one thread per channel of the whole grid)
+// (g, b: gamma[c] / beta[c], or 1 / 0 -- loaded by the caller, possibly early)
+__device__ inline void bn_fin_sums_gb(const BNFin& f, int C, int c, double s, double q, float g, float b, bool pub,
+                                      float& m, float& inv, float& sc, float& sh) {
+  const double mean = s / (double)f.count;
+  double var = q / (double)f.count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  m = (float)mean;
+  const float v = (float)var;
+  inv = rsqrtf(v + f.eps);
+  sc = g * inv;
+  sh = b - m * sc;
+  if (pub) {
+    f.st[c] = m;
+    f.st[C + c] = inv;
+    f.st[2 * C + c] = sc;
+    f.st[3 * C + c] = sh;
+    if (f.rmean) {
+      f.rmean[c] = f.rmean[c] * f.mom + m * (1.f - f.mom);
+      f.rvar[c] = f.rvar[c] * f.mom + v * (1.f - f.mom);
+    }
+  }
+}
+__device__ inline void bn_fin_sums(const BNFin& f, int C, int c, double s, double q, bool pub, float& m,
+                                   float& inv, float& sc, float& sh) {
+  bn_fin_sums_gb(f, C, c, s, q, f.gamma ? f.gamma[c] : 1.f, f.beta ? f.beta[c] : 0.f, pub, m, inv, sc, sh);
+}
+
+}  // namespace damd

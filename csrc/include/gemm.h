@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "layer_ops.h"
+
 namespace damd {
 
 enum GemmAMode { A_KC = 0, A_IM2COL = 1, A_DGRAD = 2, A_MC = 3, A_WGRAD = 4,
@@ -43,6 +45,12 @@ struct GemmArgs {
   int stats_reps;      //   M-tile tm into replica tm % reps (0 / 1: one), see layer_ops.h BNFin
   const uint16_t* bnx; // E_BNRED: the BN input x [M][ldc] bf16 and its st [4][N] (mean,
   const float* bnst;   //   invstd, scale, shift)
+  // A_CONV3 forward, bnin.acc non-null: A is a BatchNorm's INPUT; the kernel finalizes its
+  // statistics (bnin, as the apply kernels do: block (0, 0) publishes st / moving stats) and
+  // normalises + ReLUs the staged halo in LDS (bitwise bn_apply's values); the blocks of
+  // N-tile 0 also store that BN -> ReLU output to bnin_y (for the conv's weight gradient).
+  BNFin bnin;
+  uint16_t* bnin_y;
 };
 
 // tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)

@@ -7,6 +7,8 @@
 
 namespace damd {
 
+struct Ctrl;  // kernels_api.h / damd_common.h
+
 // BatchNorm (training) ---------------------------------------------------------------
 // Batch statistics without a finalize launch: the producers (conv GEMM epilogue E_STATS
 // with GemmArgs::stats_acc, splitk_finish, bn_bwd_reduce / pool_bn_bwd_reduce with `acc`)

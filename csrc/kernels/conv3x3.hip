@@ -25,6 +25,7 @@
 // (2 x 2), each wave 64 x 64 as 4 x 4 v_mfma_f32_16x16x32_bf16.  Rows of the tile beyond
 // the block's R x W pixels read a clamped halo pixel and are masked in the epilogue.
 // Epilogue: tile::epilogue (bias / residual add / BN statistics per tile / ReLU / bf16).
+#include "bn_fin.h"
 #include "damd_common.h"
 #include "gemm.h"
 #include "gemm_tile.h"
@@ -55,8 +56,10 @@ constexpr int C3_HQ = 6;
 
 // pf: issue prefetch() after tap KH's weight stage; the stage waits of the later taps then
 // leave those C3_HQ newer DMA instructions in flight
-template <int STAGES, int NQ, class Issue, class Compute, class Prefetch>
-__device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute, Prefetch& prefetch, bool pf) {
+// pre(): once, after the first tap's operands (and so the chunk's halo) have landed, before
+// any tap reads the halo (the BN-input transform; it ends with its own barrier)
+template <int STAGES, int NQ, class Issue, class Compute, class Prefetch, class Pre>
+__device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute, Prefetch& prefetch, bool pf, Pre& pre) {
   constexpr int NK = 9, KH = NK - STAGES;
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s, s);
@@ -87,6 +90,7 @@ __device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute, Prefetc
     __builtin_amdgcn_s_barrier();
     if (kt + STAGES - 1 < NK) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
     if (pf && kt == KH) prefetch();
+    if (kt == 0) pre();
     compute(kt % STAGES, kt);
   }
 }
@@ -96,7 +100,7 @@ __device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute, Prefetc
 // (% 64), N = output channels (% BN); H, W the (shared) image size.  R output rows per
 // block, tpi = ceil(H / R) row blocks per image; grid (N / BN, Nimg * tpi).
 template <int BN, bool DGRAD, int EPI, int STAGES>
-__global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi, int hb2) {
+__global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi, int hb2, int sft_off) {
   const bool stamps = g_c3_on != 0;
   unsigned long long st0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0ull, st1 = 0ull, st2 = 0ull;
   constexpr int WN = BN / 64, WM = 4 / WN, BM = WM * 64;
@@ -160,6 +164,25 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // BatchNorm on the input (a.bnin): thread t < SC requests channel t's accumulator
+  // replicas now (in flight with the first halo / weight DMA); the first chunk's pre()
+  // finalizes them into LDS (sft: [2][SC] floats past the halo / ring)
+  const bool bnin = !DGRAD && a.bnin.acc != nullptr;
+  float* sft = reinterpret_cast<float*>(smem + sft_off);
+  constexpr int FR = 8;  // replicas held in registers (more: summed in pre())
+  double fs[FR], fq[FR];
+  float fg = 1.f, fb = 0.f;
+  if (bnin && t < SC) {
+    if (a.bnin.gamma) fg = a.bnin.gamma[t];
+    if (a.bnin.beta) fb = a.bnin.beta[t];
+#pragma unroll
+    for (int r = 0; r < FR; ++r) {
+      const int rr = min(r, max(a.bnin.reps, 1) - 1);
+      fs[r] = a.bnin.acc[(size_t)rr * 2 * SC + t];
+      fq[r] = a.bnin.acc[(size_t)rr * 2 * SC + SC + t];
+    }
+  }
 
   const int nchunks = SC / 64;
   // halo instruction j (all 64 lanes): pixel q = 8j + lane / 8, 16-byte slot lane & 7 of
@@ -236,7 +259,99 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
       __builtin_amdgcn_sched_barrier(0);
       mma(1);
     };
-    tap_loop<STAGES, NB>(issue, compute, prefetch, pf_on && chunk + 1 < nchunks);
+    // BN input: y = bf16(relu(x * scale + shift)) in place over the chunk's halo (in-image
+    // pixels only: the zero padding is the padding of y), exactly bn_apply's arithmetic
+    auto pre = [&]() __attribute__((always_inline)) {
+      if (!bnin) return;
+      if (chunk == 0) {  // the statistics -> scale / shift of all SC channels
+        const bool pub = tn == 0 && tm == 0;
+        for (int c = t; c < SC; c += NT) {
+          double s, q;
+          float m, inv, sc, sh;
+          if (c == t && a.bnin.reps <= FR) {  // requested at kernel start
+            s = fs[0];
+            q = fq[0];
+#pragma unroll
+            for (int r = 1; r < FR; ++r)
+              if (r < a.bnin.reps) {
+                s += fs[r];
+                q += fq[r];
+              }
+            bn_fin_sums_gb(a.bnin, SC, c, s, q, fg, fb, pub, m, inv, sc, sh);
+          } else {
+            acc_sums(a.bnin.acc, a.bnin.reps, SC, c, s, q);
+            bn_fin_sums(a.bnin, SC, c, s, q, pub, m, inv, sc, sh);
+          }
+          sft[c] = sc;
+          sft[SC + c] = sh;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+      // thread t: 16-byte slot t & 7 of pixels q = t / 8 + 32 k; that slot holds the same
+      // 8 channels in every one of them (the swizzle c ^ (q & 7) is fixed: 32 k = 0 mod 8)
+      int q = t >> 3;
+      const int sl = t & 7, ch = c0 + 8 * (sl ^ (q & 7));
+      float sc[8], sh[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sc[e] = sft[ch + e];
+        sh[e] = sft[SC + ch + e];
+      }
+      int hr = q / HW, hc = q - hr * HW;
+      // TU pixels per pass: all their LDS reads issued before the first transform
+      constexpr int TU = 4;
+      for (; q < hpix; q += TU * (NT / 8)) {
+        uint4 v[TU];
+        bool ok[TU];
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+          const int qu = q + u * (NT / 8);
+          const int ih = oh0 - 1 + hr, iw = hc - 1;
+          ok[u] = qu < hpix && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+          v[u] = *reinterpret_cast<const uint4*>(hcur + min(qu, hpix - 1) * 128 + 16 * sl);
+          hc += NT / 8;
+          while (hc >= HW) {
+            hc -= HW;
+            ++hr;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < TU; ++u) {
+          if (!ok[u]) continue;
+          const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float lo = fmaxf(fmaf(__uint_as_float(w[k] << 16), sc[2 * k], sh[2 * k]), 0.f);
+            const float hi = fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), sc[2 * k + 1], sh[2 * k + 1]), 0.f);
+            o[k] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+          }
+          *reinterpret_cast<uint4*>(hcur + (q + u * (NT / 8)) * 128 + 16 * sl) = uint4{o[0], o[1], o[2], o[3]};
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    };
+    tap_loop<STAGES, NB>(issue, compute, prefetch, pf_on && chunk + 1 < nchunks, pre);
+    // BN input: the block's output rows of y (this chunk's 64 channels) back to memory, from
+    // the transformed halo interior (N-tile 0 only; the halo stays intact until the next
+    // chunk's barrier)
+    if (bnin && tn == 0 && a.bnin_y) {
+      const int cl = t & 7;
+      int p = t >> 3, r = p / W, c = p - r * W;
+      uint16_t* yb = a.bnin_y + (long)(img * H + oh0) * W * SC + c0 + 8 * cl;
+      for (; p < npx; p += NT / 8) {
+        const int q = (r + 1) * HW + c + 1;
+        *reinterpret_cast<uint4*>(yb + (long)p * SC) =
+            *reinterpret_cast<const uint4*>(hcur + q * 128 + 16 * (cl ^ (q & 7)));
+        c += NT / 8;
+        while (c >= W) {
+          c -= W;
+          ++r;
+        }
+      }
+    }
   }
   if (stamps) st2 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();  // `red` of the epilogue aliases the halo
@@ -277,7 +392,8 @@ hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
   // double-buffered halo: several chunks, the padded DMA count fits C3_HQ per wave, and no
   // residency lost -- the grid fits one block per CU anyway, or two blocks still fit a CU's
   // LDS (DAMD_CONV3_HB2=0: single buffer)
-  const size_t lds2 = 2 * hb + 1024 + ring;
+  const size_t sft = (!DG && a.bnin.acc) ? (size_t)2 * a.Cin * sizeof(float) : 0;  // BN-input scale / shift
+  const size_t lds2 = 2 * hb + 1024 + ring + sft;
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -288,7 +404,8 @@ hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
   const char* ev = getenv("DAMD_CONV3_HB2");
   const int hb2 = !(ev && ev[0] == '0') && a.Cin / 64 > 1 && (int)(hb / 1024) <= 4 * C3_HQ && lds2 <= 160 * 1024 &&
                   (grid <= cus || lds2 <= 80 * 1024);
-  hipLaunchKernelGGL(k, dim3(a.N / BN, nimg * tpi), dim3(NT), hb2 ? lds2 : hb + ring, s, a, R, tpi, hb2);
+  const size_t lds = hb2 ? lds2 : hb + ring + sft;
+  hipLaunchKernelGGL(k, dim3(a.N / BN, nimg * tpi), dim3(NT), lds, s, a, R, tpi, hb2, (int)(lds - sft));
   return hipGetLastError();
 }
 
@@ -345,7 +462,7 @@ hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream
   const int R = conv3_rows(a.H, a.W, bn);
   if (R == 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || a.Cin % 64 || a.N % bn || a.M % (a.H * a.W))
     return hipErrorInvalidValue;
-  if (dgrad && a.kc != a.Cin) return hipErrorInvalidValue;
+  if (dgrad && (a.kc != a.Cin || a.bnin.acc)) return hipErrorInvalidValue;
   if (epi & (E_SLAB | E_ATOMIC)) return hipErrorInvalidValue;
   // (a weight-stationary persistent variant for 64 -> 64 channels -- 72 KiB of weights +
   // two halos = the CU's 160 KiB -- measured slower on ResNet layer 1, forward 42 vs 33 us,

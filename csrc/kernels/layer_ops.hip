@@ -7,6 +7,7 @@
 // 16-byte vector of 8 channels (global_load_dwordx4) and keeps the 8 per-channel
 // parameters in registers.  Statistics are reduced in fp32 per block (LDS), then across
 // blocks in double by a finalize kernel (deterministic, no atomics on the hot reductions).
+#include "bn_fin.h"
 #include "damd_common.h"
 #include "layer_ops.h"
 
@@ -99,39 +100,6 @@ __device__ __forceinline__ void reduce_partials8(const float* __restrict__ part,
 // accumulators into LDS (s: [4][C] for the forward, [3][C] for the backward); block 0 also
 // publishes them (st / co), updates the moving statistics and adds dgamma / dbeta.  The
 // returned pointer replaces st / co in the kernel body (global when acc is null).
-// The replicas acc[r][2][C] are summed in replica order.
-__device__ __forceinline__ void acc_sums(const double* acc, int reps, int C, int c, double& s, double& q) {
-  s = acc[c];
-  q = acc[C + c];
-  for (int r = 1; r < reps; ++r) {
-    s += acc[(size_t)r * 2 * C + c];
-    q += acc[(size_t)r * 2 * C + C + c];
-  }
-}
-// coefficients of channel c (mean, invstd, scale, shift); pub: also published to st and
-// the moving statistics (one thread per channel of the whole grid)
-__device__ __forceinline__ void bn_fin_sums(const BNFin& f, int C, int c, double s, double q, bool pub, float& m,
-                                            float& inv, float& sc, float& sh) {
-  const double mean = s / (double)f.count;
-  double var = q / (double)f.count - mean * mean;
-  if (var < 0.0) var = 0.0;
-  m = (float)mean;
-  const float v = (float)var;
-  inv = rsqrtf(v + f.eps);
-  const float g = f.gamma ? f.gamma[c] : 1.f, b = f.beta ? f.beta[c] : 0.f;
-  sc = g * inv;
-  sh = b - m * sc;
-  if (pub) {
-    f.st[c] = m;
-    f.st[C + c] = inv;
-    f.st[2 * C + c] = sc;
-    f.st[3 * C + c] = sh;
-    if (f.rmean) {
-      f.rmean[c] = f.rmean[c] * f.mom + m * (1.f - f.mom);
-      f.rvar[c] = f.rvar[c] * f.mom + v * (1.f - f.mom);
-    }
-  }
-}
 // backward coefficients of channel c: dx = a dz + b + cc xhat; pub: co, dgamma, dbeta
 __device__ __forceinline__ void bn_bwd_fin_sums(const BNBwdFin& f, int C, int c, double s, double q,
                                                 const float* st, bool pub, float& a, float& b, float& cc) {

@@ -550,6 +550,7 @@ class NativeGraphEngine(Engine):
                     nd.attrs["dz"] = torch.zeros(nd.out.shape, dtype=torch.bfloat16, device=dev)
         self._plan_bn_fin()
         self._plan_bn_dgrad_fusion()
+        self._plan_bn_conv_fold()
         # one scratch bf16 buffer for "second writer" gradient accumulation
         big = max([int(np.prod(t.shape)) for t in self._all_tensors()] + [1])
         self.scratch = torch.zeros(big, dtype=torch.bfloat16, device=dev)
@@ -612,6 +613,34 @@ class NativeGraphEngine(Engine):
             a["dgrad_part"] = (a["acc_b"] if a.get("fin") is not None else
                                torch.zeros(plan["stats_T"], 2, bn.out.shape[-1], device=self.device))
             conv.attrs["bnred"] = bn
+
+    def _plan_bn_conv_fold(self):
+        """BN -> ReLU -> Conv2D with the conv as the ReLU output's only consumer and a direct
+        3x3 forward plan (the second conv of every ResNet basic block on layers 1-3): the conv
+        reads the BN INPUT, finalizes the statistics and applies BN + ReLU to its staged halo
+        in LDS, and stores y for the weight gradient -- the bn_apply launch (a read of x and a
+        write of y) disappears.  Needs the in-consumer finalize (bn_acc).  DAMD_BN_CONV_FOLD=0
+        keeps the apply launch."""
+        if self.bn_acc is None or not env.get_bool("DAMD_BN_CONV_FOLD", True):
+            return
+        for bn in self.nodes:
+            a = bn.attrs
+            if (bn.kind != "BatchNormalization" or a.get("dead") or not a.get("relu") or a.get("stats_only")
+                    or a.get("pool") is not None or a.get("fin") is None or not a.get("stats_from_conv")):
+                continue
+            outs = bn.out.consumers
+            if len(outs) != 1 or not outs[0].attrs.get("dead") or len(outs[0].out.consumers) != 1:
+                continue
+            conv = outs[0].out.consumers[0]
+            if (conv.kind != "Conv2D" or conv.attrs.get("dead") or "w_pad" in conv.attrs or conv.attrs.get("stem4")
+                    or conv.inputs[0].root() is not bn.out.root()):
+                continue
+            l = conv.layer
+            plan = H.conv_fwd_plan(tuple(bn.out.shape), tuple(l.kernel.shape), l.strides, l.padding)
+            if plan["amode"] != H.A_CONV3 or plan["splits"] != 1:
+                continue
+            a["conv_fold"] = conv
+            conv.attrs["bnin"] = bn
 
     def _view_or_none(self, var):
         return self.views[id(var)] if var is not None else None
@@ -878,8 +907,14 @@ class NativeGraphEngine(Engine):
         else:
             if "w_pad" in nd.attrs:
                 wb = nd.attrs["w_pad"]
-            H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
-                       stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
+            bn = nd.attrs.get("bnin")
+            if bn is not None:  # BN -> ReLU of the input applied on load (_plan_bn_conv_fold)
+                H.conv_fwd(bn.inputs[0].root().buf, wb, nd.out.root().buf, l.strides, l.padding, bias=bias,
+                           relu=relu, stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws,
+                           bnin=(bn.attrs["fin"], x))
+            else:
+                H.conv_fwd(x, wb, nd.out.root().buf, l.strides, l.padding, bias=bias, relu=relu,
+                           stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
         self._act_epilogue(nd)
 
     def _pad_weights(self, nd):
@@ -923,8 +958,8 @@ class NativeGraphEngine(Engine):
                 self.C.bn_bwd_reduce_acc(x.buf.data_ptr(), 0, 0, x.buf.data_ptr(), self._ident(C).data_ptr(), 0,
                                          nd.attrs["acc_f"].data_ptr(), nd.attrs["T"], M, C, H.stream_handle(),
                                          H.acc_reps(nd.attrs["acc_f"]))
-            if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None:
-                return  # finalized and applied by the fused Add / MaxPool that consumes it
+            if nd.attrs.get("stats_only") or nd.attrs.get("pool") is not None or nd.attrs.get("conv_fold"):
+                return  # finalized and applied by the fused Add / MaxPool / direct conv that consumes it
             H.bn_apply_fin(x.buf, nd.out.root().buf, fin, relu=nd.attrs.get("relu", False))
             return
         if nd.attrs.get("stats_from_conv"):

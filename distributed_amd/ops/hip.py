@@ -265,13 +265,15 @@ def _stats_ptrs(stats):
 
 
 def gemm(A, B, C, *, amode, bmode, M, N, K, lda=0, ldb=0, ldc=0, epi=0, bias=None, stats=None, R=None,
-         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0, bnx=None, bnst=None):
+         geo: Sequence[int] = (), kc=0, splits=1, k_per_split=None, tile=None, kstep=0, bnx=None, bnst=None,
+         bnin=None):
     t = pick_tile(N) if tile is None else tile
     kps = k_per_split if k_per_split is not None else -(-K // BK) * BK
     sp, sa, reps = _stats_ptrs(stats)
+    bp, bv = bnin[0].args() if bnin is not None else ([], [])
     _C().gemm(amode, bmode, epi, splits, t, _ptr(A), _ptr(B), _ptr(C), _ptr(bias), sp, _ptr(R), M, N, K,
               lda, ldb, ldc, list(geo), kc, kps, stream_handle(), kstep, stats_acc=sa, bnx=_ptr(bnx), bnst=_ptr(bnst),
-              stats_reps=reps)
+              stats_reps=reps, bnin_p=bp, bnin_v=bv, bnin_y=_ptr(bnin[1]) if bnin is not None else 0)
 
 
 # ---- dense -------------------------------------------------------------------------------
@@ -525,9 +527,13 @@ def conv_fwd_plan(x_shape, w_shape, strides=(1, 1), padding="valid") -> dict:
 
 
 def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, stats=None,
-             workspace: Optional[torch.Tensor] = None):
+             workspace: Optional[torch.Tensor] = None, bnin=None):
     """out [N,Ho,Wo,Cout] = conv(x [N,H,W,Cin], w [KH,KW,Cin,Cout]); bf16 in/out.  stats
-    (BN batch statistics partials) must have conv_fwd_plan(...)["stats_T"] rows."""
+    (BN batch statistics partials) must have conv_fwd_plan(...)["stats_T"] rows.
+    bnin = (fin: BNFin, y): x is a BatchNorm's input and the conv runs on y = relu(BN(x)),
+    finalized and applied on load by the direct kernel (A_CONV3 plans only), which also
+    stores y (bitwise bn_apply_fin(x, y, fin, relu=True)) and publishes fin's st / moving
+    statistics."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(x.shape, w.shape, strides, padding)
     _chk(x, torch.bfloat16, "x")
     _chk(w, torch.bfloat16, "w")
@@ -538,11 +544,14 @@ def conv_fwd(x, w, out, strides=(1, 1), padding="valid", bias=None, relu=False, 
     M, K = plan["M"], plan["K"]
     _check_stats(stats, plan, cout, "conv_fwd")
     geo = (h, wd, cin, ho, wo, kh, kw, s, pad)
+    if bnin is not None and (plan["amode"] != A_CONV3 or plan["splits"] != 1 or bnin[0].acc is None
+                             or tuple(bnin[1].shape) != tuple(x.shape)):
+        raise ValueError("conv_fwd: a BN input needs a direct 3x3 plan and y of x's shape")
     if plan["splits"] == 1:
         epi = (E_BIAS if bias is not None else 0) | (E_RELU if relu else 0) | E_BF16 | \
             (E_STATS if stats is not None else 0)
         gemm(x, w, out, amode=plan["amode"], bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=epi,
-             bias=bias, stats=stats, geo=geo, tile=plan["tile"])
+             bias=bias, stats=stats, geo=geo, tile=plan["tile"], bnin=bnin)
         return
     ws = _workspace(workspace, plan["ws"], x.device)
     gemm(x, w, ws, amode=plan["amode"], bmode=B_NC, M=M, N=cout, K=K, ldb=cout, ldc=cout, epi=E_SLAB,

@@ -1,7 +1,7 @@
 """Direct 3x3 conv (conv3x3.hip) on the ResNet-18 shapes: kernel time (hipEvent over 50
 back-to-back launches) and per-block in-kernel phases from s_memrealtime stamps (start,
 first tap's operands landed, taps done, epilogue done), to see where a block's lifetime
-goes.  GPU box:  python scripts/conv3_probe.py [B]"""
+goes; forward also on a BatchNorm input (bnin).  GPU box:  python scripts/conv3_probe.py [B]"""
 import os
 import sys
 
@@ -63,6 +63,16 @@ for h, cin, cout in SHAPES:
     t = timeit(f)
     print(f"fwd  {h}x{h} {cin}->{cout}: {t:7.2f} us  {flop / t / 1e6:6.1f} TFLOP/s  plan {plan['amode']} tile {plan['tile']}")
     phases(f, 4096)
+    # the same conv on a BatchNorm's input (GemmArgs::bnin: finalize + BN/ReLU on load + y store)
+    acc = torch.zeros(8, 2 * cin, dtype=torch.float64, device=dev)
+    acc[0, cin:] = B * h * h
+    bst = torch.zeros(4, cin, device=dev)
+    fin = H.BNFin(acc, None, None, bst, None, None, B * h * h, 1e-3, 0.99)
+    yb = torch.empty_like(x)
+    fb = lambda: H.conv_fwd(x, w, y, (1, 1), "same", stats=st, bnin=(fin, yb))
+    t = timeit(fb)
+    print(f"fwd+bn {h}x{h} {cin}->{cout}: {t:7.2f} us  (BN input: finalize, normalise on load, store y)")
+    phases(fb, 4096)
     dy = torch.randn(B, h, h, cout, device=dev).bfloat16()
     dx = torch.empty_like(x)
     g = lambda: H.conv_dgrad(dy, w, dx, (1, 1), "same")

@@ -464,3 +464,46 @@ def test_direct_conv3_dgrad_bnred(H, monkeypatch, n, h, cin, cout):
     xhat = (x32 - st[0]) * st[1]
     close(part[:, 0].sum(0), dz.sum(0), 1e-3, 1e-4)
     close(part[:, 1].sum(0), (dz * xhat).sum(0), 1e-3, 1e-4)
+
+
+@pytest.mark.parametrize("n,h,cin,cout", [(2, 56, 64, 64), (2, 28, 128, 128), (2, 14, 256, 256), (2, 30, 128, 64)])
+@pytest.mark.parametrize("reps", [1, 8])
+def test_direct_conv3_bn_input(H, monkeypatch, n, h, cin, cout, reps):
+    """Direct forward conv on a BatchNorm's INPUT (GemmArgs::bnin: statistics finalized from
+    the fp64 accumulator replicas in the kernel, BN + ReLU applied to the staged halo) ==
+    bn_apply_fin + the plain direct conv, bitwise: the stored y, the conv output and its
+    statistics epilogue, the published st and the moving statistics; padding stays zero."""
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    shape = (n, h, h, cin)
+    assert H.conv_fwd_plan(shape, (3, 3, cin, cout), (1, 1), "same")["amode"] == H.A_CONV3
+    xb = rb(rnd(*shape, scale=2.0, seed=31) + 0.3).bfloat16()
+    wb = rb(rnd(3, 3, cin, cout, scale=0.05, seed=32)).bfloat16()
+    gamma, beta = rnd(cin, seed=33).abs() + 0.5, rnd(cin, seed=34) * 0.2
+    x64 = xb.double().reshape(-1, cin)
+    sums = torch.cat([x64.sum(0), (x64 * x64).sum(0)])
+    acc = torch.zeros(reps, 2 * cin, dtype=torch.float64, device=dev)
+    for r in range(reps):  # split the sums over the replicas (the kernels add them in order)
+        acc[r] = sums * (0.5 ** (r + 1) if r < reps - 1 else 0.5 ** (reps - 1))
+    M = n * h * h
+    res = []
+    for fold in (True, False):
+        st = torch.zeros(4, cin, device=dev)
+        rm, rv = torch.zeros(cin, device=dev), torch.ones(cin, device=dev)
+        fin = H.BNFin(acc, gamma, beta, st, rm, rv, M, 1e-3, 0.99)
+        y = torch.full(shape, float("nan"), device=dev, dtype=torch.bfloat16)
+        out = torch.empty(n, h, h, cout, device=dev, dtype=torch.bfloat16)
+        ostat = torch.zeros(2 * cout, dtype=torch.float64, device=dev)
+        if fold:
+            H.conv_fwd(xb, wb, out, (1, 1), "same", stats=ostat, bnin=(fin, y))
+        else:
+            H.bn_apply_fin(xb, y, fin, relu=True)
+            H.conv_fwd(y, wb, out, (1, 1), "same", stats=ostat)
+        res.append((y, out, ostat, st, rm, rv))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    # and the values are BN -> ReLU of x (fp32 reference of the normalisation)
+    y = res[0][0].float().reshape(-1, cin)
+    mean = x64.mean(0)
+    var = (x64 * x64).mean(0) - mean * mean
+    ref_y = torch.relu((xb.float().reshape(-1, cin) - mean.float()) * torch.rsqrt(var.float() + 1e-3) * gamma + beta)
+    close(y, ref_y, 1e-2, 4e-3)

@@ -199,11 +199,12 @@ def test_small_resnet_step_matches_bf16_emulated_reference():
     one plain-SGD step every weight update must agree.
 
     A 1-ulp fp32 difference (summation order) flips some bf16 roundings and the BN-backward
-    cancellation amplifies them.  Bounds from a 16-init sweep (scripts/sweep_emulated_ref.py,
-    round 4): loss error <= 2.2e-3 relative, worst layer's relative update error <= 0.156,
-    median layer <= 0.098, worst layer cosine >= 0.990, head <= 9.2e-3, whole update vector
-    cosine >= 0.9946 / relative error <= 0.104 -- so any init passes the bounds below (three
-    unpinned inits per run); exact wiring checks are the bitwise fused-vs-unfused tests."""
+    cancellation amplifies them, mostly in the BN gamma / beta updates.  Init sweeps
+    (scripts/sweep_emulated_ref.py, round 4; 16 + 40 draws): loss error <= 2.2e-3 relative,
+    worst layer's relative update error <= 0.262 / cosine >= 0.966 (BN gamma / beta), median
+    layer <= 0.145, head <= 1.2e-2, whole update vector cosine >= 0.987 / relative error
+    <= 0.160 -- heavy tails, so the bounds below leave margin for any init (three fresh draws
+    per run); exact wiring checks are the bitwise fused-vs-unfused tests."""
     x, y = _data(32, (32, 32, 3), 10, seed=4)
     os.environ["DAMD_FUSED"] = "0"
     try:
@@ -233,14 +234,14 @@ def test_small_resnet_step_matches_bf16_emulated_reference():
                 nref = d_ref.norm().item()
                 rel = (d_native - d_ref).norm().item() / max(nref, 1e-12)
                 cos = float(d_native @ d_ref / max(d_native.norm().item() * nref, 1e-30))
-                assert cos > 0.97 and rel < 0.3, f"{v.name}: rel err {rel:.4f} cos {cos:.4f} (|d| {nref:.3e})"
+                assert cos > 0.93 and rel < 0.45, f"{v.name}: rel err {rel:.4f} cos {cos:.4f} (|d| {nref:.3e})"
                 rels.append(rel)
                 dn.append(d_native)
                 dr.append(d_ref)
-            assert sorted(rels)[len(rels) // 2] < 0.15, rels
-            assert rels[-2] < 2e-2, rels  # the head (predictions kernel): no BN below it
+            assert sorted(rels)[len(rels) // 2] < 0.25, rels
+            assert rels[-2] < 3e-2, rels  # the head (predictions kernel): no BN below it
             a, b = torch.cat(dn), torch.cat(dr)
-            assert float(a @ b / (a.norm() * b.norm())) > 0.99 and float((a - b).norm() / b.norm()) < 0.15
+            assert float(a @ b / (a.norm() * b.norm())) > 0.97 and float((a - b).norm() / b.norm()) < 0.3
     finally:
         os.environ.pop("DAMD_FUSED", None)
 
@@ -426,6 +427,31 @@ def test_bn_finalize_in_consumer_matches_finalize_kernels(monkeypatch, reps):
     for a, b in zip(w2, w3):
         np.testing.assert_array_equal(a, b)
     assert h2 == h3
+
+
+def test_bn_applied_inside_direct_conv_is_bitwise(monkeypatch):
+    """BN -> ReLU -> Conv2D with a direct 3x3 forward plan: the conv normalises its input on
+    load and stores the BN output for its weight gradient (DAMD_BN_CONV_FOLD, default) ==
+    the bn_apply launch + the plain conv, bitwise over two momentum steps."""
+    from distributed_amd.engine.native_graph import NativeGraphEngine
+
+    def build():
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    x, y = _data(64, (64, 64, 3), 10, seed=7)
+    tf.keras.backend.clear_session()
+    m = build()
+    m.compile(loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9))
+    e = m._get_engine(32, 32)
+    assert e.name == "native_graph" and sum(1 for nd in e.nodes if "bnin" in nd.attrs) >= 2
+    init = m.get_weights()
+    wf, hf, _ = _train(build, x, y, init, 32, 2, native=True, momentum=0.9)
+    wu, hu, _ = _train(build, x, y, init, 32, 2, native=True, momentum=0.9, extra_env={"DAMD_BN_CONV_FOLD": "0"})
+    for a, b in zip(wf, wu):
+        np.testing.assert_array_equal(a, b)
+    assert hf == hu
 
 
 def test_resnet18_full_size_trains():
