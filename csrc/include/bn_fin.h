@@ -24,21 +24,23 @@ __device__ inline void acc_sums(const double* acc, int reps, int C, int c, doubl
 __device__ inline void bn_fin_sums_gb(const BNFin& f, int C, int c, double s, double q, float g, float b, bool pub,
                                       float& m, float& inv, float& sc, float& sh) {
   const double mean = s / (double)f.count;
-  double var = q / (double)f.count - mean * mean;
+  // (every multiply-add written as an explicit fma: the compiler's contraction choices may
+  // differ between the kernels that inline this, and the moving statistics must not)
+  double var = fma(-mean, mean, q / (double)f.count);
   if (var < 0.0) var = 0.0;
   m = (float)mean;
   const float v = (float)var;
   inv = rsqrtf(v + f.eps);
   sc = g * inv;
-  sh = b - m * sc;
+  sh = fmaf(-m, sc, b);
   if (pub) {
     f.st[c] = m;
     f.st[C + c] = inv;
     f.st[2 * C + c] = sc;
     f.st[3 * C + c] = sh;
     if (f.rmean) {
-      f.rmean[c] = f.rmean[c] * f.mom + m * (1.f - f.mom);
-      f.rvar[c] = f.rvar[c] * f.mom + v * (1.f - f.mom);
+      f.rmean[c] = fmaf(f.rmean[c], f.mom, m * (1.f - f.mom));
+      f.rvar[c] = fmaf(f.rvar[c], f.mom, v * (1.f - f.mom));
     }
   }
 }

@@ -84,10 +84,14 @@ __device__ __forceinline__ void x_wait(const XArgs& xa, unsigned* f, unsigned e,
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
     __builtin_amdgcn_s_sleep(1);
-    if (__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+    if (dt > xa.timeout_ticks) {
       __hip_atomic_fetch_or(xa.status, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       break;
     }
+    // past 1 ms: give up at once when an earlier wait already expired (a broken exchange
+    // costs one deadline, not one per wait of every later step; the host raises on status)
+    if (dt > 100000ull && __hip_atomic_load(xa.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
   }
 }
 constexpr unsigned XW_SMALL = 1u << 8, XW_UNIT = 1u << 9, XW_PART = 1u << 10;  // status bits

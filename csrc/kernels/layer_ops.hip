@@ -158,7 +158,7 @@ __global__ __launch_bounds__(FT) void bn_finalize_k(const float* part, int T, in
   if (threadIdx.x >= 8) return;
   const int c = c0 + threadIdx.x;
   const double mean = sums[threadIdx.x] / count;
-  double var = sums[8 + threadIdx.x] / count - mean * mean;
+  double var = fma(-mean, mean, sums[8 + threadIdx.x] / count);  // (explicit fmas: as bn_fin.h)
   if (var < 0.0) var = 0.0;
   const float m = (float)mean, v = (float)var;
   const float inv = rsqrtf(v + eps);
@@ -167,10 +167,10 @@ __global__ __launch_bounds__(FT) void bn_finalize_k(const float* part, int T, in
   st[c] = m;
   st[C + c] = inv;
   st[2 * C + c] = sc;
-  st[3 * C + c] = b - m * sc;
+  st[3 * C + c] = fmaf(-m, sc, b);
   if (rmean) {
-    rmean[c] = rmean[c] * mom + m * (1.f - mom);
-    rvar[c] = rvar[c] * mom + v * (1.f - mom);
+    rmean[c] = fmaf(rmean[c], mom, m * (1.f - mom));
+    rvar[c] = fmaf(rvar[c], mom, v * (1.f - mom));
   }
 }
 
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(NT) void bn_infer_st_k(const float* __restrict__ rm
   st[c] = m;
   st[C + c] = inv;
   st[2 * C + c] = sc;
-  st[3 * C + c] = (beta ? beta[c] : 0.f) - m * sc;
+  st[3 * C + c] = fmaf(-m, sc, beta ? beta[c] : 0.f);
 }
 
 // logits rows of this step -> out[global row][K] (rows past the end of the data dropped);

@@ -44,10 +44,14 @@ __device__ __forceinline__ void wait_all(const PeerArgs& a, int phase, unsigned 
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
       __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+      const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t0;
+      if (dt > a.timeout_ticks) {
         __hip_atomic_fetch_or(a.status, 1u << phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
+      // past 1 ms: give up at once when an earlier wait already expired (a broken exchange
+      // then costs one deadline, not one per wait of every later call)
+      if (dt > 100000ull && __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
     }
   }
   __syncthreads();

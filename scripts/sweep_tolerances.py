@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
 
 import distributed_amd as tf  # noqa: E402
-from test_native_graph_gpu import _data, _mnist, _train  # noqa: E402
+from test_native_graph_gpu import _data, _mnist, _small_resnet, _train  # noqa: E402
 from test_native_layers_gpu import _opt_cases  # noqa: E402
 
 
@@ -37,6 +37,8 @@ def main():
     # (SGD lr 0.05 momentum 0.9 on its seed-1 data)
     cases = dict(_opt_cases(eps=1e-2), track=lambda: tf.keras.optimizers.SGD(learning_rate=0.05, momentum=0.9))
     xt, yt = _data(640, (28, 28, 1), 10, seed=1)
+    if names == ["resnet_fp32"]:
+        return sweep_resnet_fp32(seeds)
     for name in names:
         rows = []
         for s in range(seeds):
@@ -51,6 +53,35 @@ def main():
         a = np.array(rows)  # [seed][tensor][cos, rel]
         print(f"{name}: " + "  ".join(f"{nm} cos min {a[:, i, 0].min():.4f} med {np.median(a[:, i, 0]):.4f} "
                                       f"rel max {a[:, i, 1].max():.3f}" for i, nm in enumerate(names_w)), flush=True)
+
+
+def sweep_resnet_fp32(seeds):
+    """test_native_graph_gpu.py test_small_resnet_one_step_matches_fp32_reference: one SGD
+    step of the small ResNet, native graph engine (bf16 storage) vs the fp32 generic engine,
+    per tensor min cosine / max relative error and the whole-update-vector numbers."""
+    x, y = _data(64, (32, 32, 3), 10)
+    rows, whole = [], []
+    for s in range(seeds):
+        tf.set_seed(2000 + s)
+        tf.keras.backend.clear_session()
+        m0 = _small_resnet()
+        init = m0.get_weights()
+        names_w = [w.name for w in m0.weights]
+        wn, _, _ = _train(_small_resnet, x, y, init, 32, 1, native=True)
+        wr, _, _ = _train(_small_resnet, x, y, init, 32, 1, native=False, device="cpu")
+        rows.append(stats(init, wn, wr))
+        da = np.concatenate([(a - w0).ravel() for w0, a in zip(init, wn)]).astype(np.float64)
+        db = np.concatenate([(b - w0).ravel() for w0, b in zip(init, wr)]).astype(np.float64)
+        whole.append((float(da @ db / (np.linalg.norm(da) * np.linalg.norm(db))),
+                      float(np.linalg.norm(da - db) / np.linalg.norm(db))))
+        print(f"draw {s}: worst cos {min(c for c, _ in rows[-1]):.4f} worst rel {max(r for _, r in rows[-1]):.3f} "
+              f"whole cos {whole[-1][0]:.4f} rel {whole[-1][1]:.3f}", flush=True)
+    a = np.array(rows)
+    for i, nm in enumerate(names_w):
+        if np.isfinite(a[:, i, 0]).all():
+            print(f"{nm}: cos min {a[:, i, 0].min():.4f} rel max {a[:, i, 1].max():.3f}")
+    w = np.array(whole)
+    print(f"whole: cos min {w[:, 0].min():.4f} rel max {w[:, 1].max():.3f}")
 
 
 if __name__ == "__main__":

@@ -259,8 +259,18 @@ def test_small_resnet_one_step_matches_fp32_reference():
     # bf16 storage of pre-BN activations and gradients vs a pure fp32 run: the head is
     # tight, deep layers drift (|mean|/std of conv outputs amplifies bf16 rounding in
     # x-hat, and BN backward cancellation amplifies it again); wiring is checked
-    # exactly by the emulated-reference test above
-    _compare_updates(init, wn, wr, names, cos_min=0.93, rel_max=0.4)
+    # exactly by the emulated-reference test above.  Bounds by tensor class from a 16-draw
+    # init sweep (scripts/sweep_tolerances.py 16 resnet_fp32, round 4): BN gamma / beta worst
+    # cos 0.846 / rel 0.541 (heavy tail: BN-backward cancellation), conv / dense kernels worst
+    # cos 0.943 / rel 0.338, whole update vector worst cos 0.956 / rel 0.302
+    bn = [i for i, nm in enumerate(names) if "bn" in nm]
+    other = [i for i, nm in enumerate(names) if "bn" not in nm]
+    _compare_updates(init, wn, wr, [names[i] for i in bn], cos_min=0.75, rel_max=0.7, idx=bn)
+    _compare_updates(init, wn, wr, [names[i] for i in other], cos_min=0.9, rel_max=0.45, idx=other)
+    da = np.concatenate([(a - w0).ravel() for w0, a in zip(init, wn)]).astype(np.float64)
+    db = np.concatenate([(b - w0).ravel() for w0, b in zip(init, wr)]).astype(np.float64)
+    assert da @ db / (np.linalg.norm(da) * np.linalg.norm(db)) > 0.93
+    assert np.linalg.norm(da - db) / np.linalg.norm(db) < 0.4
 
 
 def test_mnist_native_graph_tracks_reference_over_steps():
@@ -412,7 +422,9 @@ def test_bn_finalize_in_consumer_matches_finalize_kernels(monkeypatch, reps):
     from distributed_amd.ops import hip as H
 
     def build():
-        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+        # two basic blocks on the 16x16x64 stage: two BN -> ReLU -> conv chains the direct
+        # kernel takes (the deeper stages' 8x8 / 4x4 tiles under-fill its MFMA rows)
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(2, 1, 1, 1))
 
     monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
     monkeypatch.setenv("DAMD_BN_REPS", reps)
@@ -441,7 +453,9 @@ def test_bn_applied_inside_direct_conv_is_bitwise(monkeypatch):
     from distributed_amd.engine.native_graph import NativeGraphEngine
 
     def build():
-        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+        # two basic blocks on the 16x16x64 stage: two BN -> ReLU -> conv chains the direct
+        # kernel takes (the deeper stages' 8x8 / 4x4 tiles under-fill its MFMA rows)
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(2, 1, 1, 1))
 
     monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
     x, y = _data(64, (64, 64, 3), 10, seed=7)
