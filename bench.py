@@ -43,7 +43,7 @@ def spawn_ranks(n: int, argv) -> int:
     if rc != 0 and "DAMD_ALLREDUCE" not in os.environ:
         print(f"bench.py: the {n}-rank run failed (exit {rc}); retrying with DAMD_ALLREDUCE=rccl",
               file=sys.stderr, flush=True)
-        rc, out = _spawn_once(n, argv, {"DAMD_ALLREDUCE": "rccl"})
+        rc, out = _spawn_once(n, argv, {"DAMD_ALLREDUCE": "rccl", "DAMD_RESTART_COUNT": "1"})
     if rc == 0:
         for line in out:
             print(line, end="", flush=True)

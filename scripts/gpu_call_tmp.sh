@@ -6,3 +6,4 @@ timeout -k 10 400 python -u -m pytest tests/test_peer_allreduce_gpu.py tests/tes
 [ $rc -le 1 ] || exit $rc
 bash scripts/prof_resnet.sh || exit 1
 bash scripts/prof_resnet_dp.sh || exit 1
+bash scripts/gpu_envprobe.sh || exit 1

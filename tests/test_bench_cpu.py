@@ -43,3 +43,15 @@ def test_bench_gang_fails_if_a_rank_fails():
                     {"DAMD_FAIL_AT": "1:0"}, timeout=300)
     assert r.returncode != 0
     assert not lines
+
+
+@pytest.mark.dist
+def test_bench_retries_a_failed_gang_once():
+    # rank 1 raises in the first attempt only (DAMD_FAIL_AT rank:step:attempt): the second
+    # attempt (exchange pinned to RCCL on a GPU node; no effect on CPU) completes, and the
+    # failed attempt prints no JSON line -- exactly one line for the job
+    r, lines = _run(["--gpus", "2", "--engine", "generic", "--steps", "3", "--warmup", "1"],
+                    {"DAMD_FAIL_AT": "1:0:0"}, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    assert "retrying with DAMD_ALLREDUCE=rccl" in r.stderr
