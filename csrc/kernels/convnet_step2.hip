@@ -943,7 +943,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 // =================================================================================
 // G / hconv: the reduced gradient (the peer all-reduce's `out` when it is folded into the
 // step, see ConvNetBuffers::Gr); hconv_w: the buffer bwd adds into (both parities cleared)
-__global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
+__global__ __launch_bounds__(1024) void flush(float* __restrict__ P, float* __restrict__ G, float* __restrict__ V,
                                              const float* __restrict__ W1alt, const float* __restrict__ V1alt,
                                              long long* __restrict__ hconv, const float* __restrict__ calt,
                                              long long* __restrict__ hacc, int B, int eager,
@@ -988,9 +988,12 @@ __global__ __launch_bounds__(256) void flush(float* __restrict__ P, float* __res
     G[OFF_LOSS] = G[OFF_CORR] = G[OFF_CNT] = 0.f;
   }
   __syncthreads();
+  // one block (eager world 1: 1,034 parameters): every read of the ctrl block is behind the
+  // barrier above, so no arrival ticket (a returning atomic costs the kernel ~1.5 us)
   if (threadIdx.x == 0) {
-    if (__hip_atomic_fetch_add(&ctrl->flush_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-        (int)gridDim.x - 1) {
+    if (gridDim.x == 1 ||
+        __hip_atomic_fetch_add(&ctrl->flush_ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            (int)gridDim.x - 1) {
       ctrl->wpar = 0;
       ctrl->pending = 0;
       ctrl->flush_ticket = 0;
@@ -1146,7 +1149,7 @@ hipError_t convnet2_launch_gather(const ConvNetBuffers& b, int PP, hipStream_t s
 }
 
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {
-  hipLaunchKernelGGL(convnet2::flush, dim3(eager2(b, B) ? 36 : 340), dim3(256), 0, st, b.P, b.Gr ? b.Gr : b.G, b.V,
+  hipLaunchKernelGGL(convnet2::flush, dim3(eager2(b, B) ? 1 : 340), dim3(eager2(b, B) ? 1024 : 256), 0, st, b.P, b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.hconv_r ? b.hconv_r : b.hconv, b.calt, b.hacc, B, eager2(b, B), b.w1bf, b.ctrl,
                      b.hconv);
   return hipGetLastError();

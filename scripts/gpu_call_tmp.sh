@@ -1,9 +1,14 @@
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 360 python -u scripts/diag_fold.py > gpurun_out/diag_fold.log 2>&1; echo "diag rc=$?"; grep -v INFO gpurun_out/diag_fold.log | tail -20
-timeout -k 10 400 python -u -m pytest tests/test_peer_allreduce_gpu.py tests/test_sharded_inproc_gpu.py -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/t_peer.log 2>&1; rc=$?; echo "peer tests rc=$rc"; tail -3 gpurun_out/t_peer.log
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest_gpu rc=$rc"; grep -E "^(FAILED|ERROR)" gpurun_out/pytest_gpu.log; tail -2 gpurun_out/pytest_gpu.log
 [ $rc -le 1 ] || exit $rc
+timeout -k 10 300 python -u __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/smoke.log; exit 1; }
+echo smoke ok
+timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_driver.log 2>&1 || exit 1
+tail -1 gpurun_out/bench_driver.log
 bash scripts/prof_resnet.sh || exit 1
 bash scripts/prof_resnet_dp.sh || exit 1
+sed -i 's/^for r in 1 2; do/for r in 1; do/' scripts/gpu_envprobe.sh
 bash scripts/gpu_envprobe.sh || exit 1
