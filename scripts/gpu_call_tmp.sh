@@ -10,5 +10,4 @@ timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out
 tail -1 gpurun_out/bench_driver.log
 bash scripts/prof_resnet.sh || exit 1
 bash scripts/prof_resnet_dp.sh || exit 1
-sed -i 's/^for r in 1 2; do/for r in 1; do/' scripts/gpu_envprobe.sh
-bash scripts/gpu_envprobe.sh || exit 1
+REPS=1 bash scripts/gpu_envprobe.sh || exit 1
