@@ -304,6 +304,7 @@ PYBIND11_MODULE(_C, m) {
       .def("metric_tail", &ConvNetTrainer::metric_tail)
       .def("step", &ConvNetTrainer::step, py::call_guard<py::gil_scoped_release>())
       .def("capture", &ConvNetTrainer::capture)
+      .def("step_graph_nodes", &ConvNetTrainer::step_graph_nodes, py::arg("steps"))
       .def("run", &ConvNetTrainer::run, py::call_guard<py::gil_scoped_release>())
       .def("capture_final", &ConvNetTrainer::capture_final, py::arg("steps"))
       .def("run_final", &ConvNetTrainer::run_final, py::arg("steps"), py::call_guard<py::gil_scoped_release>())

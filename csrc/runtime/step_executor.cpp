@@ -63,6 +63,32 @@ hipGraphExec_t StepExecutor::capture_steps(int k, bool tail, hipGraph_t* keep) {
   return ge;
 }
 
+std::pair<int, int> StepExecutor::step_graph_nodes(int k) {
+  hipGraph_t g = nullptr;
+  HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  try {
+    for (int i = 0; i < k; ++i) enqueue_one_step();
+  } catch (...) {
+    hipStreamEndCapture(stream_, &g);
+    if (g) hipGraphDestroy(g);
+    throw;
+  }
+  HIP_CHECK(hipStreamEndCapture(stream_, &g));
+  size_t n = 0;
+  hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+  std::vector<hipGraphNode_t> nodes(n);
+  if (e == hipSuccess && n) e = hipGraphGetNodes(g, nodes.data(), &n);
+  int kern = 0;
+  for (size_t i = 0; e == hipSuccess && i < n; ++i) {
+    hipGraphNodeType t;
+    e = hipGraphNodeGetType(nodes[i], &t);
+    if (e == hipSuccess && t == hipGraphNodeTypeKernel) ++kern;
+  }
+  hipGraphDestroy(g);
+  HIP_CHECK(e);
+  return {kern, (int)n};
+}
+
 void StepExecutor::capture(int k) {
   if (k <= 0 || graphs_.count(k)) return;
   graphs_[k] = capture_steps(k, false);

@@ -8,6 +8,7 @@
 
 #include <functional>
 #include <map>
+#include <utility>
 #include <memory>
 
 #include "comm.h"
@@ -52,6 +53,9 @@ class StepExecutor {
   void restrict_cus(int part, int nparts);
   void invalidate_graphs();
   int num_graphs() const { return (int)graphs_.size(); }
+  // (kernel nodes, all nodes) of a k-step graph, captured and discarded: the launch contract
+  // of a step (e.g. two kernels per step at any world size for the fused MNIST trainer)
+  std::pair<int, int> step_graph_nodes(int k);
 
  protected:
   virtual void enqueue_one_step() = 0;

@@ -86,6 +86,9 @@ def _run(W, B, steps, gbf16, ppb, P0, X, Y, lr=0.1, mom=0.9):
             rk.t.set_sharded(peers[r], rk.hred.data_ptr(), int(gbf16))
             rk.t.restrict_cus(r, W)  # each rank's own CUs (as one GPU per rank would have)
         torch.cuda.synchronize(dev)
+    for rk in ranks:  # the launch contract: two kernels per step at every world size, no
+        # all-reduce launch (the exchange runs inside them), no copy / memset nodes
+        assert tuple(rk.t.step_graph_nodes(4)) == (8, 8), rk.t.step_graph_nodes(4)
     for _ in range(2):  # two epochs of `steps` steps, each ended by the flush
         for rk in ranks:
             rk.t.step(steps)  # enqueue only: every rank's step is in flight before any wait
