@@ -488,6 +488,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            unsigned long long* st, const float* __restrict__ Gr, const XArgs xa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
+  // (timing probe only, DAMD_PROBE_HCONV=1, wrong numerics: skips the conv-gradient atomics)
+  const int cprobe = eager >> 1;
+  eager &= 1;
   Stamps sts;
   stamp(sts, st, 0);
   const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x;
@@ -902,7 +905,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   lds_barrier();
   // this slice's conv-gradient partial, fixed order over the 16 thread groups, then a
   // 64-bit fixed-point atomic add (order-independent sum over the slices)
-  for (int i = tid; i < NCONV; i += 512) {
+  for (int i = tid; i < (cprobe ? 0 : NCONV); i += 512) {
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
@@ -1080,6 +1083,10 @@ static int probe_hacc() {
   const char* e = getenv("DAMD_PROBE_HACC");
   return e ? atoi(e) & 3 : 0;
 }
+static int probe_hconv() {
+  const char* e = getenv("DAMD_PROBE_HCONV");
+  return e ? atoi(e) & 1 : 0;
+}
 
 static XArgs xargs(const ConvNetBuffers& b) {
   if (b.xa) return *b.xa;
@@ -1110,12 +1117,14 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
+                       eager2(b, B) | (probe_hconv() << 1), b.P, b.V, b.w1bf,
+                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
                        xargs(b));
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf, b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
+                       eager2(b, B) | (probe_hconv() << 1), b.P, b.V, b.w1bf,
+                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
                        xargs(b));
 }
 
