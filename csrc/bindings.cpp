@@ -51,7 +51,6 @@ class ConvNetTrainer : public StepExecutor {
     b_.hconv = P_<long long>(g("hconv"));
     b_.calt = P_<float>(g("calt"));
     b_.ppb = bufs.contains("ppb") ? (int)g("ppb") : PP;
-    b_.cslab = bufs.contains("cslab") ? P_<float>(g("cslab")) : nullptr;
     if (b_.ppb < 1 || b_.ppb > 4) throw std::invalid_argument("bwd positions per slice must be in [1,4]");
     HIP_CHECK(convnet2_set_lds_limits());
   }

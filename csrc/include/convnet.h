@@ -62,9 +62,6 @@ struct ConvNetBuffers {
   // runs 4 image groups per slice (a 228-block grid at PP 3); the backward has one block per
   // slice, so a finer slicing spreads its dW1 / dP / conv-gradient work over more CUs
   int ppb;
-  // [NSB][320] fp32 conv-gradient partials, one row per backward slice (the eager world-1
-  // step: bwd stores, fwd / flush sum in a fixed order instead of int64 atomics); may be null
-  float* cslab;
 };
 constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;

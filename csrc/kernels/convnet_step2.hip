@@ -104,33 +104,6 @@ __device__ __forceinline__ float4 unpack_bf16x4(uint2 q) {
                      bf2f((uint16_t)(q.y >> 16)));
 }
 
-// Conv-gradient slab (world 1, eager step): backward block s stores its fp32 partial of
-// the 320 conv weight / bias gradients to row s of cslab[NSB][320] (plain stores: no
-// device-scope atomics whose completion the backward's end would wait for); the consumers
-// (next forward, flush) sum the rows in ONE fixed order -- row group g = r mod 6 in
-// ascending r, then the six group sums left to right -- so every consumer derives the same
-// bits.  (Multi-rank steps keep the int64 fixed-point hconv sums: exchanged exactly.)
-constexpr int SLAB_G = 6;
-__device__ __forceinline__ float slab_sum(const float* __restrict__ cslab, int nsb, int i) {
-  float p[SLAB_G];
-#pragma unroll
-  for (int g = 0; g < SLAB_G; ++g) {
-    p[g] = 0.f;
-    for (int r = g; r < nsb; r += SLAB_G) p[g] += cslab[r * NCONV + i];
-  }
-  float t = p[0];
-#pragma unroll
-  for (int g = 1; g < SLAB_G; ++g) t += p[g];
-  return t;
-}
-// bytes of the forward's LDS before the slab partials [SLAB_G][320]
-__host__ __device__ inline size_t fwd_lds_core(int PP, int lg) {
-  const int KP = kpitch(PP), IB = 1 << lg;
-  const size_t xsb = (size_t)IB * XR * IMG * 4, partb = (size_t)IB * HID * 4;
-  return (((xsb > partb ? xsb : partb) + (size_t)(IB + HID) * KP * 2 + NCONV * 4 + (size_t)IB * PP * 32 + 256 * 4) +
-          15) & ~(size_t)15;
-}
-
 // =================================================================================
 // fwd: grid (NS slices, IG image groups of IB = 2^lg images)
 // =================================================================================
@@ -145,7 +118,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
                                            long long* __restrict__ hacc, long long* __restrict__ hconv,
                                            float* __restrict__ calt, int B, int PP, int lg, int eager,
                                            unsigned long long* st, const long long* __restrict__ hconv_r,
-                                           const XArgs xa, const float* __restrict__ cslab, int nsb) {
+                                           const XArgs xa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
@@ -186,19 +159,6 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   const bool small_on = lin >= nblk - 2 && si >= 0 && si < NSMALL;
   const int sic = OFF_B1 + max(0, min(si, NSMALL - 1));
   const float sp = P[sic], sg0 = sh ? 0.f : G[sic], sv = V[sic];
-  // conv-gradient slab (world 1): thread t < 480 sums float4 column t % 80 over the rows
-  // r = t / 80 (mod 6) in ascending order -- the first 16 of them issued here, before the
-  // ctrl load (their addresses do not depend on it)
-  const bool slab = cslab != nullptr;
-  const int sq = tid % 80, sgp = tid / 80;
-  float4 sv4[16];
-  if (slab && sgp < SLAB_G) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int r = min(sgp + SLAB_G * k, nsb - 1);
-      sv4[k] = reinterpret_cast<const float4*>(cslab + r * NCONV)[sq];
-    }
-  }
   __builtin_amdgcn_sched_barrier(0);
 
   const Ctrl c = *ctrl;
@@ -311,52 +271,14 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     }
   };
   if (!sh) w1_update();
-  float* cpart = reinterpret_cast<float*>(smem + fwd_lds_core(PP, lg));  // [SLAB_G][320]
-  if (slab && sgp < SLAB_G) {
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      if (sgp + SLAB_G * k < nsb) {
-        a.x += sv4[k].x;
-        a.y += sv4[k].y;
-        a.z += sv4[k].z;
-        a.w += sv4[k].w;
-      }
-    }
-    for (int r = sgp + SLAB_G * 16; r < nsb; r += SLAB_G) {  // (more than 96 backward slices)
-      const float4 v = reinterpret_cast<const float4*>(cslab + r * NCONV)[sq];
-      a.x += v.x;
-      a.y += v.y;
-      a.z += v.z;
-      a.w += v.w;
-    }
-    reinterpret_cast<float4*>(cpart + sgp * NCONV)[sq] = a;
-  }
   float cwn = 0.f, cvn = 0.f;
-  auto conv_update = [&]() __attribute__((always_inline)) {
-    if (tid < NCONV) {
-      float g;
-      if (slab) {
-        g = cpart[tid];
-#pragma unroll
-        for (int q = 1; q < SLAB_G; ++q) g += cpart[q * NCONV + tid];
-      } else {
-        g = from_fix(cq, CINV);
-      }
-      sgd_or_keep(pend, cp, g, cv, c, cwn, cvn);
-      cw[tid] = cwn;
-      // the conv epilogue's ReLU (fmaxf) and the head's would turn a NaN parameter into 0:
-      // a non-finite conv / b1 / W2 / b2 value raises ctrl.bad (loss NaN) here instead
-      if (!__builtin_isfinite(cwn)) __hip_atomic_fetch_or(&ctrl->bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // the owner writes the next conv buffer and zeroes the hconv parity bwd adds into next
-    if (lin == 0 && tid < NCONV) {
-      (par ? P : calt)[tid] = cwn;
-      if (mom) (par ? V : calt + NCONV)[tid] = cvn;
-      hconv[par * NCONV + tid] = 0;
-    }
-  };
-  if (!slab) conv_update();
+  if (tid < NCONV) {
+    sgd_or_keep(pend, cp, from_fix(cq, CINV), cv, c, cwn, cvn);
+    cw[tid] = cwn;
+    // the conv epilogue's ReLU (fmaxf) and the head's would turn a NaN parameter into 0:
+    // a non-finite conv / b1 / W2 / b2 value raises ctrl.bad (loss NaN) here instead
+    if (!__builtin_isfinite(cwn)) __hip_atomic_fetch_or(&ctrl->bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (small_on) {
     float wn, vn;
     sgd_or_keep(pend, sp, sg, sv, c, wn, vn);
@@ -364,13 +286,15 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     if (mom) V[sic] = vn;
     if (!__builtin_isfinite(wn)) __hip_atomic_fetch_or(&ctrl->bad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  // the owner writes the next conv buffer and zeroes the hconv parity bwd adds into next
+  if (lin == 0 && tid < NCONV) {
+    (par ? P : calt)[tid] = cwn;
+    if (mom) (par ? V : calt + NCONV)[tid] = cvn;
+    hconv[par * NCONV + tid] = 0;
+  }
   stamp(sts, st, 1);
   x_store<U8>(xst, xs, lut);
   lds_barrier();
-  if (slab) {  // the slab partials are in LDS now
-    conv_update();
-    lds_barrier();
-  }
   stamp(sts, st, 2);
 
   ConvFrag cf;
@@ -561,8 +485,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
-                                           unsigned long long* st, const float* __restrict__ Gr, const XArgs xa,
-                                           float* __restrict__ cslab) {
+                                           unsigned long long* st, const float* __restrict__ Gr, const XArgs xa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   // (timing probe only, DAMD_PROBE_HCONV=1, wrong numerics: skips the conv-gradient atomics)
@@ -986,8 +909,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     float a = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += red[r * NCONV + i];
-    if (cslab) cslab[s * NCONV + i] = a;  // world 1: the slab row of this slice
-    else atomic_add_i64(hconv + par * NCONV + i, to_fix(a, CSCALE, &ctrl->bad));
+    atomic_add_i64(hconv + par * NCONV + i, to_fix(a, CSCALE, &ctrl->bad));
   }
   // ---- aux: new b1/W2/b2 gradient, metric tail ----
   if (aux_on && aq == 0) {
@@ -1029,8 +951,7 @@ __global__ __launch_bounds__(1024) void flush(float* __restrict__ P, float* __re
                                              long long* __restrict__ hconv, const float* __restrict__ calt,
                                              long long* __restrict__ hacc, int B, int eager,
                                              uint16_t* __restrict__ w1bf, Ctrl* __restrict__ ctrl,
-                                             long long* __restrict__ hconv_w, const float* __restrict__ cslab,
-                                             int nsb) {
+                                             long long* __restrict__ hconv_w) {
   const Ctrl c = *ctrl;
   const bool mom = c.momentum != 0.f, pend = c.pending != 0;
   // after a step's bwd: current W1 / conv parameters live in the alternates when wpar is
@@ -1045,7 +966,7 @@ __global__ __launch_bounds__(1024) void flush(float* __restrict__ P, float* __re
     const bool alt1 = !eager && c.wpar && w1, altc = c.wpar && i < NCONV;
     const float w = alt1 ? W1alt[i - OFF_W1] : (altc ? calt[i] : P[i]);
     const float v = alt1 ? V1alt[i - OFF_W1] : (altc ? calt[NCONV + i] : V[i]);
-    const float g = i < NCONV ? (cslab ? slab_sum(cslab, nsb, i) : from_fix(hg[i], CINV)) : G[i];
+    const float g = i < NCONV ? from_fix(hg[i], CINV) : G[i];
     float wn, vn;
     sgd_or_keep(pend && !(eager && w1), w, g, v, c, wn, vn);  // eager: W1 is already current
     P[i] = wn;
@@ -1140,7 +1061,9 @@ int convnet_f1_lg(int B) { return B <= 256 ? 4 : 6; }
 
 size_t convnet2_fwd_lds(int PP, int lg) {
   using namespace convnet;
-  return convnet2::fwd_lds_core(PP, lg) + (size_t)convnet2::SLAB_G * NCONV * 4;  // + the slab partials
+  const int KP = kpitch(PP), IB = 1 << lg;
+  const size_t xsb = (size_t)IB * XR * IMG * 4, partb = (size_t)IB * HID * 4;
+  return (xsb > partb ? xsb : partb) + (size_t)(IB + HID) * KP * 2 + NCONV * 4 + (size_t)IB * PP * 32 + 256 * 4;
 }
 size_t convnet2_bwd_lds(int PP) {
   using namespace convnet;
@@ -1171,10 +1094,6 @@ static XArgs xargs(const ConvNetBuffers& b) {
   return a;  // world 0: not sharded
 }
 
-static int ppb_of(const ConvNetBuffers& b, int PP) { return b.ppb > 0 ? b.ppb : PP; }
-// the conv-gradient slab is used by the eager (world-1, single-chunk) step only
-static float* cslab_of(const ConvNetBuffers& b, int B) { return eager2(b, B) && b.ppb > 0 ? b.cslab : nullptr; }
-
 template <bool U8>
 static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
   using namespace convnet;
@@ -1185,10 +1104,10 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
                      b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg,
                      eager2(b, B) | (probe_hacc() << 1), b.stamps,
-                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b), cslab_of(b, B),
-                     convnet_num_slices(ppb_of(b, PP)));
+                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b));
 }
 
+static int ppb_of(const ConvNetBuffers& b, int PP) { return b.ppb > 0 ? b.ppb : PP; }
 
 template <bool U8>
 static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st) {
@@ -1200,13 +1119,13 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B) | (probe_hconv() << 1), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b), cslab_of(b, B));
+                       xargs(b));
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B) | (probe_hconv() << 1), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b), cslab_of(b, B));
+                       xargs(b));
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
@@ -1241,7 +1160,7 @@ hipError_t convnet2_launch_gather(const ConvNetBuffers& b, int PP, hipStream_t s
 hipError_t convnet2_launch_flush(const ConvNetBuffers& b, int B, hipStream_t st) {
   hipLaunchKernelGGL(convnet2::flush, dim3(eager2(b, B) ? 1 : 340), dim3(eager2(b, B) ? 1024 : 256), 0, st, b.P, b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.hconv_r ? b.hconv_r : b.hconv, b.calt, b.hacc, B, eager2(b, B), b.w1bf, b.ctrl,
-                     b.hconv, cslab_of(b, B), convnet_num_slices(b.ppb > 0 ? b.ppb : 1));
+                     b.hconv);
   return hipGetLastError();
 }
 

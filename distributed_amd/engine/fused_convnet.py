@@ -148,14 +148,6 @@ class FusedConvNetEngine(Engine):
         # for the slice's masters)
         self.eager_w1 = self.world == 1 and not force_ar and B <= 64 and env.get_bool("DAMD_EAGER_W1", True)
         bufs["eager_w1"] = int(self.eager_w1)
-        # eager world-1 step: the backward stores its conv-gradient partials as fp32 slab rows
-        # (one per backward slice) that the next forward / flush sum in a fixed order, instead
-        # of int64 fixed-point atomics (whose completion ended the backward ~0.8 us later);
-        # DAMD_CONV_SLAB=1 (opt-in until measured on the GPU)
-        self.cslab = None
-        if self.eager_w1 and env.get_bool("DAMD_CONV_SLAB", False):
-            self.cslab = torch.zeros(C.convnet_num_slices(self.PPB) * NCONV, dtype=torch.float32, device=dev)
-            bufs["cslab"] = self.cslab.data_ptr()
         self.stamps = None
         if env.get_bool("DAMD_STAMPS", False):  # diagnostics: per-phase s_memrealtime stamps
             self.stamps = torch.zeros(3, 256, 16, dtype=torch.int64, device=dev)

@@ -354,9 +354,6 @@ def test_eager_w1_update_bitwise_equals_deferred(nesterov, monkeypatch):
     flush and a host-side set_weights (which must refresh the bf16 copy)."""
     _need_gpu()
     monkeypatch.setenv("DAMD_GRAPH_STEPS", "4")
-    # (the conv gradient as int64 fixed-point sums in both runs: the eager step's default
-    # fp32 slab sum is a different -- fixed -- summation, see the slab test below)
-    monkeypatch.setenv("DAMD_CONV_SLAB", "0")
     x, y = _data(1024)
     res = []
     for eager in ("1", "0"):
@@ -378,39 +375,6 @@ def test_eager_w1_update_bitwise_equals_deferred(nesterov, monkeypatch):
         res.append((np.concatenate([v.ravel() for v in m.get_weights()]), met0, met1))
     np.testing.assert_array_equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
-
-
-def test_conv_gradient_slab_matches_fixed_point_and_is_deterministic(monkeypatch):
-    """Eager world-1 step: the backward stores its conv-gradient partials as fp32 slab rows
-    summed by the next forward / the flush in one fixed order (DAMD_CONV_SLAB, default)
-    instead of int64 fixed-point atomics.  Two slab runs are bitwise identical (graph
-    replays, an epoch flush, a second epoch); against the fixed-point run only the
-    summation of the 320 conv gradients differs (fp32 vs exact), so weights and metrics agree
-    to fp32-rounding level."""
-    _need_gpu()
-    monkeypatch.setenv("DAMD_GRAPH_STEPS", "4")
-    x, y = _data(1024)
-    res = []
-    for slab in ("1", "1", "0"):
-        monkeypatch.setenv("DAMD_CONV_SLAB", slab)
-        m = _model(lr=0.05, momentum=0.9, seed=7)
-        eng = _engine(m, 64)
-        assert (eng.cslab is not None) == (slab == "1")
-        eng.bind(x, y)
-        eng.start_epoch(0, shuffle=True)
-        eng.run(9)
-        met0 = eng.end_epoch()
-        eng.start_epoch(1, shuffle=True)
-        eng.run(7)
-        met1 = eng.end_epoch()
-        eng.finish()
-        res.append((np.concatenate([v.ravel() for v in m.get_weights()]), met0, met1))
-    np.testing.assert_array_equal(res[0][0], res[1][0])
-    assert res[0][1] == res[1][1] and res[0][2] == res[1][2]
-    d = np.abs(res[0][0] - res[2][0])
-    print("slab vs fixed point: max |dw|", float(d.max()), "loss", res[0][2]["loss"], res[2][2]["loss"])
-    np.testing.assert_allclose(res[0][0], res[2][0], rtol=1e-4, atol=1e-5)
-    assert abs(res[0][2]["loss"] - res[2][2]["loss"]) < 1e-4 * abs(res[2][2]["loss"])
 
 
 def test_final_graph_equals_run_then_flush(monkeypatch):
