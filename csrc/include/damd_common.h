@@ -24,8 +24,20 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 }
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops, not for its
-// outstanding global stores (__syncthreads() also drains vmcnt, i.e. waits for every
-// prior global store to be acknowledged -- a full memory round trip per barrier).
+// outstanding global stores.  Neither does __syncthreads() on gfx950: its workgroup-scope
+// fence need not wait for vector-memory stores (the ISA shows a bare s_barrier after a
+// store loop), so a cross-device publish drains explicitly -- see damd_publish_drain().
+
+// Cross-device publish protocol (sharded exchange, peer all-reduce): the payload stores
+// go to uncached (MTYPE UC) staging; before the flag store that announces them, EVERY wave
+// that issued payload waits for its stores' acknowledgements (s_waitcnt vmcnt(0)).  The
+// markers below are assembly comments (no code): scripts/check_publish_isa.py reads them
+// from the device assembly to tell a workgroup publish (payload from all waves: the drain
+// must precede the workgroup barrier ahead of the flag) from a per-wave publish (the
+// wave's own drain must precede its flag).
+__device__ __forceinline__ void damd_publish_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+#define DAMD_PUBLISH_WG() asm volatile(";damd.publish wg")
+#define DAMD_PUBLISH_WAVE() asm volatile(";damd.publish wave")
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

@@ -39,9 +39,18 @@
 // Step counter / parity without intra-kernel races: fwd block 0 copies ctrl.cursor and
 // ctrl.wpar to cur2 / par2; bwd reads those and its block 0 advances cursor / iterations,
 // flips wpar and sets `pending`; no kernel uses a ctrl field that the same kernel writes.
-#include <cstdlib>
-
 #include "convnet_dev.h"
+
+// Timing probes (wrong numerics, never in a product build): a probe build compiles this
+// file with -DDAMD_PROBE_HACC=1|2 (skip all / half of the dense-1 atomics) or
+// -DDAMD_PROBE_HCONV=1 (skip the conv-gradient atomics); scripts/probe_build.py makes one
+// in a scratch directory.  The default build has both at 0, so the branches fold away.
+#ifndef DAMD_PROBE_HACC
+#define DAMD_PROBE_HACC 0
+#endif
+#ifndef DAMD_PROBE_HCONV
+#define DAMD_PROBE_HCONV 0
+#endif
 
 namespace damd {
 namespace convnet2 {
@@ -122,9 +131,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
-  // (timing probe only, DAMD_PROBE_HACC, wrong numerics: 1 skips the dense-1 atomics, 2 issues half)
-  const int hprobe = eager >> 1;
-  eager &= 1;
+  constexpr int hprobe = DAMD_PROBE_HACC;  // 0 in every product build (see the top of the file)
   const int nblk = gridDim.x * gridDim.y, lin = blockIdx.y * gridDim.x + s;
   Stamps sts;
   stamp(sts, st, 0);
@@ -392,7 +399,8 @@ __device__ __forceinline__ void exchange_tail(const XArgs& xa, Ctrl* ctrl, const
                                               int dm0, int lane, int tid, bool xown, int xo, int xu) {
   __shared__ int last_flag;
   const int NU = 4 * NS, W = xa.world, ps = xe & 1;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  damd_publish_drain();
+  DAMD_PUBLISH_WAVE();
   if (!xown && lane == 0) x_signal(x_pflag(xa.out[xo], xu, xa.rank * 2 + dm0), xe);
   // 2. ticket (counts forever: NS arrivals per step)
   __syncthreads();
@@ -410,7 +418,12 @@ __device__ __forceinline__ void exchange_tail(const XArgs& xa, Ctrl* ctrl, const
       const float v = i < SM_GRAD ? hc[i] : (i < SM_MET ? G[OFF_B1 + i - SM_GRAD] : G[OFF_LOSS + i - SM_MET]);
       for (int r = 0; r < W; ++r) x_small(xa.out[r], ps, xa.rank)[i] = v;
     }
-    __syncthreads();  // (drains every wave's stores)
+    // publish: EVERY wave drains its own small-message stores before the barrier (a
+    // workgroup barrier does not wait for outstanding vector-memory stores), then the
+    // flag -- the order scripts/check_publish_isa.py verifies on the gfx950 code object
+    damd_publish_drain();
+    __syncthreads();
+    DAMD_PUBLISH_WG();
     if (tid < W) x_signal(x_sflag(xa.out[tid], NU, ps, xa.rank), xe);
   }
   // 3. owners
@@ -468,7 +481,8 @@ __device__ __forceinline__ void exchange_tail(const XArgs& xa, Ctrl* ctrl, const
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    damd_publish_drain();
+    DAMD_PUBLISH_WAVE();
     if (lane < W) x_signal(x_gflag(xa.out[lane], NU, xu, dm0), xe);
   }
 }
@@ -488,9 +502,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            unsigned long long* st, const float* __restrict__ Gr, const XArgs xa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
-  // (timing probe only, DAMD_PROBE_HCONV=1, wrong numerics: skips the conv-gradient atomics)
-  const int cprobe = eager >> 1;
-  eager &= 1;
+  constexpr int cprobe = DAMD_PROBE_HCONV;  // 0 in every product build (see the top of the file)
   Stamps sts;
   stamp(sts, st, 0);
   const int s = blockIdx.x, tid = threadIdx.x, NS = gridDim.x;
@@ -1079,15 +1091,6 @@ size_t convnet2_bwd_lds(int PP) {
 // eager W1 update: world-1 runs with the single-chunk backward (B <= 64) only
 static int eager2(const ConvNetBuffers& b, int B) { return b.eager_w1 && B <= convnet::CH ? 1 : 0; }
 
-static int probe_hacc() {
-  const char* e = getenv("DAMD_PROBE_HACC");
-  return e ? atoi(e) & 3 : 0;
-}
-static int probe_hconv() {
-  const char* e = getenv("DAMD_PROBE_HCONV");
-  return e ? atoi(e) & 1 : 0;
-}
-
 static XArgs xargs(const ConvNetBuffers& b) {
   if (b.xa) return *b.xa;
   XArgs a{};
@@ -1103,7 +1106,7 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P,
                      b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg,
-                     eager2(b, B) | (probe_hacc() << 1), b.stamps,
+                     eager2(b, B), b.stamps,
                      b.hconv_r ? b.hconv_r : b.hconv, xargs(b));
 }
 
@@ -1117,13 +1120,13 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B) | (probe_hconv() << 1), b.P, b.V, b.w1bf,
+                       eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
                        xargs(b));
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B) | (probe_hconv() << 1), b.P, b.V, b.w1bf,
+                       eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
                        xargs(b));
 }

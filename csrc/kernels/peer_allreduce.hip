@@ -14,6 +14,7 @@
 //  - The local gradient itself is ordinary (cached) memory: it is only read and written
 //    by this device, in stream order with the kernels around this one.
 //  - Reductions are in a fixed peer order, so all ranks end bitwise identical.
+#include "damd_common.h"
 #include "peer_comm.h"
 
 namespace damd {
@@ -27,8 +28,9 @@ __device__ __forceinline__ unsigned* flag_slot(unsigned* base, int phase, int sr
 
 // thread 0: publish this block's phase to every rank (own flags included: uniform waits)
 __device__ __forceinline__ void signal_all(const PeerArgs& a, int phase, unsigned e) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's UC stores have landed
+  damd_publish_drain();  // this wave's UC stores have landed
   __syncthreads();
+  DAMD_PUBLISH_WG();
   if (threadIdx.x == 0) {
     for (int p = 0; p < a.world; ++p)
       __hip_atomic_store(flag_slot(a.flags[p], phase, a.rank, blockIdx.x), e, __ATOMIC_RELAXED,

@@ -56,17 +56,39 @@ def _run(cmd, verbose):
     return r.stdout
 
 
-def _build_C(verbose=False, jobs=None) -> Path:
-    out = PKG / f"_C{EXT}"
+def _common_flags(defines=()):
+    inc = ["-I", str(CSRC / "include"), "-I", str(CSRC / "runtime")]
+    for p in _pybind_includes():
+        inc += ["-I", p]
+    return ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-DNDEBUG"] + inc + [f"-D{d}" for d in defines]
+
+
+def hip_kernel_cmd(src: Path, obj: Path, defines=(), device_asm: bool = False):
+    """The hipcc line of one kernel source.  ``device_asm``: the gfx950 device assembly of
+    the very same compilation (``--cuda-device-only -S``) instead of the object -- what
+    scripts/check_publish_isa.py reads (it also checks that its instruction stream equals
+    the shipped object's)."""
+    # kernarg preloading: the first 16 argument dwords arrive in SGPRs, so a kernel's first
+    # dependent load does not wait on a kernarg-segment fetch (DAMD_KERNARG_PRELOAD=0 turns
+    # it off for A/B runs)
+    pre = ["-mllvm", "-amdgpu-kernarg-preload-count=16"] if os.environ.get("DAMD_KERNARG_PRELOAD", "1") != "0" else []
+    mode = ["--cuda-device-only", "-S"] if device_asm else ["-c"]
+    return [HIPCC, f"--offload-arch={ARCH}"] + mode + [str(src), "-o", str(obj)] + _common_flags(defines) + pre
+
+
+def _build_C(verbose=False, jobs=None, defines=(), out_dir: Path | None = None) -> Path:
+    """``defines``/``out_dir``: a diagnostic variant (e.g. the wrong-numerics timing probes
+    of convnet_step2.hip, scripts/probe_build.py) built into its own directory with its own
+    objects -- never over the product extension."""
+    if defines and out_dir is None:
+        raise ValueError("a build with extra defines needs its own out_dir")
+    out = (out_dir or PKG) / f"_C{EXT}"
     srcs = sorted((CSRC / "kernels").glob("*.hip")) + sorted((CSRC / "runtime").glob("*.cpp")) + [
         CSRC / "bindings.cpp",
         CSRC / "ops_bindings.cpp",
     ]
-    inc = ["-I", str(CSRC / "include"), "-I", str(CSRC / "runtime")]
-    for p in _pybind_includes():
-        inc += ["-I", p]
-    common = ["-O3", "-fPIC", "-std=c++17", "-Wno-unused-result", "-DNDEBUG"] + inc
-    objdir = BUILD / "obj"
+    common = _common_flags(defines)
+    objdir = (out_dir / "obj") if out_dir is not None else BUILD / "obj"
     objdir.mkdir(parents=True, exist_ok=True)
     hdrs = _headers()
     jobs_list = []
@@ -74,12 +96,7 @@ def _build_C(verbose=False, jobs=None) -> Path:
         o = objdir / (s.name + ".o")
         if _deps_newer(o, [s] + hdrs):
             if s.suffix == ".hip":
-                # kernarg preloading: the first 16 argument dwords arrive in SGPRs, so a
-                # kernel's first dependent load does not wait on a kernarg-segment fetch
-                # (DAMD_KERNARG_PRELOAD=0 turns it off for A/B runs)
-                pre = ["-mllvm", "-amdgpu-kernarg-preload-count=16"] if os.environ.get(
-                    "DAMD_KERNARG_PRELOAD", "1") != "0" else []
-                cmd = [HIPCC, f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)] + common + pre
+                cmd = hip_kernel_cmd(s, o, defines)
             else:
                 cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-c", str(s), "-o", str(o)] + common + [
                     "-fvisibility=hidden"
@@ -92,7 +109,7 @@ def _build_C(verbose=False, jobs=None) -> Path:
             list(ex.map(lambda c: _run(c, verbose), jobs_list))
     # relink also when the object SET changed (a source added or deleted): mtimes alone
     # would keep a deleted kernel file's object inside the library
-    manifest = BUILD / "C.objs"
+    manifest = (out_dir / "C.objs") if out_dir is not None else BUILD / "C.objs"
     listing = "\n".join(o.name for o in objs)
     if _deps_newer(out, objs) or not manifest.exists() or manifest.read_text() != listing:
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(out)] + [str(o) for o in objs] + [
