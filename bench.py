@@ -43,7 +43,10 @@ def spawn_ranks(n: int, argv) -> int:
     if rc != 0 and "DAMD_ALLREDUCE" not in os.environ:
         print(f"bench.py: the {n}-rank run failed (exit {rc}); retrying with DAMD_ALLREDUCE=rccl",
               file=sys.stderr, flush=True)
-        rc, out = _spawn_once(n, argv, {"DAMD_ALLREDUCE": "rccl", "DAMD_RESTART_COUNT": "1"})
+        # the JSON line of the retry names the failed first attempt ("fallback_from"), so a
+        # regression of the default transport stays visible in the record
+        rc, out = _spawn_once(n, argv, {"DAMD_ALLREDUCE": "rccl", "DAMD_RESTART_COUNT": "1",
+                                        "DAMD_BENCH_FALLBACK_FROM": f"gang-exit-{rc}"})
     if rc == 0:
         for line in out:
             print(line, end="", flush=True)
@@ -125,6 +128,13 @@ def main():
                          "all-reduce / optimizer) and add them to the JSON line as phases_ms")
     args = ap.parse_args()
 
+    probes = sorted(k for k in os.environ if k.startswith("DAMD_PROBE_"))
+    if probes:
+        # timing probes skip work inside the step (wrong numerics): a number measured with
+        # one is not a training step, so it never reaches a benchmark line
+        print(f"bench.py: refusing to run with timing-probe variables set ({', '.join(probes)})", file=sys.stderr)
+        sys.exit(2)
+
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and "TF_CONFIG" not in os.environ:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
@@ -159,53 +169,6 @@ def main():
     B = args.per_gpu_batch
     GB = B * n
 
-    if args.model == "mnist":
-        (x, y), _ = tf.keras.datasets.mnist.load_data()
-        x = x.reshape(len(x), 28, 28, 1) / 255.0
-        with strategy.scope():
-            model = tf.models.mnist_cnn()
-            tf.models.compile_reference(model, 0.001)
-    else:
-        rows = args.samples or max(4 * GB, 256)
-        rng = np.random.default_rng(1234)
-        x = (rng.integers(0, 256, size=(rows, 224, 224, 3), dtype=np.uint8) / np.float32(255.0)).astype(np.float32)
-        y = rng.integers(0, 1000, size=rows).astype(np.int64)
-        with strategy.scope():
-            model = tf.models.resnet18()
-            tf.models.compile_resnet(model, 0.1, 0.9)
-    engine = model._get_engine(B, GB)
-    engine.bind(x, y)
-    wrap = len(x) // GB
-    device_wrap = engine.name in ("fused_convnet", "native_graph")
-    if device_wrap:
-        engine.start_epoch(0, True, wrap_steps=wrap)
-    else:
-        engine.start_epoch(0, True)
-
-    def run(k):
-        # generic engine has no device-side wrap: restart epochs on the host
-        if not device_wrap:
-            while k > 0:
-                left = wrap - engine.step_in_epoch
-                if left <= 0:
-                    engine.start_epoch(1, True)
-                    left = wrap
-                d = min(k, left)
-                engine.run(d)
-                k -= d
-        else:
-            engine.run(k)
-
-    fail_at = runtime.fault_injection_step()  # DAMD_FAIL_AT=rank:step (launcher / gang tests)
-    if fail_at is not None and fail_at <= args.warmup:
-        raise RuntimeError(f"injected failure on rank {rt.rank} at step {fail_at} (DAMD_FAIL_AT)")
-    # build the replayed HIP graph(s) first: capture is setup, not part of a timed step
-    engine.prepare(max(args.steps, args.warmup))
-    # fused engine: the K timed steps and the final flush as one graph (setup, untimed)
-    final = (engine.name == "fused_convnet" and 0 < args.steps <= 64
-             and os.environ.get("DAMD_BENCH_FINAL_GRAPH", "1") != "0" and engine.prepare_final(args.steps))
-    run(args.warmup)
-    engine.sync()
     comm = strategy.communicator
     on_gpu = rt.device.type == "cuda"
 
@@ -217,29 +180,127 @@ def main():
         if on_gpu:
             torch.cuda.synchronize()
 
-    barrier()
-    device_sync()
-    t0 = time.perf_counter()
-    if final:
-        engine.run_and_flush(args.steps)  # K steps + the last deferred SGD update, one graph
+    if args.model == "mnist":
+        (x, y), _ = tf.keras.datasets.mnist.load_data()
+        x = x.reshape(len(x), 28, 28, 1) / 255.0
     else:
-        run(args.steps)
-        if engine.name == "fused_convnet":
-            engine._flush()  # the last deferred SGD update is part of the timed work
-    if not on_gpu:
-        engine.sync()
-    # on the GPU the device-wide synchronize waits for every stream, the engines' own
-    # (C++-created) step streams included: a second, engine-level host wait would only
-    # add a round trip to the timed window
-    device_sync()
-    barrier()
-    t1 = time.perf_counter()
-    dt = t1 - t0
-    if n > 1:
-        dts = comm.allgather_object(dt)
-        dt = max(dts)
+        rows = args.samples or max(4 * GB, 256)
+        rng = np.random.default_rng(1234)
+        x = (rng.integers(0, 256, size=(rows, 224, 224, 3), dtype=np.uint8) / np.float32(255.0)).astype(np.float32)
+        y = rng.integers(0, 1000, size=rows).astype(np.int64)
+    wrap = len(x) // GB
+
+    def make_engine(transport=None):
+        """A fresh model (random init, broadcast from rank 0) and its engine; ``transport``
+        pins the fused engine's gradient exchange (DAMD_ALLREDUCE) for that engine only."""
+        old = os.environ.get("DAMD_ALLREDUCE")
+        if transport is not None:
+            os.environ["DAMD_ALLREDUCE"] = transport
+        try:
+            with strategy.scope():
+                if args.model == "mnist":
+                    model = tf.models.mnist_cnn()
+                    tf.models.compile_reference(model, 0.001)
+                else:
+                    model = tf.models.resnet18()
+                    tf.models.compile_resnet(model, 0.1, 0.9)
+            eng = model._get_engine(B, GB)
+        finally:
+            if transport is not None:
+                if old is None:
+                    os.environ.pop("DAMD_ALLREDUCE", None)
+                else:
+                    os.environ["DAMD_ALLREDUCE"] = old
+        eng.bind(x, y)
+        if eng.name in ("fused_convnet", "native_graph"):
+            eng.start_epoch(0, True, wrap_steps=wrap)
+        else:
+            eng.start_epoch(0, True)
+        return model, eng
+
+    def run(eng, k):
+        # generic engine has no device-side wrap: restart epochs on the host
+        if eng.name not in ("fused_convnet", "native_graph"):
+            while k > 0:
+                left = wrap - eng.step_in_epoch
+                if left <= 0:
+                    eng.start_epoch(1, True)
+                    left = wrap
+                d = min(k, left)
+                eng.run(d)
+                k -= d
+        else:
+            eng.run(k)
+
+    def timed(eng, k, final):
+        """Seconds for k full steps (the last deferred SGD update included), bracketed by a
+        barrier + device synchronize on both sides, max over ranks."""
+        barrier()
+        device_sync()
+        t0 = time.perf_counter()
+        if final:
+            eng.run_and_flush(k)  # K steps + the last deferred SGD update, one graph
+        else:
+            run(eng, k)
+            if eng.name == "fused_convnet":
+                eng._flush()  # the last deferred SGD update is part of the timed work
+        if not on_gpu:
+            eng.sync()
+        # on the GPU the device-wide synchronize waits for every stream, the engines' own
+        # (C++-created) step streams included: a second, engine-level host wait would only
+        # add a round trip to the timed window
+        device_sync()
+        barrier()
+        dt = time.perf_counter() - t0
+        return max(comm.allgather_object(dt)) if n > 1 else dt
+
+    fail_at = runtime.fault_injection_step()  # DAMD_FAIL_AT=rank:step (launcher / gang tests)
+    if fail_at is not None and fail_at <= args.warmup:
+        raise RuntimeError(f"injected failure on rank {rt.rank} at step {fail_at} (DAMD_FAIL_AT)")
+
+    # N > 1, fused engine, transport not pinned: every candidate gradient exchange (each
+    # self-tested at engine start, engine/xchg_selftest.py) runs warmup + K untimed-for-the-
+    # metric steps; the fastest carries the measured run.  This is also where BASELINE
+    # config 3's "RCCL ring all-reduce" gets its own number on the same ranks.
+    transports = {}
+    model, engine = None, None
+    tune = (n > 1 and args.model == "mnist" and args.engine in ("auto", "fused") and "DAMD_ALLREDUCE" not in os.environ
+            and os.environ.get("DAMD_BENCH_TUNE", "1") != "0" and args.steps > 0)
+    if tune:
+        best = None
+        for cand in ("sharded", "xgmi", "rccl"):
+            m_c, e_c = make_engine(cand)
+            kind = getattr(e_c, "allreduce_kind", cand)
+            if e_c.name != "fused_convnet" or kind in transports:
+                continue  # fell back onto a transport already measured
+            e_c.prepare(max(args.steps, args.warmup))
+            run(e_c, args.warmup)
+            e_c.sync()
+            dt_c = timed(e_c, args.steps, False)
+            transports[kind] = round(dt_c * 1e3 / args.steps, 5)
+            if best is None or dt_c < best[0]:
+                best = (dt_c, m_c, e_c)
+        model, engine = best[1], best[2]
+    else:
+        model, engine = make_engine()
+    # build the replayed HIP graph(s) first: capture is setup, not part of a timed step
+    engine.prepare(max(args.steps, args.warmup))
+    # fused engine: the K timed steps and the final flush as one graph (setup, untimed)
+    final = (engine.name == "fused_convnet" and 0 < args.steps <= 64
+             and os.environ.get("DAMD_BENCH_FINAL_GRAPH", "1") != "0" and engine.prepare_final(args.steps))
+    run(engine, args.warmup)
+    engine.sync()
+    dt = timed(engine, args.steps, final)
     phases = engine.phase_times(args.phases) if args.phases > 0 else None
     m = engine.metrics()
+    # MirrorCheck after the window: every rank holds bitwise the same parameters
+    mirrored = None
+    if n > 1 and hasattr(engine, "P"):
+        import hashlib
+
+        engine.sync()
+        dig = hashlib.sha1(engine.P.detach().cpu().numpy().tobytes()).hexdigest()
+        mirrored = len(set(comm.allgather_object(dig))) == 1
     ms = dt * 1e3 / args.steps
     value = GB * args.steps / dt
     if rt.rank == 0:
@@ -278,6 +339,21 @@ def main():
                                       or getattr(engine, "grad_bf16", False)) and n > 1 else "fp32"),
             "rccl_ranks": _rccl_ranks(comm),
         }
+        if n > 1:
+            ev = getattr(engine, "exchange_verified", None)
+            # the device exchange passed its start-up self-test (bitwise vs the host rank-order
+            # reduction) AND the replicas are bitwise mirrored after the window; None: the
+            # transport (RCCL / host) is not self-tested
+            out["exchange_verified"] = (bool(ev) and bool(mirrored)) if ev is not None else None
+            out["replicas_mirrored"] = mirrored
+            fb = list(getattr(engine, "exchange_fallback_from", []) or [])
+            if os.environ.get("DAMD_BENCH_FALLBACK_FROM"):
+                fb = [os.environ["DAMD_BENCH_FALLBACK_FROM"]] + fb
+            out["fallback_from"] = fb
+            if transports:
+                out["transport_ms_per_step"] = transports
+            out["rccl_ms_per_step"] = transports.get("rccl", round(dt * 1e3 / args.steps, 5)
+                                                     if getattr(engine, "allreduce_kind", "") == "rccl" else None)
         if phases is not None:
             out["phases_ms"] = {k: (round(v, 5) if isinstance(v, float) else v) for k, v in phases.items()}
         print(json.dumps(out), flush=True)

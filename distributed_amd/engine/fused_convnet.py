@@ -169,6 +169,10 @@ class FusedConvNetEngine(Engine):
         # Both peer modes need every rank to map every peer (one node); else RCCL.
         self.peer = None
         self.sharded = False
+        # start-up self-test outcome of the device exchange (None: no device exchange was
+        # self-tested -- world 1, RCCL or the host all-reduce) and the transports that failed it
+        self.exchange_verified = None
+        self.exchange_fallback_from: list = []
         self.hred = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)  # sharded: conv sums for flush
         mode = env.get_str("DAMD_ALLREDUCE", "auto").lower()
         if mode not in ("auto", "sharded", "xgmi", "rccl", "off"):
@@ -197,22 +201,50 @@ class FusedConvNetEngine(Engine):
                                             timeout_s=wd if wd > 0 else 60.0)
             if self.peer is None and mode in ("xgmi", "sharded"):
                 raise RuntimeError(f"DAMD_ALLREDUCE={mode} but the xGMI peer mapping is unavailable")
-            if self.peer is not None and want_sharded:
-                self.trainer.set_sharded(self.peer, self.hred.data_ptr(), int(self.grad_dtype == "bf16"))
-                self.sharded = True
+            if self.peer is not None:
                 # ranks sharing one device (the 1-GPU rehearsal of a multi-GPU run): each
                 # rank's step stream gets its own CUs -- the in-kernel waits of one rank must
                 # not hold the CUs another rank needs to publish what they wait for
-                ndev = max(1, torch.cuda.device_count())
-                share = [q for q in range(self.world) if q % ndev == (dev.index or 0)]
                 # (two ranks need no split: one rank's waiting forward leaves the other's
                 # 57-169-block backward enough CUs to finish -- measured 44.7 us/step shared
                 # vs 78 us with halved CUs; from three ranks on, the waiting forwards of two
                 # ranks can hold every CU)
-                if len(share) > 2 and env.get_bool("DAMD_SHARED_CU_SPLIT", True):
-                    self.trainer.restrict_cus(share.index(self.rank), len(share))
-                # every rank's flags are zero before any rank's first step writes into them
-                strategy.communicator.barrier()
+                ndev = max(1, torch.cuda.device_count())
+                share = [q for q in range(self.world) if q % ndev == (dev.index or 0)]
+                cu_split = ((share.index(self.rank), len(share))
+                            if len(share) > 2 and env.get_bool("DAMD_SHARED_CU_SPLIT", True) else None)
+                # start-up self-test of each candidate transport against the host rank-order
+                # reduction, bitwise, on every rank (engine/xchg_selftest.py); the first that
+                # passes carries the run: sharded -> xgmi -> RCCL
+                cands = (["xgmi-sharded"] if want_sharded else []) + ([] if mode == "sharded" else ["xgmi-peer"])
+                chosen = None
+                if env.get_bool("DAMD_XCHG_SELFTEST", True):
+                    from . import xchg_selftest
+
+                    for kind in cands:
+                        if xchg_selftest.verify(kind, C, strategy.communicator, self.peer, dev, B, self.PPB, self.PP,
+                                                self.P, gbf16=self.grad_dtype == "bf16" and kind == "xgmi-sharded",
+                                                cu_split=cu_split):
+                            chosen = kind
+                            self.exchange_verified = True
+                            break
+                        self.exchange_fallback_from.append(kind)
+                    self.peer.set_timeout(wd if wd > 0 else 60.0)
+                else:
+                    chosen = cands[0]
+                if chosen is None:
+                    if mode in ("xgmi", "sharded"):
+                        raise RuntimeError(f"DAMD_ALLREDUCE={mode}: the exchange failed its start-up self-test")
+                    dlog.warning("fused ConvNet engine: no xGMI exchange passed its self-test; using %s",
+                                 "RCCL" if native is not None else "the host (gloo) all-reduce")
+                    self.peer = None
+                elif chosen == "xgmi-sharded":
+                    self.trainer.set_sharded(self.peer, self.hred.data_ptr(), int(self.grad_dtype == "bf16"))
+                    self.sharded = True
+                    if cu_split is not None:
+                        self.trainer.restrict_cus(*cu_split)
+                    # every rank's flags are zero before any rank's first step writes into them
+                    strategy.communicator.barrier()
         if self.grad_dtype == "bf16" and not self.sharded:
             if self.world > 1:
                 dlog.warning("DAMD_GRAD_DTYPE=bf16 applies to the sharded exchange only; exchanging fp32")
@@ -413,6 +445,9 @@ class FusedConvNetEngine(Engine):
         c = self._ctrl_host()
         # the last step's reduced metric tail (in the peer `out` staging when folded)
         tail = list(self.trainer.metric_tail()) if self._pending else [0.0, 0.0, 0.0]
+        # metric_tail's gather waits (bounded) for every rank's last message: a wait that
+        # expired there leaves a stale tail -- never report it
+        self._check_peer()
         loss = _i2f(c[C_AL]) + tail[0]
         corr = _i2f(c[C_AC]) + tail[1]
         cnt = _i2f(c[C_AN]) + tail[2]

@@ -62,6 +62,8 @@ def main():
         json.dump({"history": h.history, "world": num_workers, "rank": rank,
                    "engine": getattr(eng, "name", None),
                    "exchange": getattr(eng, "allreduce_kind", None),
+                   "exchange_verified": getattr(eng, "exchange_verified", None),
+                   "fallback_from": list(getattr(eng, "exchange_fallback_from", []) or []),
                    "iterations": int(model.optimizer.iterations)}, f)
     if rank == 0:
         np.savez(os.path.join(out, "init0.npz"), *init)

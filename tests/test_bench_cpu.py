@@ -55,3 +55,14 @@ def test_bench_retries_a_failed_gang_once():
     assert r.returncode == 0, r.stderr[-3000:]
     assert len(lines) == 1, r.stdout
     assert "retrying with DAMD_ALLREDUCE=rccl" in r.stderr
+    out = json.loads(lines[0])
+    # the failed first attempt stays visible in the record
+    assert out["fallback_from"] == ["gang-exit-1"], out
+
+
+def test_bench_refuses_timing_probes():
+    """A DAMD_PROBE_* variable (wrong-numerics timing probe) must never yield a bench line."""
+    r, lines = _run(["--steps", "2", "--warmup", "1", "--engine", "generic"], {"DAMD_PROBE_HACC": "1"}, timeout=120)
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert not lines
+    assert "refusing" in r.stderr

@@ -41,45 +41,58 @@ def test_peer_allreduce_bitwise(tmp_path, world, blocks):
           "(ranks sharing one GPU)")
 
 
-@pytest.mark.parametrize("mode,world", [("xgmi", 2), ("sharded", 2)])
-@pytest.mark.timeout(600)
-def test_fused_trainer_over_peer_exchange_matches_single_rank(tmp_path, mode, world):
-    """world ranks x (64 / world) rows == 1 rank x 64 rows after 2 epochs x 8 momentum steps
-    (graph replays, an epoch flush in between); replicas bitwise mirrored and every rank's
-    History identical (reference README.md:229-231).  xgmi: the standalone peer all-reduce
-    kernel after bwd; sharded: the exchange inside the two step kernels (dW1 units reduced
-    by their owner rank, small gradients + metrics as one message per rank)."""
+def _fused_run(tmp_path, name, world, init=None, **kw):
     worker = os.path.join(ROOT, "tests", "helpers", "dist_worker.py")
-    d2 = tmp_path / "wN"
-    d2.mkdir()
-    per = 64 // world
-    res = launch.launch_script([worker], nproc=world, env=_env(d2, DAMD_ALLREDUCE=mode, DAMD_TEST_PER_REPLICA=per,
-                                                              DAMD_TEST_STEPS=8, DAMD_GRAPH_STEPS=5), timeout=400)
-    assert res.ok, res.returncodes
-    ws = []
-    for r in range(world):
-        w = [a for a in np.load(d2 / f"rank{r}.npz").values()]
-        j = json.load(open(d2 / f"rank{r}.json"))
-        assert j["engine"] == "fused_convnet"
-        assert j["exchange"] == ("xgmi-sharded" if mode == "sharded" else "xgmi-peer"), j["exchange"]
-        ws.append((w, j))
-    w0, j0 = ws[0]
-    for w, j in ws[1:]:
-        assert all(np.array_equal(a, b) for a, b in zip(w0, w))
-        assert j["history"] == j0["history"]
+    d = tmp_path / name
+    d.mkdir()
+    env = dict(DAMD_TEST_PER_REPLICA=64 // world, DAMD_TEST_STEPS=8, DAMD_GRAPH_STEPS=5, **kw)
+    if init is not None:
+        env["DAMD_TEST_INIT_FROM"] = init
+    res = launch.launch_script([worker], nproc=world, env=_env(d, **env), timeout=400)
+    assert res.ok, (name, res.returncodes)
+    runs = [([a for a in np.load(d / f"rank{r}.npz").values()], json.load(open(d / f"rank{r}.json")))
+            for r in range(world)]
+    w0, j0 = runs[0]
+    assert j0["engine"] == "fused_convnet"
+    for w, j in runs[1:]:  # mirrored replicas, identical History on every worker (README.md:229-231)
+        assert all(np.array_equal(a, b) for a, b in zip(w0, w)), f"{name}: replicas diverged"
+        assert j["history"] == j0["history"], name
     assert j0["iterations"] == 16
-    d1 = tmp_path / "w1"
-    d1.mkdir()
-    res = launch.launch_script([worker], nproc=1, env=_env(d1, DAMD_TEST_PER_REPLICA=64, DAMD_TEST_STEPS=8,
-                                                          DAMD_GRAPH_STEPS=5, DAMD_TEST_INIT_FROM=d2 / "init0.npz"),
-                               timeout=400)
-    assert res.ok, res.returncodes
-    w = [a for a in np.load(d1 / "rank0.npz").values()]
-    j1 = json.load(open(d1 / "rank0.json"))
+    return w0, j0, d
+
+
+@pytest.mark.timeout(900)
+def test_fused_exchanges_bitwise_equal_host_rank_order_reduction(tmp_path):
+    """W = 2, 2 epochs x 8 momentum steps (graph replays, an epoch flush in between): the
+    sharded exchange inside the step kernels, the standalone xGMI peer kernel, and the
+    sharded exchange made to FAIL its start-up self-test (injected) -- which must fall back
+    in process to the peer kernel before step 1 -- all end BITWISE equal (weights and
+    History) to the host-gloo all-reduce: at W = 2 every transport computes a + b."""
+    wh, jh, dh = _fused_run(tmp_path, "host", 2, DAMD_ALLREDUCE="off")
+    assert jh["exchange"] == "host-gloo" and jh["exchange_verified"] is None, jh
+    init = dh / "init0.npz"
+    cases = {"sharded": dict(DAMD_ALLREDUCE="sharded"),
+             "xgmi": dict(DAMD_ALLREDUCE="xgmi"),
+             "injected": dict(DAMD_ALLREDUCE="auto", DAMD_XCHG_SELFTEST_INJECT="xgmi-sharded:1")}
+    want = {"sharded": ("xgmi-sharded", []), "xgmi": ("xgmi-peer", []), "injected": ("xgmi-peer", ["xgmi-sharded"])}
+    for name, kw in cases.items():
+        w, j, _ = _fused_run(tmp_path, name, 2, init=init, **kw)
+        kind, fb = want[name]
+        assert j["exchange"] == kind and j["fallback_from"] == fb and j["exchange_verified"] is True, (name, j)
+        for i, (a, b) in enumerate(zip(w, wh)):
+            assert np.array_equal(a, b), (name, i, float(np.abs(a - b).max()))
+        assert j["history"] == jh["history"], (name, j["history"], jh["history"])
+
+
+@pytest.mark.timeout(600)
+def test_fused_sharded_exchange_matches_single_rank(tmp_path):
+    """world 2 x 32 rows == 1 rank x 64 rows (the same global batch), up to the grouping of
+    the per-row gradient sums."""
+    w0, j0, d2 = _fused_run(tmp_path, "wN", 2, DAMD_ALLREDUCE="sharded")
+    w, j1, _ = _fused_run(tmp_path, "w1", 1, init=d2 / "init0.npz")
     # the 16-step weight UPDATES agree: the two runs differ only in how the per-row
     # gradients are grouped before the fp32 sums, and that 1-ulp fp32 noise flips some bf16
-    # roundings of the activations, which the next steps carry on (absolute weight
-    # tolerances held for one init and not for others)
+    # roundings of the activations, which the next steps carry on
     init = [a for a in np.load(d2 / "init0.npz").values()]
     for i, (a, b, w_0) in enumerate(zip(w0, w, init)):
         da, db = (a - w_0).ravel().astype(np.float64), (b - w_0).ravel().astype(np.float64)
