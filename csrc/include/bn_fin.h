@@ -5,18 +5,34 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "damd_common.h"
 #include "layer_ops.h"
 
 namespace damd {
 
-// The replicas acc[r][2][C] are summed in replica order.
-__device__ inline void acc_sums(const double* acc, int reps, int C, int c, double& s, double& q) {
-  s = acc[c];
-  q = acc[C + c];
-  for (int r = 1; r < reps; ++r) {
-    s += acc[(size_t)r * 2 * C + c];
-    q += acc[(size_t)r * 2 * C + C + c];
+// Forward statistics: the replicas acc[r][2][C] (one word per value) summed as integers
+// (exact, any order), then decoded.
+__device__ inline void acc_sums(const long long* acc, int reps, int C, int c, double& s, double& q) {
+  long long ws = 0, wq = 0;
+  for (int r = 0; r < max(reps, 1); ++r) {
+    ws += acc[(size_t)r * 2 * C + c];
+    wq += acc[(size_t)r * 2 * C + C + c];
   }
+  s = bnacc_value1(ws);
+  q = bnacc_value1(wq);
+}
+// Backward sums: acc[r][2][C][2] (hi, lo words), the same way.
+__device__ inline void acc_sums2(const long long* acc, int reps, int C, int c, double& s, double& q) {
+  long long sh = 0, sl = 0, qh = 0, ql = 0;
+  for (int r = 0; r < max(reps, 1); ++r) {
+    const long long* a = acc + (size_t)r * 4 * C;
+    sh += a[2 * c];
+    sl += a[2 * c + 1];
+    qh += a[2 * (C + c)];
+    ql += a[2 * (C + c) + 1];
+  }
+  s = bnacc_value2(sh, sl);
+  q = bnacc_value2(qh, ql);
 }
 // coefficients of channel c (mean, invstd, scale, shift); pub: also published to st and
 // the moving statistics (one thread per channel of the whole grid)

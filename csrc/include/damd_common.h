@@ -36,6 +36,50 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
 // must precede the workgroup barrier ahead of the flag) from a per-wave publish (the
 // wave's own drain must precede its flag).
 __device__ __forceinline__ void damd_publish_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// ---- order-independent BatchNorm statistics accumulators (layer_ops.h BNFin) ----
+// Producer blocks add fp32 partials into shared accumulators with atomics; with fp64
+// atomics the rounding of each add depends on the arrival order.  Here every value is an
+// int64 fixed-point number (wrapping integer adds are associative and commutative, so a
+// sum is bitwise independent of the order in which the blocks arrive):
+//  * forward statistics (sum x, sum x^2; BNFin): ONE word, v rounded to a multiple of
+//    2^-24.  The rounding (<= 3e-8 per partial) is far below the fp32 partials' own and
+//    is divided by the element count (>= 64 x 7 x 7) before it meets eps = 1e-3.
+//    Range: |sum| < 2^35.
+//  * backward sums (sum dz, sum dz xhat; BNBwdFin -- gradients, ~1e-9 per element): TWO
+//    words, hi = floor(v 2^24), lo = floor((v 2^24 - hi) 2^40) in [0, 2^40): resolution
+//    2^-64, exact for |v| >= 2^-40; < 2^23 addends per lo word.
+// A non-finite or out-of-range partial adds a poison (+-2^58 to the hi word): the decoded
+// sum is NaN (a diverged run shows NaN statistics rather than wrapped ones).
+constexpr long long kBnAccPoison = 1LL << 58;
+__device__ __forceinline__ long long bnacc_hi_or_poison(float v, double& d) {
+  d = (double)v * 16777216.0;  // 2^24: exact
+  return fabsf(v) < 1073741824.f ? 0 : (v < 0.f ? -kBnAccPoison : kBnAccPoison);  // 2^30 (false for NaN)
+}
+__device__ __forceinline__ void bnacc_add1(long long* p, float v) {
+  double d;
+  long long w = bnacc_hi_or_poison(v, d);
+  if (w == 0) w = __double2ll_rn(d);
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)w);
+}
+__device__ __forceinline__ void bnacc_add2(long long* p, float v) {
+  double d;
+  long long hi = bnacc_hi_or_poison(v, d), lo = 0;
+  if (hi == 0) {
+    const double fh = floor(d);
+    hi = (long long)fh;
+    lo = (long long)((d - fh) * 1099511627776.0);  // [0, 1) x 2^40: exact, then floor
+  }
+  atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)hi);
+  if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(p + 1), (unsigned long long)lo);
+}
+__device__ __forceinline__ double bnacc_value1(long long w) {
+  if (w >= (kBnAccPoison >> 1) || w <= -(kBnAccPoison >> 1)) return __builtin_nan("");
+  return (double)w * 5.9604644775390625e-08;  // 2^-24
+}
+__device__ __forceinline__ double bnacc_value2(long long hi, long long lo) {
+  return bnacc_value1(hi) + (double)lo * 5.42101086242752217e-20;  // 2^-64
+}
+
 #define DAMD_PUBLISH_WG() asm volatile(";damd.publish wg")
 #define DAMD_PUBLISH_WAVE() asm volatile(";damd.publish wave")
 __device__ __forceinline__ void lds_barrier() {

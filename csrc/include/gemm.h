@@ -40,7 +40,7 @@ struct GemmArgs {
   int kc;              // B_KC: inner k length per tap
   int k_per_split;     // multiple of 32
   int kstep;           // conv_gemm.hip k-step depth: 32 | 64 (0: DAMD_CONV_KB / 64)
-  double* stats_acc;   // E_STATS: non-null -> the tile's column sum / sumsq are added (fp64
+  long long* stats_acc;  // E_STATS: non-null -> the tile's column sum / sumsq are added (bnacc_add
                        // atomics) into stats_acc[reps][2][N] instead of stored to `stats`:
   int stats_reps;      //   M-tile tm into replica tm % reps (0 / 1: one), see layer_ops.h BNFin
   const uint16_t* bnx; // E_BNRED: the BN input x [M][ldc] bf16 and its st [4][N] (mean,
@@ -83,7 +83,7 @@ hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipS
 // of rows_per_block rows: [ceil(M / rows_per_block)][2][N]
 hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
                          float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s,
-                         double* stats_acc = nullptr, int stats_reps = 1);
+                         long long* stats_acc = nullptr, int stats_reps = 1);
 // fp32 split-K epilogue (dense logits): out[m][n] = relu?(sum_s slab[s][m][n] + bias[n]),
 // slab [splits][M][N], out pitch ldc, fixed summation order
 hipError_t splitk_finish_f32(const float* slab, int splits, int M, int N, const float* bias, int relu, float* out,

@@ -206,9 +206,16 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       const int n = n0 + t;
       if (n < a.N) {
         if (a.stats_acc) {
-          double* acc = a.stats_acc + (size_t)(a.stats_reps > 1 ? tm % a.stats_reps : 0) * 2 * a.N;
-          unsafeAtomicAdd(acc + n, (double)s);
-          unsafeAtomicAdd(acc + a.N + n, (double)q);
+          const size_t rep = a.stats_reps > 1 ? tm % a.stats_reps : 0;
+          if constexpr (EPI & E_BNRED) {  // BN-backward sums: two words per value
+            long long* acc = a.stats_acc + rep * 4 * a.N;
+            bnacc_add2(acc + 2 * n, s);
+            bnacc_add2(acc + 2 * (a.N + n), q);
+          } else {  // forward statistics: one word per value
+            long long* acc = a.stats_acc + rep * 2 * a.N;
+            bnacc_add1(acc + n, s);
+            bnacc_add1(acc + a.N + n, q);
+          }
         } else {
           float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;
           st[n] = s;

@@ -12,16 +12,17 @@ struct Ctrl;  // kernels_api.h / damd_common.h
 // BatchNorm (training) ---------------------------------------------------------------
 // Batch statistics without a finalize launch: the producers (conv GEMM epilogue E_STATS
 // with GemmArgs::stats_acc, splitk_finish, bn_bwd_reduce / pool_bn_bwd_reduce with `acc`)
-// add their per-block fp32 partials into acc[reps][2][C] with fp64 atomics (exact for
-// partials within 2^29 of each other: arrival order does not change the sum in practice);
-// producer block / M-tile b adds into replica b % reps, so that same-address atomics --
+// add their per-block fp32 partials into acc[reps][2][C] as int64 fixed point (one word
+// per value forward, two backward: damd_common.h bnacc_add1 / bnacc_add2 -- integer
+// atomics, so the sums are bitwise independent of the blocks' arrival order); producer
+// block / M-tile b adds into replica b % reps, so that same-address atomics --
 // serialised at the memory side -- form reps short chains instead of one long one; the
 // consumer kernel (bn_apply, bn_relu_maxpool_fwd / bn_bwd_apply, pool_bn_bwd_apply)
 // derives the coefficients from acc (replicas summed in order) in its prologue (every
 // block, into LDS); its block 0 also writes st / co, the moving statistics and dgamma /
 // dbeta.  The accumulators are zeroed once per step (gather_batch's `zero` range).
 struct BNFin {
-  const double* acc;   // [reps][2][C] sum, sum of squares; null: the kernel reads st as before
+  const long long* acc;  // [reps][2][C] sum, sum of squares (bnacc_add1); null: the kernel reads st
   const float* gamma;  // may be null (1)
   const float* beta;   // may be null (0)
   float* st;           // [4][C] out (block 0): mean, invstd, scale, shift
@@ -31,7 +32,7 @@ struct BNFin {
   int reps;            // replicas of acc (0 / 1: one)
 };
 struct BNBwdFin {
-  const double* acc;   // [reps][2][C] sum dz, sum dz * xhat; null: the kernel reads co as before
+  const long long* acc;  // [reps][2][C][2 words] sum dz, sum dz * xhat (bnacc_add2); null: reads co
   float* dgamma;       // += (block 0), may be null
   float* dbeta;
   float* co;           // [3][C] out (block 0)
@@ -53,8 +54,10 @@ hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const
 // dz * xhat -> part [T][2][C]; optionally writes dz (bf16).  Returns T via *T_out.
 hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
                          const float* st, uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s,
-                         double* acc = nullptr, int acc_reps = 1);
+                         long long* acc = nullptr, int acc_reps = 1);
 int bn_bwd_blocks(long M, int C);
+// tests: bn_bwd_reduce launches its row ranges in reversed block order (order independence)
+void bn_reduce_reverse(bool on);
 // pass 2: dgamma/dbeta (accumulated into the gradient sinks, may be null) and the
 // coefficients co[3][C] so that dx = a*dz + b + c*xhat
 hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const float* st, const float* gamma,
@@ -75,7 +78,7 @@ hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H,
 // its backward: BN-backward partials / apply with the pool routing + ReLU mask recomputed
 hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                               int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                              float* part, int T, hipStream_t s, double* acc = nullptr, int acc_reps = 1);
+                              float* part, int T, hipStream_t s, long long* acc = nullptr, int acc_reps = 1);
 hipError_t pool_bn_bwd_apply(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                              int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
                              const float* co, uint16_t* dx, hipStream_t s, const BNBwdFin* bf = nullptr);

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
   const bool bnin = !DGRAD && a.bnin.acc != nullptr;
   float* sft = reinterpret_cast<float*>(smem + sft_off);
   constexpr int FR = 8;  // replicas held in registers (more: summed in pre())
-  double fs[FR], fq[FR];
+  long long fs[FR], fq[FR];  // fixed-point words (damd_common.h bnacc_add1)
   float fg = 1.f, fb = 0.f;
   if (bnin && t < SC) {
     if (a.bnin.gamma) fg = a.bnin.gamma[t];
@@ -269,14 +269,15 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
           double s, q;
           float m, inv, sc, sh;
           if (c == t && a.bnin.reps <= FR) {  // requested at kernel start
-            s = fs[0];
-            q = fq[0];
+            long long ws = fs[0], wq = fq[0];
 #pragma unroll
             for (int r = 1; r < FR; ++r)
               if (r < a.bnin.reps) {
-                s += fs[r];
-                q += fq[r];
+                ws += fs[r];
+                wq += fq[r];
               }
+            s = bnacc_value1(ws);
+            q = bnacc_value1(wq);
             bn_fin_sums_gb(a.bnin, SC, c, s, q, fg, fb, pub, m, inv, sc, sh);
           } else {
             acc_sums(a.bnin.acc, a.bnin.reps, SC, c, s, q);

@@ -532,7 +532,7 @@ __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__
 __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ slab, int S, int M, int N,
                                                       const float* __restrict__ bias, const uint16_t* R, int relu,
                                                       float* __restrict__ stats, int rb, uint16_t* out, int ldc,
-                                                      double* __restrict__ stats_acc, int reps) {
+                                                      long long* __restrict__ stats_acc, int reps) {
   __shared__ float red[2][NT * 8];
   // blockIdx.y: band of up to NT x 8 columns (wide layers: N > 2048)
   const int c0 = blockIdx.y * NT * 8, Nb = min(N - c0, NT * 8);
@@ -601,9 +601,9 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
       b += red[1][(q * cg + gg) * 8 + e];
     }
     if (stats_acc) {
-      double* acc = stats_acc + (size_t)(blockIdx.x % reps) * 2 * N;
-      unsafeAtomicAdd(acc + c0 + c, (double)a);
-      unsafeAtomicAdd(acc + N + c0 + c, (double)b);
+      long long* acc = stats_acc + (size_t)(blockIdx.x % reps) * 2 * N;  // forward statistics
+      bnacc_add1(acc + c0 + c, a);
+      bnacc_add1(acc + N + c0 + c, b);
     } else {
       stats[(size_t)blockIdx.x * 2 * N + c0 + c] = a;
       stats[(size_t)blockIdx.x * 2 * N + N + c0 + c] = b;
@@ -684,7 +684,7 @@ hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipS
 }
 
 hipError_t splitk_finish(const float* slab, int splits, int M, int N, const float* bias, const uint16_t* R, int relu,
-                         float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s, double* stats_acc,
+                         float* stats, int rows_per_block, uint16_t* out, int ldc, hipStream_t s, long long* stats_acc,
                          int stats_reps) {
   if (splits < 1 || N % 8 || ldc % 8 || rows_per_block < 1 || stats_reps < 1) return hipErrorInvalidValue;
   const int grid = (M + rows_per_block - 1) / rows_per_block;

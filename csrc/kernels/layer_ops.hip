@@ -130,19 +130,19 @@ __device__ __forceinline__ const float* bn_bwd_fin_prologue(const BNBwdFin& f, i
   if (f.acc == nullptr) return co;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     double a, b;
-    acc_sums(f.acc, f.reps, C, c, a, b);
+    acc_sums2(f.acc, f.reps, C, c, a, b);
     bn_bwd_fin_sums(f, C, c, a, b, st, blockIdx.x == 0, s[c], s[C + c], s[2 * C + c]);
   }
   __syncthreads();
   return s;
 }
 // per-block (fp32, fixed order) partial of channel ch -> replica blockIdx.x % reps of the
-// fp64 accumulator, or the partials row of this block
-__device__ __forceinline__ void put_partial(float* part, double* acc, int reps, int C, int ch, float a, float b) {
+// accumulator (order-independent fixed point), or the partials row of this block
+__device__ __forceinline__ void put_partial(float* part, long long* acc, int reps, int C, int ch, float a, float b) {
   if (acc) {
-    double* r = acc + (size_t)(blockIdx.x % reps) * 2 * C;
-    unsafeAtomicAdd(r + ch, (double)a);
-    unsafeAtomicAdd(r + C + ch, (double)b);
+    long long* r = acc + (size_t)(blockIdx.x % reps) * 4 * C;  // (backward sums: two words)
+    bnacc_add2(r + 2 * ch, a);
+    bnacc_add2(r + 2 * (C + ch), b);
   } else {
     part[(size_t)blockIdx.x * 2 * C + ch] = a;
     part[(size_t)blockIdx.x * 2 * C + C + ch] = b;
@@ -346,12 +346,15 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
                                                       int relu_mask, const uint16_t* __restrict__ x,
                                                       const float* __restrict__ st, uint16_t* __restrict__ dz_out,
                                                       float* __restrict__ part, long M, int C, long rows_per_block,
-                                                      double* __restrict__ acc, int reps) {
+                                                      long long* __restrict__ acc, int reps, int rev) {
   __shared__ float red[2][NT * 8];
   const int cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;  // rows per iteration
   const int g = t % cg, rr = t / cg;
   const int c = g * 8;
+  // rev (tests, bn_reduce_reverse): block b reduces the rows of block G-1-b -- the same
+  // partials, produced in a different order and added into different replicas
+  const long blk = rev ? (long)gridDim.x - 1 - blockIdx.x : blockIdx.x;
   float s0[8], s1[8], mean[8], inv[8], sc[8], sh[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
     ld8f(st + 2 * C + c, sc);
     ld8f(st + 3 * C + c, sh);
   }
-  const long r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const long r0 = blk * rows_per_block, r1 = min(M, r0 + rows_per_block);
   if (rr < rpi) {
     for (long row = r0 + rr; row < r1; row += rpi) {
       const long off = (row * C + c) / 8;
@@ -789,7 +792,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_k(const uint16_t* __res
                                                            const uint8_t* __restrict__ arg, PoolGeo g,
                                                            const uint16_t* __restrict__ x, const float* __restrict__ st,
                                                            float* __restrict__ part, long M, long rows_per_block,
-                                                           double* __restrict__ acc, int reps) {
+                                                           long long* __restrict__ acc, int reps) {
   __shared__ float red[2][NT * 8];
   const int C = g.C, cg = C / 8, t = threadIdx.x;
   const int rpi = NT / cg;
@@ -934,7 +937,7 @@ __global__ __launch_bounds__(NT) void pool_bn_bwd_reduce_q_k(const uint16_t* __r
                                                              const uint8_t* __restrict__ arg, PoolGeo g,
                                                              const uint16_t* __restrict__ x,
                                                              const float* __restrict__ st, float* __restrict__ part,
-                                                             long nquad, long quads_per_block, double* __restrict__ acc,
+                                                             long nquad, long quads_per_block, long long* __restrict__ acc,
                                                              int reps) {
   __shared__ float red[2][NT * 8];
   const int C = g.C, cg = C / 8, t = threadIdx.x;
@@ -1743,13 +1746,16 @@ int bn_bwd_blocks(long M, int C) {
   return (int)((M + rows - 1) / rows);
 }
 
+bool g_bn_reduce_reverse = false;
+void bn_reduce_reverse(bool on) { g_bn_reduce_reverse = on; }
+
 hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
-                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s, double* acc,
+                         uint16_t* dz_out, float* part, int T, long M, int C, hipStream_t s, long long* acc,
                          int acc_reps) {
   if (C % 8 || C / 8 > NT || (!part && !acc) || acc_reps < 1) return hipErrorInvalidValue;
   const long rows = (M + T - 1) / T;
   hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows,
-                     acc, acc_reps);
+                     acc, acc_reps, g_bn_reduce_reverse ? 1 : 0);
   return hipGetLastError();
 }
 
@@ -1816,7 +1822,7 @@ hipError_t bn_relu_maxpool_fwd(const uint16_t* x, const float* st, int N, int H,
 
 hipError_t pool_bn_bwd_reduce(const uint16_t* dpool, const uint8_t* arg, int N, int H, int W, int C, int ph, int pw,
                               int sh, int sw, int pad_t, int pad_l, int Ho, int Wo, const uint16_t* x, const float* st,
-                              float* part, int T, hipStream_t s, double* acc, int acc_reps) {
+                              float* part, int T, hipStream_t s, long long* acc, int acc_reps) {
   if (C % 8 || C / 8 > NT || (!part && !acc) || acc_reps < 1) return hipErrorInvalidValue;
   PoolGeo g{N, H, W, C, ph, pw, sh, sw, pad_t, pad_l, Ho, Wo};
   const long M = (long)N * H * W, rows = (M + T - 1) / T;

@@ -35,13 +35,13 @@ void register_kernel_ops(py::module_& m) {
         if (!bnin_p.empty()) {  // BN on the input (A_CONV3 forward): [acc, gamma, beta, st, rmean, rvar]
           if (bnin_p.size() != 6 || bnin_v.size() != 4)
             throw std::invalid_argument("bnin: 6 pointers + [count, eps, momentum, reps]");
-          a.bnin.acc = P_<const double>(bnin_p[0]); a.bnin.gamma = P_<const float>(bnin_p[1]);
+          a.bnin.acc = P_<const long long>(bnin_p[0]); a.bnin.gamma = P_<const float>(bnin_p[1]);
           a.bnin.beta = P_<const float>(bnin_p[2]); a.bnin.st = P_<float>(bnin_p[3]);
           a.bnin.rmean = P_<float>(bnin_p[4]); a.bnin.rvar = P_<float>(bnin_p[5]);
           a.bnin.count = bnin_v[0]; a.bnin.eps = bnin_v[1]; a.bnin.mom = bnin_v[2]; a.bnin.reps = (int)bnin_v[3];
           a.bnin_y = P_<uint16_t>(bnin_y);
         }
-        a.stats_acc = P_<double>(stats_acc);
+        a.stats_acc = P_<long long>(stats_acc);
         a.stats_reps = stats_reps;
         a.bnx = P_<const uint16_t>(bnx);
         a.bnst = P_<const float>(bnst);
@@ -90,7 +90,7 @@ void register_kernel_ops(py::module_& m) {
                             int stats_reps) {
     check(damd::splitk_finish(P_<const float>(slab), splits, M, N, P_<const float>(bias), P_<const uint16_t>(R), relu,
                               P_<float>(stats), rb, P_<uint16_t>(out), ldc, P_<ihipStream_t>(stream),
-                              P_<double>(stats_acc), stats_reps),
+                              P_<long long>(stats_acc), stats_reps),
           "splitk_finish");
   }, py::arg("slab"), py::arg("splits"), py::arg("M"), py::arg("N"), py::arg("bias"), py::arg("R"), py::arg("relu"),
      py::arg("stats"), py::arg("rb"), py::arg("out"), py::arg("ldc"), py::arg("stream"), py::arg("stats_acc") = 0,
@@ -142,7 +142,7 @@ void register_kernel_ops(py::module_& m) {
     damd::BNFin f{};
     if (p.empty()) return f;
     if (p.size() != 6 || v.size() != 4) throw std::invalid_argument("fin: 6 pointers + [count, eps, momentum, reps]");
-    f.acc = P_<const double>(p[0]); f.gamma = P_<const float>(p[1]); f.beta = P_<const float>(p[2]);
+    f.acc = P_<const long long>(p[0]); f.gamma = P_<const float>(p[1]); f.beta = P_<const float>(p[2]);
     f.st = P_<float>(p[3]); f.rmean = P_<float>(p[4]); f.rvar = P_<float>(p[5]);
     f.count = v[0]; f.eps = v[1]; f.mom = v[2]; f.reps = (int)v[3];
     return f;
@@ -150,7 +150,7 @@ void register_kernel_ops(py::module_& m) {
   auto mkbfin = [](const std::vector<U>& p, float count, int reps) {
     damd::BNBwdFin f{};
     if (p.size() != 4) throw std::invalid_argument("bfin: [acc, dgamma, dbeta, co]");
-    f.acc = P_<const double>(p[0]); f.dgamma = P_<float>(p[1]); f.dbeta = P_<float>(p[2]); f.co = P_<float>(p[3]);
+    f.acc = P_<const long long>(p[0]); f.dgamma = P_<float>(p[1]); f.dbeta = P_<float>(p[2]); f.co = P_<float>(p[3]);
     f.count = count;
     f.reps = reps;
     return f;
@@ -162,10 +162,11 @@ void register_kernel_ops(py::module_& m) {
                          P_<ihipStream_t>(s), &a, &b),
           "bn_apply_fin");
   });
+  m.def("bn_reduce_reverse", &damd::bn_reduce_reverse);
   m.def("bn_bwd_reduce_acc", [](U dy, U y, int relu_mask, U x, U st, U dz, U acc, int T, long M, int C, U s,
                                 int reps) {
     check(damd::bn_bwd_reduce(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x), P_<const float>(st),
-                              P_<u16>(dz), nullptr, T, M, C, P_<ihipStream_t>(s), P_<double>(acc), reps),
+                              P_<u16>(dz), nullptr, T, M, C, P_<ihipStream_t>(s), P_<long long>(acc), reps),
           "bn_bwd_reduce_acc");
   });
   m.def("bn_bwd_apply_fin", [mkbfin](U dy, U y, int relu_mask, U x, U st, U dx, long M, int C, std::vector<U> bp,
@@ -187,7 +188,7 @@ void register_kernel_ops(py::module_& m) {
     if (g.size() != 12) throw std::invalid_argument("pool geometry");
     check(damd::pool_bn_bwd_reduce(P_<const u16>(dpool), P_<const uint8_t>(arg), g[0], g[1], g[2], g[3], g[4], g[5],
                                    g[6], g[7], g[8], g[9], g[10], g[11], P_<const u16>(x), P_<const float>(st),
-                                   nullptr, T, P_<ihipStream_t>(s), P_<double>(acc), reps),
+                                   nullptr, T, P_<ihipStream_t>(s), P_<long long>(acc), reps),
           "pool_bn_bwd_reduce_acc");
   });
   m.def("pool_bn_bwd_apply_fin", [mkbfin](U dpool, U arg, std::vector<int> g, U x, U st, U dx, std::vector<U> bp,

@@ -137,7 +137,8 @@ class NativeGraphEngine(Engine):
                  "AveragePooling2D", "GlobalAveragePooling2D", "Flatten", "Dense", "Dropout")
     ACTIVATIONS = ("linear", "relu", "sigmoid", "tanh")
     _weights_static = False  # True for an inference plan: padded weight copies made once per call
-    # DAMD_BN_FIN (default on): BatchNorm statistics through fp64 accumulators finalized
+    # DAMD_BN_FIN (default on): BatchNorm statistics through int64 fixed-point accumulators
+    # (order-independent: bitwise the same sums whatever order the producer blocks arrive in) finalized
     # inside the consumer kernels (ops/hip.py BNFin): 40 fewer launches per ResNet-18 step.
     # Same-address fp64 atomics serialise at the memory side (~18 ns each: with one
     # accumulator bn_bwd_reduce took 8.6 -> 26 us, the step 3.02 ms), so the producers add
@@ -561,7 +562,7 @@ class NativeGraphEngine(Engine):
         self.act_bytes = nbytes
 
     def _plan_bn_fin(self):
-        """fp64 statistics accumulators of every BatchNorm ([2][C] forward sums, [2][C]
+        """Fixed-point statistics accumulators of every BatchNorm ([2][C] forward sums, [2][C]
         backward sums) in one buffer, cleared by the step's gather_batch launch; the conv
         producing a BN input accumulates into it from its epilogue."""
         bns = [nd for nd in self.nodes if nd.kind == "BatchNormalization" and not nd.attrs.get("dead")]
@@ -571,14 +572,16 @@ class NativeGraphEngine(Engine):
         if not use or not bns:
             return
         R = max(1, env.get_int("DAMD_BN_REPS", 8))
-        tot = sum(4 * R * nd.out.shape[-1] for nd in bns)
-        self.bn_acc = torch.zeros(tot, dtype=torch.float64, device=self.device)
+        # int64 fixed point (ops/hip.py bn_acc_encode): forward [R][2C] one word per value,
+        # backward [R][4C] two words per value
+        tot = sum(6 * R * nd.out.shape[-1] for nd in bns)
+        self.bn_acc = torch.zeros(tot, dtype=torch.int64, device=self.device)
         o = 0
         for nd in bns:
             C = nd.out.shape[-1]
             nd.attrs["acc_f"] = self.bn_acc[o:o + 2 * C * R].view(R, 2 * C)
-            nd.attrs["acc_b"] = self.bn_acc[o + 2 * C * R:o + 4 * C * R].view(R, 2 * C)
-            o += 4 * C * R
+            nd.attrs["acc_b"] = self.bn_acc[o + 2 * C * R:o + 6 * C * R].view(R, 4 * C)
+            o += 6 * C * R
             if nd.attrs.get("stats_from_conv"):
                 self._producer(nd.inputs[0]).attrs["stats_buf"] = nd.attrs["acc_f"]
             l = nd.layer
@@ -609,7 +612,7 @@ class NativeGraphEngine(Engine):
             plan = H.conv_dgrad_plan(bn.out.shape, tuple(l.kernel.shape), l.strides, l.padding)
             if plan["amode"] != H.A_DGRAD3:
                 continue
-            # with the in-consumer finalize the epilogue adds into the fp64 accumulator
+            # with the in-consumer finalize the epilogue adds into the fixed-point accumulator
             a["dgrad_part"] = (a["acc_b"] if a.get("fin") is not None else
                                torch.zeros(plan["stats_T"], 2, bn.out.shape[-1], device=self.device))
             conv.attrs["bnred"] = bn

@@ -248,18 +248,51 @@ def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=(), ac
 
 
 def acc_reps(acc):
-    """Replica count of an fp64 BatchNorm accumulator: [reps][2][C] (2-D [reps, 2C]) or a
-    single [2][C] (1-D).  Producer block b adds into replica b % reps (layer_ops.h BNFin)."""
+    """Replica count of a BatchNorm statistics accumulator (int64 fixed point, layer_ops.h
+    BNFin): [reps, 2C] forward / [reps, 4C] backward (2-D) or a single replica (1-D).
+    Producer block b adds into replica b % reps."""
     return int(acc.shape[0]) if acc is not None and acc.dim() == 2 else 1
 
 
+# Fixed-point BatchNorm accumulators (csrc/include/damd_common.h bnacc_add1 / bnacc_add2):
+# integer atomics, so the statistics are bitwise independent of the producer blocks'
+# arrival order.  Forward sums: one int64 word per value (unit 2^-24); backward sums: two
+# (hi = floor(v 2^24), lo = floor((v 2^24 - hi) 2^40)).
+ACC_UNIT = 2.0 ** -24
+
+
+def bn_acc_encode(values: torch.Tensor, words: int = 1) -> torch.Tensor:
+    """Host encoding of fp64 sums into accumulator words (tests / diagnostics): [..., K]
+    doubles -> [..., K] (words 1) or [..., 2K] (words 2, (hi, lo) interleaved) int64."""
+    v = values.double().cpu()
+    if words == 1:
+        return torch.round(v * 2.0 ** 24).to(torch.int64)
+    d = v * 2.0 ** 24
+    hi = torch.floor(d)
+    lo = torch.floor((d - hi) * 2.0 ** 40)
+    return torch.stack([hi.to(torch.int64), lo.to(torch.int64)], -1).reshape(*v.shape[:-1], 2 * v.shape[-1])
+
+
+def bn_acc_decode(acc: torch.Tensor, words: int = 1) -> torch.Tensor:
+    """Replica-summed values of an accumulator ([reps, K * words] or [K * words]) as fp64."""
+    a = acc.cpu()
+    if a.dim() == 1:
+        a = a.unsqueeze(0)
+    a = a.sum(0)
+    if words == 1:
+        return a.double() * ACC_UNIT
+    a = a.view(-1, 2)
+    return a[:, 0].double() * ACC_UNIT + a[:, 1].double() * 2.0 ** -64
+
+
 def _stats_ptrs(stats):
-    """(partials pointer, fp64 accumulator pointer, replicas) of a stats argument: an fp32
-    [T][2][N] partials tensor, or an fp64 [2][N] / [reps][2N] accumulator (BNFin: producers
-    add, the consumer finalizes)."""
+    """(partials pointer, accumulator pointer, replicas) of a stats argument: an fp32
+    [T][2][N] partials tensor, or an int64 fixed-point accumulator [2N] / [reps, 2N]
+    (forward) or [reps, 4N] (backward, E_BNRED) (BNFin: producers add, the consumer
+    finalizes)."""
     if stats is None:
         return 0, 0, 1
-    if stats.dtype == torch.float64:
+    if stats.dtype == torch.int64:
         return 0, _ptr(stats), acc_reps(stats)
     return _ptr(stats), 0, 1
 
@@ -431,9 +464,9 @@ def conv_fwd_stem4(x, w8, out, kernel_size, strides=(2, 2), padding="same", bias
 def _check_stats(stats, plan, cout, who):
     if stats is None:
         return
-    if stats.dtype == torch.float64:
+    if stats.dtype == torch.int64:
         if stats.numel() != 2 * cout * acc_reps(stats) or stats.shape[-1] != 2 * cout:
-            raise ValueError(f"{who}: an fp64 statistics accumulator is [reps][2 x {cout}], got {tuple(stats.shape)}")
+            raise ValueError(f"{who}: a statistics accumulator is int64 [reps][2 x {cout}], got {tuple(stats.shape)}")
     elif stats.shape[0] != plan["stats_T"]:
         raise ValueError(f"{who}: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
 
@@ -597,7 +630,7 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
     (x, st, part): dx is the gradient of relu(BN(x)) (BN coefficients st [4][Cin]); when the
     direct kernel runs (conv_dgrad_plan stats_T rows) it also writes the BN-backward
     partials (sum dz, sum dz * xhat per tile) into part [stats_T][2][Cin] (or adds them into
-    an fp64 accumulator [reps][2 Cin]), replacing
+    an int64 fixed-point accumulator [reps][4 Cin]: two words per value), replacing
     bn_bwd_reduce.  Returns True when it did."""
     n, h, wd, cin, ho, wo, kh, kw, s, pad, cout = conv_geo(dx.shape, w.shape, strides, padding)
     if s not in (1, 2):
@@ -612,8 +645,8 @@ def conv_dgrad(dy, w, dx, strides=(1, 1), padding="valid", accumulate=False,
     geo = (h, wd, cout, ho, wo, kh, kw, s, pad)
     if bnred is not None and plan["amode"] == A_DGRAD3 and not accumulate:
         bx, bst, part = bnred
-        fp64 = part.dtype == torch.float64  # an fp64 accumulator [reps][2 Cin] (BNBwdFin)
-        if ((part.shape[-1] != 2 * cin if fp64 else part.shape[0] != plan["stats_T"])
+        is_acc = part.dtype == torch.int64  # a fixed-point accumulator [reps][4 Cin] (BNBwdFin)
+        if ((part.shape[-1] != 4 * cin if is_acc else part.shape[0] != plan["stats_T"])
                 or tuple(bx.shape) != tuple(dx.shape)):
             raise ValueError("conv_dgrad: bnred partials / BN input do not match the plan")
         gemm(dy, w, dx, amode=A_DGRAD3, bmode=B_KC, M=M, N=cin, K=K, ldc=cin, epi=E_BF16 | E_BNRED, kc=cout,
@@ -730,9 +763,10 @@ def pool_bn_bwd(dpool, arg, x, st, part, co, dx, pool, strides, padding, dgamma=
 
 
 # ---- BatchNorm with the finalize folded into the consumer kernel (layer_ops.h BNFin) ------
-# The producers (conv / dense GEMM epilogue with an fp64 `stats` tensor, split-K finish,
-# bn_bwd_reduce with `acc`) add their per-block partials into an fp64 [2][C] accumulator
-# (or [reps, 2C]: block b into replica b % reps, summed in order by the consumer);
+# The producers (conv / dense GEMM epilogue with an int64 `stats` accumulator, split-K
+# finish, bn_bwd_reduce with `acc`) add their per-block partials into an int64 fixed-point
+# accumulator ([2C] / [reps, 2C] forward, [reps, 4C] backward: block b into replica
+# b % reps; integer sums, so the statistics do not depend on the blocks' arrival order);
 # the consumer derives the coefficients in its prologue, so neither bn_finalize nor
 # bn_bwd_finalize is launched.  The accumulators must be zero before the producers run
 # (the native graph engine clears them all in the step's gather_batch launch).
@@ -740,7 +774,7 @@ FIN_MAX_C = 4096
 
 
 class BNFin:
-    """Forward finalize parameters of one BatchNorm: fp64 accumulator acc [2][C] (sum,
+    """Forward finalize parameters of one BatchNorm: int64 accumulator acc [2][C] (sum,
     sum of squares of the BN input), gamma / beta (None: 1 / 0), st [4][C] written by the
     consumer's block 0 (mean, invstd, scale, shift), moving statistics (None: not
     updated), the element count per channel, epsilon and the moving-average momentum."""
@@ -768,8 +802,8 @@ def bn_apply_fin(x, y, fin: BNFin, relu=False, r=None, fin2: Optional[BNFin] = N
 
 
 def bn_bwd_fin(dy, y, relu_mask, x, st, acc, co, dx, dgamma=None, dbeta=None, dz_out=None, reduce=True):
-    """BN backward in two launches: bn_bwd_reduce adds sum(dz), sum(dz * xhat) into the fp64
-    accumulator acc [2][C] (reduce=False: a conv epilogue, E_BNRED, already did); bn_bwd_apply
+    """BN backward in two launches: bn_bwd_reduce adds sum(dz), sum(dz * xhat) into the int64
+    accumulator acc [reps][4C] (two words per value; reduce=False: a conv epilogue, E_BNRED, already did); bn_bwd_apply
     derives co, adds dgamma / dbeta (block 0) and writes dx."""
     C = x.shape[-1]
     M = x.numel() // C

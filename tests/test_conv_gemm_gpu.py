@@ -481,9 +481,9 @@ def test_direct_conv3_bn_input(H, monkeypatch, n, h, cin, cout, reps):
     gamma, beta = rnd(cin, seed=33).abs() + 0.5, rnd(cin, seed=34) * 0.2
     x64 = xb.double().reshape(-1, cin)
     sums = torch.cat([x64.sum(0), (x64 * x64).sum(0)])
-    acc = torch.zeros(reps, 2 * cin, dtype=torch.float64, device=dev)
-    for r in range(reps):  # split the sums over the replicas (the kernels add them in order)
-        acc[r] = sums * (0.5 ** (r + 1) if r < reps - 1 else 0.5 ** (reps - 1))
+    # split the sums over the replicas (the consumers add the replicas' integer words)
+    acc = torch.stack([H.bn_acc_encode(sums * (0.5 ** (r + 1) if r < reps - 1 else 0.5 ** (reps - 1)))
+                       for r in range(reps)]).to(dev)
     M = n * h * h
     res = []
     for fold in (True, False):
@@ -492,7 +492,7 @@ def test_direct_conv3_bn_input(H, monkeypatch, n, h, cin, cout, reps):
         fin = H.BNFin(acc, gamma, beta, st, rm, rv, M, 1e-3, 0.99)
         y = torch.full(shape, float("nan"), device=dev, dtype=torch.bfloat16)
         out = torch.empty(n, h, h, cout, device=dev, dtype=torch.bfloat16)
-        ostat = torch.zeros(2 * cout, dtype=torch.float64, device=dev)
+        ostat = torch.zeros(2 * cout, dtype=torch.int64, device=dev)
         if fold:
             H.conv_fwd(xb, wb, out, (1, 1), "same", stats=ostat, bnin=(fin, y))
         else:

@@ -312,3 +312,56 @@ def test_gap_fwd_paths(H, n, hw, c, f32):
     y = torch.empty(n, c, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
     H.gap_fwd(x.bfloat16(), y)
     close(y, x.mean(dim=(1, 2)), 1e-4 if f32 else 1e-2, 1e-5 if f32 else 4e-3)
+
+
+def test_bn_statistics_accumulators_are_order_independent(H):
+    """BatchNorm statistics through the int64 fixed-point accumulators (damd_common.h
+    bnacc_add1 / bnacc_add2): the sums do not depend on the order in which producer blocks
+    arrive nor on how they are spread over replicas -- bitwise.  Backward (two words per
+    value): bn_bwd_reduce with 8 replicas, with its grid launched in REVERSED block order
+    (block b reduces the rows of block G-1-b) and with 1 replica.  Forward (one word): a
+    conv epilogue's statistics into 1 and 8 replicas.  Both agree with an fp64 reference."""
+    from distributed_amd.native import require_C
+
+    C_ = require_C()
+    M, C = 4096 + 37, 64
+    dy = rb(rnd(M, C, scale=1e-4, seed=41)).bfloat16()
+    x = rb(rnd(M, C, seed=42) * 2 + 0.5).bfloat16()
+    st = torch.stack([x.float().mean(0), torch.rsqrt(x.float().var(0) + 1e-3),
+                      torch.ones(C, device=dev), torch.zeros(C, device=dev)]).contiguous()
+    T = C_.bn_bwd_blocks(M, C)
+    s = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for reps, rev in ((8, False), (8, True), (1, False)):
+        acc = torch.zeros(reps, 4 * C, dtype=torch.int64, device=dev)
+        C_.bn_reduce_reverse(rev)
+        try:
+            C_.bn_bwd_reduce_acc(dy.data_ptr(), 0, 0, x.data_ptr(), st.data_ptr(), 0, acc.data_ptr(), T, M, C, s, reps)
+            torch.cuda.synchronize()
+        finally:
+            C_.bn_reduce_reverse(False)
+        words = acc.cpu().sum(0)
+        outs.append(words)
+    assert torch.equal(outs[0], outs[1]), "reversed block order changed the backward sums"
+    assert torch.equal(outs[0], outs[2]), "the replica count changed the backward sums"
+    got = H.bn_acc_decode(outs[0].unsqueeze(0), words=2)
+    d, xh = dy.double(), (x.double() - st[0].double()) * st[1].double()
+    want = torch.cat([d.sum(0), (d * xh).sum(0)]).cpu()
+    assert torch.allclose(got, want, rtol=1e-5, atol=1e-12), (got - want).abs().max()
+
+    # forward statistics (one word per value) from a conv epilogue, 1 vs 8 replicas
+    n, h, cin, cout = 8, 16, 64, 64
+    xb = rb(rnd(n, h, h, cin, seed=43)).bfloat16()
+    wb = rb(rnd(3, 3, cin, cout, scale=0.05, seed=44)).bfloat16()
+    sums = []
+    for reps in (1, 8):
+        acc = torch.zeros(reps, 2 * cout, dtype=torch.int64, device=dev)
+        out = torch.empty(n, h, h, cout, device=dev, dtype=torch.bfloat16)
+        H.conv_fwd(xb, wb, out, (1, 1), "same", stats=acc if reps > 1 else acc[0])
+        torch.cuda.synchronize()
+        sums.append(acc.cpu().sum(0))
+    assert torch.equal(sums[0], sums[1]), "the replica count changed the forward statistics"
+    o = out.double().reshape(-1, cout)
+    want = torch.cat([o.sum(0), (o * o).sum(0)]).cpu()
+    got = H.bn_acc_decode(sums[0].unsqueeze(0), words=1)
+    assert torch.allclose(got, want, rtol=1e-5, atol=1e-3), (got - want).abs().max()

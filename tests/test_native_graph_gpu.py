@@ -413,12 +413,12 @@ def test_bn_backward_reduce_fused_into_dgrad_epilogue(monkeypatch):
 
 @pytest.mark.parametrize("reps", ["1", "8"])
 def test_bn_finalize_in_consumer_matches_finalize_kernels(monkeypatch, reps):
-    """BatchNorm statistics through fp64 accumulators (DAMD_BN_FIN=1: producers -- conv
-    epilogues, split-K finish, the backprop-input E_BNRED epilogue, bn_bwd_reduce, the stem
-    pool -- add per-block partials into `reps` replicas, the apply kernels finalize in their
-    prologue) == the per-block partials + finalize launches, one step, three initial draws;
-    and two runs with it are bitwise equal (fp64 sums of fp32 partials: arrival order does
-    not change them)."""
+    """BatchNorm statistics through int64 fixed-point accumulators (DAMD_BN_FIN=1: producers
+    -- conv epilogues, split-K finish, the backprop-input E_BNRED epilogue, bn_bwd_reduce,
+    the stem pool -- add per-block partials into `reps` replicas, the apply kernels finalize
+    in their prologue) == the per-block partials + finalize launches, one step, three
+    initial draws; and two runs with it are bitwise equal (integer sums: the arrival order
+    of the producer blocks cannot change them)."""
     from distributed_amd.ops import hip as H
 
     def build():
