@@ -70,7 +70,8 @@ class ConvNetTrainer : public StepExecutor {
       HIP_CHECK(convnet2_launch_bwd(b_, B_, PP_, stream_));
       HIP_CHECK(hipEventRecord(ev[2], stream_));
       if (grad_allreduce_ && !sharded_) {
-        if (peer_ && fold_) peer_->allreduce_staged((long)convnet_grad_count(PP_), 2 * kConvNetNConv, stream_);
+        if (peer_ && fold_)
+          peer_->allreduce_staged((long)convnet_grad_count(PP_), 2 * kConvNetNConv, stream_, b_.hconv);
         else if (peer_) peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, b_.hconv, 2 * kConvNetNConv);
         else if (comm_) comm_->allreduce_f32_i64(b_.G, convnet_grad_count(PP_), b_.hconv, 2 * kConvNetNConv, stream_);
       }
@@ -102,7 +103,10 @@ class ConvNetTrainer : public StepExecutor {
       if (PeerAllreduce::message_words(n, 2 * kConvNetNConv) > p->capacity())
         throw std::invalid_argument("peer all-reduce capacity too small for the folded step");
       b_.G = p->in_local();
-      b_.hconv = reinterpret_cast<long long*>(p->in_local() + nfp);
+      // the conv-gradient int64 sums stay in the engine's own (cached) buffer: bwd adds into
+      // them with atomics, which must not target the uncached staging (measured: replicas
+      // diverged in the conv parameters now and then); the peer kernel copies them in
+      b_.hconv = hconv_own_;
       b_.Gr = p->out_local();
       b_.hconv_r = reinterpret_cast<long long*>(p->out_local() + nfp);
     } else {
@@ -186,7 +190,7 @@ class ConvNetTrainer : public StepExecutor {
     long long* aux = b_.hconv;
     const long n64 = 2 * kConvNetNConv;
     if (peer_ && fold_)  // the message is already in the peer `in` staging: exchange only
-      peer_->allreduce_staged((long)convnet_grad_count(PP_), n64, stream_);
+      peer_->allreduce_staged((long)convnet_grad_count(PP_), n64, stream_, b_.hconv);
     else if (peer_)  // native xGMI two-shot all-reduce
       peer_->allreduce(b_.G, (long)convnet_grad_count(PP_), stream_, aux, n64);
     else if (comm_)  // comm set only when a reduction is wanted

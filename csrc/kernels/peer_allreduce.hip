@@ -111,7 +111,8 @@ __device__ __forceinline__ float4 msg_add(float4 a, float4 b, bool i64) {
 
 // staged: the caller already wrote the message into own `in` and reads the result from own
 // `out` (the fused trainer's folded step): phases A and D are skipped, the flags alone
-// order the exchange (stream order covers the local side, see peer_comm.h)
+// order the exchange (stream order covers the local side, see peer_comm.h).  With `aux`
+// the int64 segment still lives in the caller's memory: phase A copies just that part.
 __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __restrict__ data, long n,
                                                        long long* __restrict__ aux, long n64, int staged) {
   const int b = blockIdx.x, t = threadIdx.x, W = a.world;
@@ -126,6 +127,13 @@ __global__ __launch_bounds__(NT) void peer_allreduce_k(PeerArgs a, float* __rest
     for (int s = 0; s < W; ++s) {
       const long base = s * shard + (long)b * chunk;
       for (long i = t; i < c4; i += NT) in_own[base / 4 + i] = msg_load(data, n, aux, n64, nfp, base + 4 * i);
+    }
+  } else if (aux != nullptr) {  // the int64 words of this block's chunk set only
+    const long a0 = nfp, a1 = nfp + (2 * n64 + 3) / 4 * 4;
+    for (int s = 0; s < W; ++s) {
+      const long base = s * shard + (long)b * chunk;
+      const long lo = max(base, a0), hi = min(base + chunk, a1);
+      for (long g = lo + 4 * t; g < hi; g += 4 * NT) in_own[g / 4] = msg_load(data, n, aux, n64, nfp, g);
     }
   }
   signal_all(a, 0, e);
@@ -172,11 +180,12 @@ hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, long lo
   return hipGetLastError();
 }
 
-hipError_t peer_allreduce_staged_launch(const PeerArgs& a, long n, long n64, hipStream_t st) {
+hipError_t peer_allreduce_staged_launch(const PeerArgs& a, long n, long n64, hipStream_t st, const long long* aux64) {
   if (a.world < 1 || a.world > kPeerMaxRanks || a.nblk < 1 || a.nblk > kPeerMaxBlocks || a.chunk % 4)
     return hipErrorInvalidValue;
   if ((long)a.world * a.nblk * a.chunk < (n + 3) / 4 * 4 + 2 * n64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, nullptr, n, nullptr, n64, 1);
+  hipLaunchKernelGGL(peer_allreduce_k, dim3(a.nblk), dim3(NT), 0, st, a, nullptr, n,
+                     const_cast<long long*>(aux64), n64, 1);
   return hipGetLastError();
 }
 

@@ -116,14 +116,18 @@ void PeerAllreduce::allreduce(float* data, long n, hipStream_t st, long long* au
   HIP_CHECK(peer_allreduce_launch(a_, data, n, aux64, n64, st));
 }
 
-void PeerAllreduce::allreduce_staged(long n, long n64, hipStream_t st) {
+void PeerAllreduce::allreduce_staged(long n, long n64, hipStream_t st, const long long* aux64) {
   if (!opened_) throw std::runtime_error("peer all-reduce: open() the peers' handles first");
   if (n64 < 0 || message_words(n, n64) > cap_) throw std::invalid_argument("peer all-reduce: bad staged message");
   if (a_.world == 1) {  // the result is the input
-    HIP_CHECK(hipMemcpyAsync(out_, in_, (size_t)message_words(n, n64) * sizeof(float), hipMemcpyDeviceToDevice, st));
+    const long nfp = (n + 3) / 4 * 4;
+    HIP_CHECK(hipMemcpyAsync(out_, in_, (size_t)(aux64 ? nfp : message_words(n, n64)) * sizeof(float),
+                             hipMemcpyDeviceToDevice, st));
+    if (aux64)
+      HIP_CHECK(hipMemcpyAsync(out_ + nfp, aux64, (size_t)n64 * sizeof(long long), hipMemcpyDeviceToDevice, st));
     return;
   }
-  HIP_CHECK(peer_allreduce_staged_launch(a_, n, n64, st));
+  HIP_CHECK(peer_allreduce_staged_launch(a_, n, n64, st, aux64));
 }
 
 unsigned PeerAllreduce::status() const {

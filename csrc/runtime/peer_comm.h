@@ -54,8 +54,10 @@ struct PeerArgs {
 // `aux64` (fixed-point accumulators, summed exactly as integers) starting at the next
 // 16-byte word boundary; every rank ends with the same bits.
 hipError_t peer_allreduce_launch(const PeerArgs& a, float* data, long n, long long* aux64, long n64, hipStream_t st);
-// staged: the message is already in `in` of this rank, the result stays in `out`
-hipError_t peer_allreduce_staged_launch(const PeerArgs& a, long n, long n64, hipStream_t st);
+// staged: the fp32 part of the message is already in `in` of this rank, the result stays in
+// `out`; aux64 (may be null: already staged too) is copied into `in` by the kernel itself
+hipError_t peer_allreduce_staged_launch(const PeerArgs& a, long n, long n64, hipStream_t st,
+                                        const long long* aux64 = nullptr);
 
 class PeerAllreduce {
  public:
@@ -80,7 +82,10 @@ class PeerAllreduce {
   // left in `out` (same layout) -- no copy-in / copy-out passes.  The caller writes `in`
   // only after this call's previous instance completed on its stream and reads `out` only
   // after this one did (stream order), which is what keeps the buffer reuse safe.
-  void allreduce_staged(long n, long n64, hipStream_t st);
+  // aux64: the int64 segment lives in the caller's own (cached) memory instead -- e.g.
+  // accumulated there by atomics, which must not target the uncached staging -- and the
+  // kernel copies it into `in` (n64 values, a few KB) before it signals.
+  void allreduce_staged(long n, long n64, hipStream_t st, const long long* aux64 = nullptr);
   // the pointer table of every rank's mapped staging (for kernels that exchange through it
   // directly, e.g. the sharded MNIST step)
   const PeerArgs& args() const { return a_; }

@@ -18,6 +18,9 @@ for s in ${STAGES:-xtests bench}; do
     xtests)  # the exchange: in-process sharded ranks, bitwise cross-transport, self-test fallback
       step xtests 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread \
         tests/test_sharded_inproc_gpu.py tests/test_peer_allreduce_gpu.py ;;
+    bn)  # BatchNorm fixed-point statistics
+      step bntests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+        tests/test_hip_ops_gpu.py tests/test_conv_gemm_gpu.py -k "bn or bnin" ;;
     tests)
       step gputests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     bench)
