@@ -24,7 +24,15 @@ void check(hipError_t e, const char* what) {
 }
 }  // namespace
 
+namespace damd {
+hipError_t spin_stamp(long long ticks, int blocks, unsigned long long* out, int slot, hipStream_t s);
+}
+
 void register_kernel_ops(py::module_& m) {
+  // diagnostics (csrc/kernels/diag.hip): blocks holding their CU for `ticks` x 10 ns
+  m.def("spin_stamp", [](long long ticks, int blocks, uintptr_t out, int slot, uintptr_t s) {
+    check(damd::spin_stamp(ticks, blocks, P_<unsigned long long>(out), slot, P_<ihipStream_t>(s)), "spin_stamp");
+  });
   m.def(
       "gemm",
       [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,

@@ -269,7 +269,7 @@ class NativeGraphEngine(Engine):
         self._phase_events = None  # phase_times(): (name, event) marks of an eager step
         self.feed = None
         self._plan()
-        self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0))
+        self._plan_buckets(env.get_float("DAMD_BUCKET_MB", 8.0), env.get_float("DAMD_BUCKET_LAST_MB", 1.0))
         # bucket transport at world > 1 (DAMD_ALLREDUCE): RCCL (auto, when the RCCL
         # communicator exists), or the native xGMI peer all-reduce over IPC-mapped staging
         # (xgmi; auto without RCCL, e.g. ranks sharing one GPU in a rehearsal) -- both on the
@@ -278,12 +278,24 @@ class NativeGraphEngine(Engine):
         if self.world > 1 and (mode == "xgmi" or (mode == "auto" and self.native_comm is None)):
             from ..parallel.communicator import make_peer_allreduce
 
-            cap = max(b["hi"] - b["lo"] for b in self._buckets)
             from ..utils.watchdog import deadline_for
 
             wd = deadline_for(self.world)  # in-kernel wait deadline = the watchdog's
-            self.peer = make_peer_allreduce(strategy.communicator, dev.index or 0, cap,
-                                            blocks=env.get_int("DAMD_PEER_BLOCKS", 64), timeout_s=wd if wd > 0 else 60.0)
+            # one peer all-reduce (own IPC-mapped staging, own epochs) PER BUCKET, each on its
+            # own side stream: the buckets' all-reduces then need no order among themselves, so
+            # in the captured graph each depends on the backward kernels that wrote its bucket
+            # only.  (One staging for all = a chain of all-reduce nodes, each with two parents
+            # -- the previous all-reduce and the backward -- which the HIP graph executor ran in
+            # line with the backward: profiles/r04_resnet18_dp, scripts/probe_graph_branches.py)
+            self.peers = []
+            for b in self._buckets:
+                p = make_peer_allreduce(strategy.communicator, dev.index or 0, b["hi"] - b["lo"],
+                                        blocks=env.get_int("DAMD_PEER_BLOCKS", 64), timeout_s=wd if wd > 0 else 60.0)
+                if p is None:
+                    self.peers = []
+                    break
+                self.peers.append(p)
+            self.peer = self.peers[0] if self.peers else None
             if self.peer is None and mode == "xgmi":
                 raise RuntimeError("DAMD_ALLREDUCE=xgmi but the xGMI peer mapping is unavailable")
         if self.peer is not None and self.grad_bf16:
@@ -298,9 +310,13 @@ class NativeGraphEngine(Engine):
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.g16 = (torch.zeros(self.nparam, dtype=torch.bfloat16, device=dev)
                     if self.grad_bf16 and self.native_comm is not None else None)
-        # created up front: no stream creation while a graph is being captured
+        # created up front: no stream creation while a graph is being captured.  RCCL: one
+        # comm stream (collectives on one communicator stay in order); peer: one per bucket
         self._comm_stream = (torch.cuda.Stream(dev) if (self.native_comm is not None or self.peer is not None)
                              else None)
+        self._comm_streams = ([torch.cuda.Stream(dev) for _ in self._buckets] if self.peer is not None else [])
+        for k, b in enumerate(self._buckets):
+            b["k"] = k
         opt._iter_source = self._iterations
         torch.cuda.synchronize(dev)
         dlog.info("native graph engine: %d nodes, %d params, %.1f MB planned activations", len(self.nodes), n,
@@ -649,11 +665,13 @@ class NativeGraphEngine(Engine):
         return self.views[id(var)] if var is not None else None
 
     # --- gradient buckets (all-reduce overlapped with the rest of backward) ------------------
-    def _plan_buckets(self, bucket_mb: float):
+    def _plan_buckets(self, bucket_mb: float, last_mb: float = 1.0):
         """Contiguous ranges of G, filled from the END of the Keras weight order (backward
         produces the last layers' gradients first); the metric tail rides in the first
         bucket.  A bucket is all-reduced on a side stream as soon as the backward ops that
-        write its variables have been enqueued."""
+        write its variables have been enqueued.  The bucket of the FIRST
+        layers (written last, its all-reduce trails the whole backward) is cut at
+        ``last_mb``, so the exposed tail of the step is one small all-reduce."""
         writers = {}
         for nd in self.nodes:
             if nd.attrs.get("dead"):
@@ -672,7 +690,14 @@ class NativeGraphEngine(Engine):
                 writers[id(nd)] = vs
         self._writes = {k: [id(v) for v in vs] for k, vs in writers.items()}
         limit = max(1, int(bucket_mb * 2**20 / 4))
-        order = list(range(len(self.vars)))[::-1]
+        first = []  # the first layers' variables, up to last_mb (reduced last)
+        n_first, lim_first = 0, max(1, int(min(last_mb, bucket_mb) * 2**20 / 4))
+        for i in range(len(self.vars)):
+            if first and n_first + self.sizes[i] > lim_first:
+                break
+            first.append(i)
+            n_first += self.sizes[i]
+        order = list(range(len(first), len(self.vars)))[::-1]
         buckets, cur, cur_n = [], [], 0
         for i in order:
             cur.append(i)
@@ -682,6 +707,8 @@ class NativeGraphEngine(Engine):
                 cur, cur_n = [], 0
         if cur:
             buckets.append(cur)
+        if first:
+            buckets.append(first)
         self._buckets = []
         for bi, idxs in enumerate(buckets):
             lo = min(self.offsets[i] for i in idxs)
@@ -704,7 +731,7 @@ class NativeGraphEngine(Engine):
         lo, hi = b["lo"], b["hi"]
         gp = self.G.data_ptr()
         if self.peer is not None:
-            self.peer.allreduce(gp + 4 * lo, hi - lo, st)
+            self.peers[b["k"]].allreduce(gp + 4 * lo, hi - lo, st)
         elif self.g16 is not None:
             n = min(hi, self.nparam) - lo  # the parameter part travels as bf16 ...
             g16 = self.g16.data_ptr() + 2 * lo
@@ -727,12 +754,13 @@ class NativeGraphEngine(Engine):
             b["left"] -= done
             if b["left"] and not final:
                 continue
-            cs = self._comm_stream
+            cs = self._comm_streams[b["k"]] if self.peer is not None else self._comm_stream
             cs.wait_stream(main)
             self._reduce_bucket(b, cs.cuda_stream)
             b["sent"] = True
         if final:
-            main.wait_stream(self._comm_stream)
+            for cs in (self._comm_streams if self.peer is not None else [self._comm_stream]):
+                main.wait_stream(cs)
 
     def _all_tensors(self):
         out = [self.x0]
@@ -1343,7 +1371,7 @@ class NativeGraphEngine(Engine):
         self.graph = g
 
     def _check_peer(self):
-        if self.peer is not None and self.peer.status():
+        if self.peer is not None and any(p.status() for p in self.peers):
             raise RuntimeError("xGMI peer all-reduce: a wait for a peer timed out (peer missing or wedged)")
 
     def metrics(self):

@@ -25,12 +25,24 @@ for s in ${STAGES:-xtests bench}; do
       step gputests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
     bench)
       step bench_n1 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      step bench_n1b 200 python bench.py --gpus 1 --steps 20 --warmup 5
       step bench_n1_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200 ;;
     rehearse)  # the driver's multi-GPU launch, N ranks sharing cuda:0 (gloo control plane)
       for N in ${RANKS:-2}; do
         DAMD_COMM=gloo step share_n$N 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N \
           --master-addr 127.0.0.1 --master-port $((29500 + N)) bench.py --gpus $N --steps 200 --warmup 20
       done ;;
+    fused)
+      step fused 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_convnet_gpu.py ;;
+    stamps)
+      step stamps 200 python scripts/stamps.py 64 ;;
+    gprobe)
+      step gprobe 300 python scripts/probe_graph_branches.py 4 8 ;;
+    dpprof)  # ResNet-18 N = 2 sharing the GPU: bucket all-reduce overlap (peer transport)
+      step dpprof 500 bash scripts/prof_resnet_dp.sh
+      python scripts/dp_overlap.py "$(ls gpurun_out/prof_rn_dp/*/rn_kernel_trace.csv 2>/dev/null | head -1 || ls gpurun_out/prof_rn_dp/rn_kernel_trace.csv)" gpurun_out/dp_overlap.txt || true ;;
+    ngpeer)
+      step ngpeer 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_peer_allreduce_gpu.py -k native_graph ;;
     resnet)
       step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5 ;;
   esac

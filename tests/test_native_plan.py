@@ -67,6 +67,11 @@ def test_gradient_buckets_tile_the_flat_buffer():
     # every trainable variable has exactly one writer node in the backward plan
     written = [i for vs in pl._writes.values() for i in vs]
     assert sorted(written) == sorted(id(v) for v in pl.vars)
+    # the bucket of the first layers -- written last by backward, so its all-reduce trails
+    # the step -- is cut at DAMD_BUCKET_LAST_MB (1 MB): a short exposed tail
+    last = [b for b in bs if b["lo"] == 0][0]
+    assert (last["hi"] - last["lo"]) * 4 <= 2**20, last["hi"] * 4
+    assert bs[-1] is last
 
 
 class _FakeGPUStrategy:
