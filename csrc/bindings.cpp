@@ -51,6 +51,10 @@ class ConvNetTrainer : public StepExecutor {
     b_.hconv = P_<long long>(g("hconv"));
     b_.calt = P_<float>(g("calt"));
     b_.ppb = bufs.contains("ppb") ? (int)g("ppb") : PP;
+    // optional next-batch prefetch buffers (convnet.h): [B][784] x 4 bytes + one int64 tag
+    b_.xnext = bufs.contains("xnext") ? P_<void>(g("xnext")) : nullptr;
+    b_.xtag = bufs.contains("xtag") ? P_<long long>(g("xtag")) : nullptr;
+    if ((b_.xnext == nullptr) != (b_.xtag == nullptr)) throw std::invalid_argument("xnext and xtag go together");
     if (b_.ppb < 1 || b_.ppb > 4) throw std::invalid_argument("bwd positions per slice must be in [1,4]");
     HIP_CHECK(convnet2_set_lds_limits());
   }
@@ -88,6 +92,8 @@ class ConvNetTrainer : public StepExecutor {
   // epoch-permuted copies (stable pointers).
   void set_data(uintptr_t X, uintptr_t labels, int x_u8) {
     b_.X = P_<const void>(X); b_.labels = P_<const int>(labels); b_.x_u8 = x_u8;
+    // a prefetched batch of the previous data must never match a tag again
+    if (b_.xtag) HIP_CHECK(hipMemsetAsync(b_.xtag, 0, sizeof(long long), stream_));
     invalidate_graphs();
   }
   // Fold the per-step peer all-reduce into the step kernels: bwd writes its gradient

@@ -58,6 +58,12 @@ struct ConvNetBuffers {
   // Then Gr = this rank's gradient staging and hconv_r = the conv-gradient sums that
   // convnet2_launch_gather fills for flush / the host
   const XArgs* xa;
+  // next-batch prefetch (B <= 64; both may be null = off): the backward of step t copies the
+  // input rows of step t + 1 into xnext ([B][784] in X's dtype) and tags them in *xtag with
+  // (ctrl.xgen << 32) | (cursor + 1); the forward of step t + 1 loads them before it has
+  // read the ctrl block and keeps them when the tag matches (else it loads X as before)
+  void* xnext;
+  long long* xtag;
   // pooled positions per slice of the backward kernel (0: the forward's PP).  The forward
   // runs 4 image groups per slice (a 228-block grid at PP 3); the backward has one block per
   // slice, so a finer slicing spreads its dW1 / dP / conv-gradient work over more CUs

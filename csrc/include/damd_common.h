@@ -124,7 +124,9 @@ struct Ctrl {
                             //    rank's small-gradient message)
   int   pend2;              // 24 `pending` as seen by the step's fwd (set by it): bwd folds the
                             //    previous step's metric tail only when there was one
-  int   pad[7];
+  int   xgen;               // 25 input-data generation: the host bumps it whenever it changes the
+                            //    cursor or the epoch's rows (tags the prefetched next batch)
+  int   pad[6];
 };
 static_assert(sizeof(Ctrl) == 128, "Ctrl must be 128 bytes");
 

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
                                            long long* __restrict__ hacc, long long* __restrict__ hconv,
                                            float* __restrict__ calt, int B, int PP, int lg, int eager,
                                            unsigned long long* st, const long long* __restrict__ hconv_r,
-                                           const XArgs xa) {
+                                           const XArgs xa, const void* __restrict__ xnext,
+                                           const long long* __restrict__ xtag) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
@@ -145,6 +146,16 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
   const float* lut = nullptr;  // (x_store converts k / 255 arithmetically)
   const int n4 = K * HID / 4;  // <= 2048
+  const int r0 = 2 * (p0 / PO);
+  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
+  // ---- the batch rows as the previous step's bwd prefetched them (xnext): issued first,
+  // before the ctrl block is known; kept below if their tag names this step's rows ----
+  XStage<U8> xst;
+  long long xt = 0;
+  if (xnext != nullptr) {
+    x_load<U8>(xst, xnext, img0, B, B - img0, IB, r0, nrows);
+    xt = *xtag;
+  }
   // ---- first the loads whose addresses do not depend on the ctrl block: the bf16 W1 slice
   // (eager), both parities of the conv parameters, the b1/W2/b2 triplet; the scheduling
   // barrier keeps them ahead of the ctrl load (left alone, hipcc issued the ctrl load first
@@ -179,13 +190,12 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   }
   const bool pend = c.pending != 0;
   const long row_base = (long)c.cursor * c.global_batch + c.row0 + img0;
-  const int r0 = 2 * (p0 / PO);
-  const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const bool mom = c.momentum != 0.f;
 
-  // ---- then the ctrl-dependent loads: the batch rows (and, deferred update, W1 by parity) ----
-  XStage<U8> xst;
-  x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
+  // ---- then the ctrl-dependent loads: the batch rows unless prefetched (and, deferred
+  // update, W1 by parity) ----
+  const bool xhit = xnext != nullptr && xt == (((long long)c.xgen << 32) | (long long)(unsigned)(c.cursor + 1));
+  if (!xhit) x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
   float4 wv[4], gv[4], vv[4];
   const float* Wcur = c.wpar ? W1alt : P + OFF_W1;
   const float* Vcur = c.wpar ? V1alt : V + OFF_W1;
@@ -499,7 +509,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
                                            long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
-                                           unsigned long long* st, const float* __restrict__ Gr, const XArgs xa) {
+                                           unsigned long long* st, const float* __restrict__ Gr, const XArgs xa,
+                                           void* __restrict__ xnext, long long* __restrict__ xtag) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   constexpr int cprobe = DAMD_PROBE_HCONV;  // 0 in every product build (see the top of the file)
@@ -591,6 +602,19 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   const long row_base = gstart + c.row0;
   const int gcount = (int)min((long)c.global_batch, (long)c.nsamples - gstart);
   const float inv = gcount > 0 ? 1.f / (float)gcount : 0.f;
+  // next-batch prefetch for the next fwd: this block's share of the next step's rows as
+  // 16-byte units (stored at the end; the loads travel meanwhile)
+  const int ncur = next_cursor(c, cur);
+  constexpr int UPI = U8 ? NPIX / 16 : NPIX / 4;  // 16-byte units per image
+  const int xpu = s * 512 + tid;
+  const bool xpf = ONE && xnext != nullptr && xpu < B * UPI;
+  uint4 xnv = make_uint4(0u, 0u, 0u, 0u);
+  if (xpf) {
+    const int b = xpu / UPI, q = xpu - b * UPI;
+    const long g = (long)ncur * c.global_batch + c.row0 + b;
+    if (g < c.nsamples)
+      xnv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + g * (U8 ? NPIX : 4 * NPIX))[q];
+  }
 
   // then the ctrl-dependent ones: the dense-1 sums by parity, the labels, the batch rows
   auto load_dep = [&](int chunk) __attribute__((always_inline)) {
@@ -947,6 +971,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     uint4* h4 = reinterpret_cast<uint4*>(hacc + (long)(par ^ 1) * B * HID);
     for (int i = s * 512 + tid; i < B * HID / 2; i += NS * 512) h4[i] = make_uint4(0u, 0u, 0u, 0u);
   }
+  if (xpf) reinterpret_cast<uint4*>(xnext)[xpu] = xnv;
+  if (ONE && xnext != nullptr && s == 0 && tid == 0) *xtag = ((long long)c.xgen << 32) | (long long)(unsigned)(ncur + 1);
   if (sh) exchange_tail(xa, ctrl, G, hconv + par * NCONV, accw, xe, s, NS, np, p0, dn, dm0, lane, tid, xown, xo, xu);
   stamp(sts, st, 5);
   stamp_flush(sts, st, 9);
@@ -1107,7 +1133,7 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
                      b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg,
                      eager2(b, B), b.stamps,
-                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b));
+                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b), B <= CH ? b.xnext : nullptr, b.xtag);
 }
 
 static int ppb_of(const ConvNetBuffers& b, int PP) { return b.ppb > 0 ? b.ppb : PP; }
@@ -1122,13 +1148,13 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b));
+                       xargs(b), b.xnext, b.xtag);
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b));
+                       xargs(b), b.xnext, b.xtag);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {

@@ -158,6 +158,12 @@ void StepExecutor::restrict_cus(int part, int nparts) {
   HIP_CHECK(hipStreamSynchronize(stream_));
   HIP_CHECK(hipStreamDestroy(stream_));
   stream_ = nullptr;
+  // (hipExtStreamCreateWithCUMask takes no flags: the new stream is a BLOCKING stream, i.e.
+  // it synchronizes with the legacy null stream, unlike the constructor's non-blocking one.
+  // Its users -- ranks sharing one device, one rank per process in the engine -- enqueue no
+  // null-stream work between steps (host reads sync first); several ranks in ONE process
+  // (tests/test_sharded_inproc_gpu.py) must not queue null-stream work while their steps
+  // wait on each other, or the waits serialise until the in-kernel deadline.)
   HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()));
 }
 

@@ -29,7 +29,7 @@ NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 # ctrl word indices (csrc/include/damd_common.h struct Ctrl)
 (C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
- C_FLUSHT, C_PEND, C_PAR2, C_BAD, C_XCNT, C_XCNT2, C_TICKET, C_PEND2) = range(25)
+ C_FLUSHT, C_PEND, C_PAR2, C_BAD, C_XCNT, C_XCNT2, C_TICKET, C_PEND2, C_XGEN) = range(26)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
 
 
@@ -114,6 +114,12 @@ class FusedConvNetEngine(Engine):
         self.hacc = torch.zeros(2 * B * HID, dtype=torch.int64, device=dev)  # by step parity
         self.hconv = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
         self.calt = torch.zeros(2 * NCONV, **f32)  # alternate conv parameters + velocity
+        # next-batch prefetch (B <= 64): bwd copies the next step's rows here for the next fwd,
+        # tagged with the ctrl block's data generation + cursor (DAMD_XPREFETCH=0: off)
+        self.xnext = self.xtag = None
+        if B <= 64 and env.get_bool("DAMD_XPREFETCH", True):
+            self.xnext = torch.zeros(B * 784, **f32)  # (u8 rows use the first quarter)
+            self.xtag = torch.zeros(1, dtype=torch.int64, device=dev)
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
         off = 0
@@ -140,6 +146,8 @@ class FusedConvNetEngine(Engine):
                     v1alt=self.v1alt.data_ptr(), w1bf=self.w1bf.data_ptr(),
                     hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr(),
                     ppb=self.PPB)
+        if self.xnext is not None:
+            bufs.update(xnext=self.xnext.data_ptr(), xtag=self.xtag.data_ptr())
         # world 1 (no gradient all-reduce): bwd applies the W1 update itself as soon as it
         # has the slice's gradient, and fwd reads only the bf16 copy (DAMD_EAGER_W1=0: the
         # deferred update in fwd, as with an all-reduce between the launches)
@@ -293,6 +301,9 @@ class FusedConvNetEngine(Engine):
         c = self.ctrl.cpu()
         for k, v in updates.items():
             c[k] = v
+        # any host write may move the cursor or follow new epoch rows: a batch the last bwd
+        # prefetched must not match its tag any more
+        c[C_XGEN] = (int(c[C_XGEN]) + 1) & 0x7fffffff
         self.ctrl.copy_(c.to(self.device))
         torch.cuda.synchronize(self.device)
 
