@@ -54,7 +54,14 @@ class ConvNetTrainer : public StepExecutor {
     // optional next-batch prefetch buffers (convnet.h): [B][784] x 4 bytes + one int64 tag
     b_.xnext = bufs.contains("xnext") ? P_<void>(g("xnext")) : nullptr;
     b_.xtag = bufs.contains("xtag") ? P_<long long>(g("xtag")) : nullptr;
-    if ((b_.xnext == nullptr) != (b_.xtag == nullptr)) throw std::invalid_argument("xnext and xtag go together");
+    b_.xcur = bufs.contains("xcur") ? P_<void>(g("xcur")) : nullptr;
+    b_.ycur = bufs.contains("ycur") ? P_<int>(g("ycur")) : nullptr;
+    if ((b_.xnext == nullptr) != (b_.xtag == nullptr) || (b_.xcur == nullptr) != (b_.ycur == nullptr))
+      throw std::invalid_argument("xnext / xtag and xcur / ycur go in pairs");
+    // parity hints (convnet.h par_hint; DAMD_PAR_HINT=0: the kernels read ctrl.wpar)
+    const char* ph = getenv("DAMD_PAR_HINT");
+    hint_ = !(ph && ph[0] == '0');
+    b_.par_hint = -1;
     if (b_.ppb < 1 || b_.ppb > 4) throw std::invalid_argument("bwd positions per slice must be in [1,4]");
     HIP_CHECK(convnet2_set_lds_limits());
   }
@@ -69,9 +76,11 @@ class ConvNetTrainer : public StepExecutor {
     std::vector<std::vector<float>> out;
     for (int i = 0; i < k; ++i) {
       HIP_CHECK(hipEventRecord(ev[0], stream_));
+      b_.par_hint = hint_ ? par_ : -1;
       HIP_CHECK(convnet2_launch_fwd(b_, B_, PP_, stream_));
       HIP_CHECK(hipEventRecord(ev[1], stream_));
       HIP_CHECK(convnet2_launch_bwd(b_, B_, PP_, stream_));
+      par_ ^= 1;
       HIP_CHECK(hipEventRecord(ev[2], stream_));
       if (grad_allreduce_ && !sharded_) {
         if (peer_ && fold_)
@@ -176,7 +185,9 @@ class ConvNetTrainer : public StepExecutor {
   void flush() {
     gather();
     HIP_CHECK(convnet2_launch_flush(b_, B_, stream_));
+    par_ = 0;  // flush resets ctrl.wpar
   }
+  int parity() const { return par_; }
   // timed runs: k steps + the flush of the last deferred update as one graph
   void capture_final(int k) { StepExecutor::capture_final(k); }
   bool run_final(int k) { return StepExecutor::run_final(k); }
@@ -187,9 +198,14 @@ class ConvNetTrainer : public StepExecutor {
 
  protected:
   void enqueue_tail() override { flush(); }
+  int phase_value() const override { return par_; }
+  void set_phase(int p) override { par_ = p; }
+  int phase_after(int p, int k, bool tail) const override { return tail ? 0 : p ^ (k & 1); }
   void enqueue_one_step() override {
     if (!b_.X) throw std::runtime_error("ConvNetTrainer: set_data() not called");
+    b_.par_hint = hint_ ? par_ : -1;
     HIP_CHECK(convnet2_launch_step(b_, B_, PP_, stream_));
+    par_ ^= 1;  // bwd flips ctrl.wpar
     if (!grad_allreduce_ || sharded_) return;  // sharded: the exchange is inside the step kernels
     // the conv gradient is int64 fixed point (hconv): reduced exactly, in the same call as
     // the fp32 gradient + metric buffer; both parities (see convnet_step2.hip)
@@ -210,6 +226,8 @@ class ConvNetTrainer : public StepExecutor {
   bool fold_ = false;
   bool sharded_ = false;
   XArgs xa_{};  // b_.xa points here (kernels take it by value at launch)
+  int par_ = 0;        // host shadow of ctrl.wpar (0 at construction and after every flush)
+  bool hint_ = true;   // pass it to the kernels (par_hint)
   int B_, PP_, grad_allreduce_;
 };
 
@@ -328,6 +346,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("num_slices", &ConvNetTrainer::num_slices)
       .def_property_readonly("num_slices_bwd", &ConvNetTrainer::num_slices_bwd)
       .def_property_readonly("batch", &ConvNetTrainer::batch)
+      .def_property_readonly("parity", &ConvNetTrainer::parity)
       .def_property_readonly("stream", [](ConvNetTrainer& t) { return reinterpret_cast<uintptr_t>(t.stream()); });
 
   register_kernel_ops(m);

@@ -64,6 +64,15 @@ struct ConvNetBuffers {
   // read the ctrl block and keeps them when the tag matches (else it loads X as before)
   void* xnext;
   long long* xtag;
+  // this step's rows and labels as the forward read them ([B][784] in X's dtype, [B] int32,
+  // -1 = no row): the backward reads them there instead of through the ctrl block's cursor
+  // (both may be null = off; used together with xnext)
+  void* xcur;
+  int* ycur;
+  // the step parity (ctrl.wpar) the host expects at this launch, or -1 = unknown: with it
+  // the kernels address the parity buffers before the ctrl block arrives (a mismatch with
+  // ctrl.wpar -- a host bookkeeping bug -- raises ctrl.bad: the loss reads NaN)
+  int par_hint;
   // pooled positions per slice of the backward kernel (0: the forward's PP).  The forward
   // runs 4 image groups per slice (a 228-block grid at PP 3); the backward has one block per
   // slice, so a finer slicing spreads its dW1 / dP / conv-gradient work over more CUs

@@ -58,34 +58,32 @@ constexpr int C3_HQ = 6;
 // leave those C3_HQ newer DMA instructions in flight
 // pre(): once, after the first tap's operands (and so the chunk's halo) have landed, before
 // any tap reads the halo (the BN-input transform; it ends with its own barrier)
+// wait until at most ahead x NQ + EXTRA DMA instructions of this wave are outstanding (the
+// stage this tap reads has landed; `ahead` later stages -- and EXTRA halo-prefetch pieces --
+// stay in flight); vmcnt takes an immediate, so one branch per possible `ahead`
+template <int NQ, int EXTRA, int A>
+__device__ __forceinline__ void wait_ahead(int ahead) {
+  if constexpr (A > 0) {
+    if (ahead >= A) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A * NQ + EXTRA) : "memory");
+      return;
+    }
+    wait_ahead<NQ, EXTRA, A - 1>(ahead);
+  } else {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EXTRA) : "memory");
+  }
+}
+
 template <int STAGES, int NQ, class Issue, class Compute, class Prefetch, class Pre>
 __device__ __forceinline__ void tap_loop(Issue& issue, Compute& compute, Prefetch& prefetch, bool pf, Pre& pre) {
   constexpr int NK = 9, KH = NK - STAGES;
+  static_assert(STAGES >= 2 && STAGES <= 8 && (STAGES - 2) * NQ + C3_HQ <= 63, "vmcnt range");
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s) issue(s, s);
   for (int kt = 0; kt < NK; ++kt) {
     const int ahead = min(NK - 1 - kt, STAGES - 2);
-    if (pf && kt > KH) {
-      if constexpr (STAGES >= 4) {
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQ + C3_HQ) : "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ + C3_HQ) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C3_HQ) : "memory");
-      } else if constexpr (STAGES == 3) {
-        if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ + C3_HQ) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C3_HQ) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(C3_HQ) : "memory");
-      }
-    } else if constexpr (STAGES >= 4) {
-      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NQ) : "memory");
-      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if constexpr (STAGES == 3) {
-      if (ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NQ) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (pf && kt > KH) wait_ahead<NQ, C3_HQ, STAGES - 2>(ahead);
+    else wait_ahead<NQ, 0, STAGES - 2>(ahead);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (kt + STAGES - 1 < NK) issue((kt + STAGES - 1) % STAGES, kt + STAGES - 1);
@@ -373,12 +371,21 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
 
 template <int BN>
 constexpr int conv3_stages() { return BN == 64 ? 4 : 3; }
+// DAMD_CONV3_DEEP=1: two more weight stages (a deeper ring, fewer blocks per CU when the LDS
+// no longer fits two) -- an A/B switch for the latency-hiding question
+static int conv3_deep() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DAMD_CONV3_DEEP");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v;
+}
 
 int halo_bytes_of(int R, int W) { return (((R + 2) * (W + 2)) * 128 + 1023) & ~1023; }
 
-template <int BN, bool DG, int EPI>
-hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
-  constexpr int ST = conv3_stages<BN>();
+template <int BN, bool DG, int EPI, int ST>
+hipError_t launch3_st(const GemmArgs& a, int R, hipStream_t s) {
   const int tpi = (a.H + R - 1) / R;
   const size_t hb = (size_t)halo_bytes_of(R, a.W), ring = (size_t)ST * BN * 64 * 2;
   auto k = conv3_kernel<BN, DG, EPI, ST>;
@@ -406,8 +413,15 @@ hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
   const int hb2 = !(ev && ev[0] == '0') && a.Cin / 64 > 1 && (int)(hb / 1024) <= 4 * C3_HQ && lds2 <= 160 * 1024 &&
                   (grid <= cus || lds2 <= 80 * 1024);
   const size_t lds = hb2 ? lds2 : hb + ring + sft;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k, dim3(a.N / BN, nimg * tpi), dim3(NT), lds, s, a, R, tpi, hb2, (int)(lds - sft));
   return hipGetLastError();
+}
+
+template <int BN, bool DG, int EPI>
+hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
+  if (conv3_deep()) return launch3_st<BN, DG, EPI, conv3_stages<BN>() + 2>(a, R, s);
+  return launch3_st<BN, DG, EPI, conv3_stages<BN>()>(a, R, s);
 }
 
 template <int BN, bool DG>

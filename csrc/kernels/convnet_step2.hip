@@ -128,7 +128,8 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
                                            float* __restrict__ calt, int B, int PP, int lg, int eager,
                                            unsigned long long* st, const long long* __restrict__ hconv_r,
                                            const XArgs xa, const void* __restrict__ xnext,
-                                           const long long* __restrict__ xtag) {
+                                           const long long* __restrict__ xtag, const int* __restrict__ labels,
+                                           void* __restrict__ xcur, int* __restrict__ ycur, int phint) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
@@ -180,7 +181,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   __builtin_amdgcn_sched_barrier(0);
 
   const Ctrl c = *ctrl;
-  const int par = c.wpar;
+  const int par = phint >= 0 ? phint : c.wpar;
+  if (phint >= 0 && phint != c.wpar && lin == 0 && tid == 0)
+    __hip_atomic_fetch_or(&ctrl->bad, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned xe = (unsigned)c.xcnt;  // sharded: exchange epoch of the pending update
   if (lin == 0 && tid == 0) {
     ctrl->cur2 = c.cursor;
@@ -196,11 +199,28 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // update, W1 by parity) ----
   const bool xhit = xnext != nullptr && xt == (((long long)c.xgen << 32) | (long long)(unsigned)(c.cursor + 1));
   if (!xhit) x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
+  // this step's rows and labels for the backward (xcur / ycur): a share per block, from the
+  // prefetch when it hit (L2-hot), else from the dataset; stored at the end of the kernel
+  constexpr int UPI = U8 ? NPIX / 16 : NPIX / 4;  // 16-byte units per image
+  const int xcu = lin * 512 + tid;
+  const bool xcp = xcur != nullptr && xcu < B * UPI;
+  uint4 xcv = make_uint4(0u, 0u, 0u, 0u);
+  int ycv = -1;
+  {
+    const long rb0 = (long)c.cursor * c.global_batch + c.row0;
+    if (xcp) {
+      const int b = xcu / UPI, q = xcu - b * UPI;
+      if (xhit) xcv = reinterpret_cast<const uint4*>(xnext)[xcu];
+      else if (rb0 + b < c.nsamples)
+        xcv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + (rb0 + b) * (U8 ? NPIX : 4 * NPIX))[q];
+    }
+    if (xcur != nullptr && lin == 0 && tid < B && rb0 + tid < c.nsamples) ycv = labels[rb0 + tid];
+  }
   float4 wv[4], gv[4], vv[4];
-  const float* Wcur = c.wpar ? W1alt : P + OFF_W1;
-  const float* Vcur = c.wpar ? V1alt : V + OFF_W1;
-  float* Wnext = c.wpar ? P + OFF_W1 : W1alt;
-  float* Vnext = c.wpar ? V + OFF_W1 : V1alt;
+  const float* Wcur = par ? W1alt : P + OFF_W1;
+  const float* Vcur = par ? V1alt : V + OFF_W1;
+  float* Wnext = par ? P + OFF_W1 : W1alt;
+  float* Vnext = par ? V + OFF_W1 : V1alt;
   const float4* P4 = reinterpret_cast<const float4*>(Wcur + p0 * 32 * HID);
   const float4* G4 = reinterpret_cast<const float4*>(G + OFF_W1 + p0 * 32 * HID);
   const float4* V4 = reinterpret_cast<const float4*>((mom ? Vcur : Wcur) + p0 * 32 * HID);
@@ -388,6 +408,8 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   long long* hp = hacc + (long)par * B * HID;
   for (int r = wave; r < (hprobe == 1 ? 0 : hprobe == 2 ? IB / 2 : IB); r += 8)
     if (img0 + r < B) atomic_add_i64(hp + (long)(img0 + r) * HID + lane, to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
+  if (xcp) reinterpret_cast<uint4*>(xcur)[xcu] = xcv;
+  if (xcur != nullptr && lin == 0 && tid < B) ycur[tid] = ycv;
   stamp(sts, st, 4);
   if (st != nullptr && tid == 0 && lin < 256)
     for (int i = 0; i < 5; ++i) st[lin * 16 + i] = sts.t[i];
@@ -510,7 +532,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
                                            unsigned long long* st, const float* __restrict__ Gr, const XArgs xa,
-                                           void* __restrict__ xnext, long long* __restrict__ xtag) {
+                                           void* __restrict__ xnext, long long* __restrict__ xtag,
+                                           const void* __restrict__ xcur, const int* __restrict__ ycur, int phint) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   constexpr int cprobe = DAMD_PROBE_HCONV;  // 0 in every product build (see the top of the file)
@@ -559,12 +582,25 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   const float ag_old = sh ? 0.f : Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];
   // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
   const float spv0 = P[OFF_B1 + tid], spv1 = P[OFF_B1 + min(tid + 512, NSMALL - 1)];
+  uint4 hq0, hq1, hq2, hq3;  // hacc row (tid >> 3), columns 8 (tid & 7) .. + 8
+  // known parity (single chunk): the head's first operand -- this step's dense-1 sums --
+  // right behind b1 / W2 / b2, before the ctrl block
+  const bool hq_early = ONE && phint >= 0;
+  auto load_hq = [&](int chunk, int p) __attribute__((always_inline)) {
+    const int r = tid >> 3, q = tid & 7;
+    const int row = min(chunk * CH + r, B - 1);
+    const uint4* hp = reinterpret_cast<const uint4*>(hacc + (long)p * B * HID + (long)row * HID + q * 8);
+    hq0 = hp[0];
+    hq1 = hp[1];
+    hq2 = hp[2];
+    hq3 = hp[3];
+  };
+  if (hq_early) load_hq(0, phint);
   const int n8 = K * HID / 8;
   uint4 wv0, wv1;
   wv0 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid, n8 - 1)];
   wv1 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + 512, n8 - 1)];
   XStage<U8> xst;
-  uint4 hq0, hq1, hq2, hq3;  // hacc row (tid >> 3), columns 8 (tid & 7) .. + 8
   uint4 pv0, pv1;
   uint4 cv;                  // argmax codes, zeroed at the LDS store unless cok
   bool cok = false;
@@ -583,14 +619,21 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       cok = i < CH * kc && lb < B;
       cv = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF + min(q, kc - 1) * 16);
     }
+    if (ycur != nullptr) {  // labels and rows as this step's fwd read them: no cursor needed
+      const int b = chunk * CH + min(tid, CH - 1);
+      ylab = ycur[min(b, B - 1)];
+      yval = tid < CH && b < B && ylab >= 0;
+      x_load<U8>(xst, xcur, chunk * CH, B, B - chunk * CH, CH, r0, nrows);
+    }
   };
   load_indep(0);
   __builtin_amdgcn_sched_barrier(0);
 
   const Ctrl c = *ctrl;
-  const int cur = c.cur2, par = c.par2;
+  const int cur = c.cur2, par = phint >= 0 ? phint : c.par2;
+  if (phint >= 0 && phint != c.par2 && s == 0 && tid == 0)
+    __hip_atomic_fetch_or(&ctrl->bad, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned xe = (unsigned)c.xcnt2 + 1u;  // sharded: this step's exchange epoch
-  const long long* hcur = hacc + (long)par * B * HID;
   if (s == 0 && tid == 0) {
     ctrl->cursor = next_cursor(c, cur);
     ctrl->iterations = c.iterations + 1;
@@ -609,31 +652,20 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   const int xpu = s * 512 + tid;
   const bool xpf = ONE && xnext != nullptr && xpu < B * UPI;
   uint4 xnv = make_uint4(0u, 0u, 0u, 0u);
-  if (xpf) {
-    const int b = xpu / UPI, q = xpu - b * UPI;
-    const long g = (long)ncur * c.global_batch + c.row0 + b;
-    if (g < c.nsamples)
-      xnv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + g * (U8 ? NPIX : 4 * NPIX))[q];
-  }
 
-  // then the ctrl-dependent ones: the dense-1 sums by parity, the labels, the batch rows
+  // then the ctrl-dependent ones: the dense-1 sums by parity (unless known), the labels and
+  // the batch rows (unless the fwd staged them in ycur / xcur)
   auto load_dep = [&](int chunk) __attribute__((always_inline)) {
-    {
-      const int r = tid >> 3, q = tid & 7;
-      const int row = min(chunk * CH + r, B - 1);
-      const uint4* hp = reinterpret_cast<const uint4*>(hcur + (long)row * HID + q * 8);
-      hq0 = hp[0];
-      hq1 = hp[1];
-      hq2 = hp[2];
-      hq3 = hp[3];
+    if (!hq_early || chunk > 0) load_hq(chunk, par);
+    if (ycur == nullptr) {
+      {
+        const int b = chunk * CH + min(tid, CH - 1);
+        const long g = row_base + b;
+        yval = tid < CH && b < B && g < c.nsamples;
+        ylab = labels[max(0L, min(g, (long)c.nsamples - 1))];
+      }
+      x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
     }
-    {
-      const int b = chunk * CH + min(tid, CH - 1);
-      const long g = row_base + b;
-      yval = tid < CH && b < B && g < c.nsamples;
-      ylab = labels[max(0L, min(g, (long)c.nsamples - 1))];
-    }
-    x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
   };
   auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
     load_indep(chunk);
@@ -662,6 +694,13 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     store_head();
   };
   load_dep(0);
+  // the next step's rows for its fwd (issued after this step's own loads: in-order vmcnt)
+  if (xpf) {
+    const int b = xpu / UPI, q = xpu - b * UPI;
+    const long g = (long)ncur * c.global_batch + c.row0 + b;
+    if (g < c.nsamples)
+      xnv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + g * (U8 ? NPIX : 4 * NPIX))[q];
+  }
   // (w1s is read only by the dP MFMAs, several barriers later)
   if (tid < n8) *reinterpret_cast<uint4*>(w1s + (tid >> 3) * HP + (tid & 7) * 8) = wv0;
   if (tid + 512 < n8) *reinterpret_cast<uint4*>(w1s + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = wv1;
@@ -1133,7 +1172,8 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
                      b.Gr ? b.Gr : b.G, b.V,
                      b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg,
                      eager2(b, B), b.stamps,
-                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b), B <= CH ? b.xnext : nullptr, b.xtag);
+                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b), B <= CH ? b.xnext : nullptr, b.xtag, b.labels,
+                     B <= CH ? b.xcur : nullptr, b.ycur, b.par_hint);
 }
 
 static int ppb_of(const ConvNetBuffers& b, int PP) { return b.ppb > 0 ? b.ppb : PP; }
@@ -1148,13 +1188,15 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b), b.xnext, b.xtag);
+                       xargs(b), b.xnext, b.xtag, B <= CH ? b.xcur : nullptr, B <= CH ? b.ycur : nullptr,
+                       b.par_hint);
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b), b.xnext, b.xtag);
+                       xargs(b), b.xnext, b.xtag, B <= CH ? b.xcur : nullptr, B <= CH ? b.ycur : nullptr,
+                       b.par_hint);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {

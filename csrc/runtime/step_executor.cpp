@@ -42,6 +42,7 @@ void StepExecutor::step(int k) {
 
 hipGraphExec_t StepExecutor::capture_steps(int k, bool tail, hipGraph_t* keep) {
   hipGraph_t g = nullptr;
+  const int p0 = phase_value();  // the captured steps do not run: the phase stays
   HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
     for (int i = 0; i < k; ++i) enqueue_one_step();
@@ -49,8 +50,10 @@ hipGraphExec_t StepExecutor::capture_steps(int k, bool tail, hipGraph_t* keep) {
   } catch (...) {
     hipStreamEndCapture(stream_, &g);
     if (g) hipGraphDestroy(g);
+    set_phase(p0);
     throw;
   }
+  set_phase(p0);
   HIP_CHECK(hipStreamEndCapture(stream_, &g));
   hipGraphExec_t ge = nullptr;
   hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
@@ -65,14 +68,17 @@ hipGraphExec_t StepExecutor::capture_steps(int k, bool tail, hipGraph_t* keep) {
 
 std::pair<int, int> StepExecutor::step_graph_nodes(int k) {
   hipGraph_t g = nullptr;
+  const int p0 = phase_value();
   HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   try {
     for (int i = 0; i < k; ++i) enqueue_one_step();
   } catch (...) {
     hipStreamEndCapture(stream_, &g);
     if (g) hipGraphDestroy(g);
+    set_phase(p0);
     throw;
   }
+  set_phase(p0);
   HIP_CHECK(hipStreamEndCapture(stream_, &g));
   size_t n = 0;
   hipError_t e = hipGraphGetNodes(g, nullptr, &n);
@@ -90,20 +96,22 @@ std::pair<int, int> StepExecutor::step_graph_nodes(int k) {
 }
 
 void StepExecutor::capture(int k) {
-  if (k <= 0 || graphs_.count(k)) return;
-  graphs_[k] = capture_steps(k, false);
+  const Key key{k, phase_value()};
+  if (k <= 0 || graphs_.count(key)) return;
+  graphs_[key] = capture_steps(k, false);
 }
 
 void StepExecutor::capture_final(int k) {
-  if (k <= 0 || finals_.count(k)) return;
+  const Key key{k, phase_value()};
+  if (k <= 0 || finals_.count(key)) return;
   hipGraph_t g = nullptr;
-  finals_[k] = capture_steps(k, true, &g);
-  final_graphs_[k] = g;
+  finals_[key] = capture_steps(k, true, &g);
+  final_graphs_[key] = g;
 }
 
 bool StepExecutor::warm_final(int k) {
-  auto it = finals_.find(k);
-  auto gt = final_graphs_.find(k);
+  auto it = finals_.find(Key{k, phase_value()});
+  auto gt = final_graphs_.find(Key{k, phase_value()});
   if (it == finals_.end() || gt == final_graphs_.end()) return false;
   size_t n = 0;
   if (hipGraphGetNodes(gt->second, nullptr, &n) != hipSuccess || n == 0) return false;
@@ -129,19 +137,31 @@ bool StepExecutor::warm_final(int k) {
 }
 
 bool StepExecutor::run_final(int k) {
-  auto it = finals_.find(k);
+  const int p = phase_value();
+  auto it = finals_.find(Key{k, p});
   if (it == finals_.end()) return false;
   HIP_CHECK(hipGraphLaunch(it->second, stream_));
+  set_phase(phase_after(p, k, true));
   return true;
 }
 
 void StepExecutor::run(int k) {
   while (k > 0) {
-    auto it = graphs_.upper_bound(k);  // first key > k
-    if (it == graphs_.begin()) break;  // no graph <= k
-    --it;
+    // the longest captured step count <= k (any phase) ...
+    int kk = 0;
+    for (auto& kv : graphs_)
+      if (kv.first.first <= k && kv.first.first > kk) kk = kv.first.first;
+    if (kk == 0) break;
+    // ... in the variant for the current phase (captured on first use)
+    const int p = phase_value();
+    auto it = graphs_.find(Key{kk, p});
+    if (it == graphs_.end()) {
+      graphs_[Key{kk, p}] = capture_steps(kk, false);
+      it = graphs_.find(Key{kk, p});
+    }
     HIP_CHECK(hipGraphLaunch(it->second, stream_));
-    k -= it->first;
+    set_phase(phase_after(p, kk, false));
+    k -= kk;
   }
   step(k);
 }

@@ -53,6 +53,9 @@ class StepExecutor {
   void restrict_cus(int part, int nparts);
   void invalidate_graphs();
   int num_graphs() const { return (int)graphs_.size(); }
+  // host-side step phase (e.g. the fused trainer's parity): graphs are captured per (k,
+  // phase) because their kernel arguments depend on it; a replay advances it
+  int phase() const { return phase_value(); }
   // (kernel nodes, all nodes) of a k-step graph, captured and discarded: the launch contract
   // of a step (e.g. two kernels per step at any world size for the fused MNIST trainer)
   std::pair<int, int> step_graph_nodes(int k);
@@ -60,15 +63,21 @@ class StepExecutor {
  protected:
   virtual void enqueue_one_step() = 0;
   virtual void enqueue_tail() {}
+  // phase bookkeeping (default: a single phase): the phase before a step, restoring it after
+  // a capture (capturing enqueues steps that do not run), and the phase after k steps (+ tail)
+  virtual int phase_value() const { return 0; }
+  virtual void set_phase(int) {}
+  virtual int phase_after(int p, int, bool) const { return p; }
   hipStream_t stream_ = nullptr;
   RcclComm* comm_ = nullptr;
   PeerAllreduce* peer_ = nullptr;
   int device_;
 
  private:
-  std::map<int, hipGraphExec_t> graphs_;
-  std::map<int, hipGraphExec_t> finals_;
-  std::map<int, hipGraph_t> final_graphs_;  // kept for the node handles (warm_final)
+  using Key = std::pair<int, int>;  // (steps, phase at the start)
+  std::map<Key, hipGraphExec_t> graphs_;
+  std::map<Key, hipGraphExec_t> finals_;
+  std::map<Key, hipGraph_t> final_graphs_;  // kept for the node handles (warm_final)
   hipGraphExec_t capture_steps(int k, bool tail, hipGraph_t* keep = nullptr);
 };
 

@@ -116,10 +116,13 @@ class FusedConvNetEngine(Engine):
         self.calt = torch.zeros(2 * NCONV, **f32)  # alternate conv parameters + velocity
         # next-batch prefetch (B <= 64): bwd copies the next step's rows here for the next fwd,
         # tagged with the ctrl block's data generation + cursor (DAMD_XPREFETCH=0: off)
-        self.xnext = self.xtag = None
+        self.xnext = self.xtag = self.xcur = self.ycur = None
         if B <= 64 and env.get_bool("DAMD_XPREFETCH", True):
             self.xnext = torch.zeros(B * 784, **f32)  # (u8 rows use the first quarter)
             self.xtag = torch.zeros(1, dtype=torch.int64, device=dev)
+            # this step's rows / labels as the fwd read them, for the bwd (no cursor needed)
+            self.xcur = torch.zeros(B * 784, **f32)
+            self.ycur = torch.zeros(B, dtype=torch.int32, device=dev)
         # model variables -> views of the fp32 master buffer (Keras weight order)
         self.vars = model.trainable_weights
         off = 0
@@ -147,7 +150,8 @@ class FusedConvNetEngine(Engine):
                     hacc=self.hacc.data_ptr(), hconv=self.hconv.data_ptr(), calt=self.calt.data_ptr(),
                     ppb=self.PPB)
         if self.xnext is not None:
-            bufs.update(xnext=self.xnext.data_ptr(), xtag=self.xtag.data_ptr())
+            bufs.update(xnext=self.xnext.data_ptr(), xtag=self.xtag.data_ptr(), xcur=self.xcur.data_ptr(),
+                        ycur=self.ycur.data_ptr())
         # world 1 (no gradient all-reduce): bwd applies the W1 update itself as soon as it
         # has the slice's gradient, and fwd reads only the bf16 copy (DAMD_EAGER_W1=0: the
         # deferred update in fwd, as with an all-reduce between the launches)

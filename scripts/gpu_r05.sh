@@ -43,6 +43,9 @@ for s in ${STAGES:-xtests bench}; do
       python scripts/dp_overlap.py "$(ls gpurun_out/prof_rn_dp/*/rn_kernel_trace.csv 2>/dev/null | head -1 || ls gpurun_out/prof_rn_dp/rn_kernel_trace.csv)" gpurun_out/dp_overlap.txt || true ;;
     ngpeer)
       step ngpeer 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_peer_allreduce_gpu.py -k native_graph ;;
+    c3deep)  # direct conv weight ring: default vs two more stages
+      step c3base 300 python scripts/conv3_probe.py 64
+      DAMD_CONV3_DEEP=1 step c3deep 300 python scripts/conv3_probe.py 64 ;;
     resnet)
       step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5 ;;
   esac

@@ -193,6 +193,9 @@ def _emulated_reference_grads(engine, model, x, y, global_batch):
     return {i: g for i, g in zip(ids, grads)}, float(loss)
 
 
+PINNED_INIT_SEED = 20240521  # the tight-bounds case of the emulated-reference test
+
+
 def test_small_resnet_step_matches_bf16_emulated_reference():
     """The plan's wiring (fusion, residual fan-in, BN backward, padding, split-K
     accumulation) against an fp32 re-execution with the same bf16 storage points: after
@@ -204,14 +207,18 @@ def test_small_resnet_step_matches_bf16_emulated_reference():
     worst layer's relative update error <= 0.262 / cosine >= 0.966 (BN gamma / beta), median
     layer <= 0.145, head <= 1.2e-2, whole update vector cosine >= 0.987 / relative error
     <= 0.160 -- heavy tails, so the bounds below leave margin for any init (three fresh draws
-    per run); exact wiring checks are the bitwise fused-vs-unfused tests."""
+    per run); exact wiring checks are the bitwise fused-vs-unfused tests.  The first case is
+    a PINNED init held to the round-3 tight bounds (a reproducible regression detector for
+    e.g. BN gamma / beta wiring), the two fresh draws to the sweep-derived ones."""
     x, y = _data(32, (32, 32, 3), 10, seed=4)
     os.environ["DAMD_FUSED"] = "0"
     try:
         for rep in range(3):
             tf.keras.backend.clear_session()
-            seed = int.from_bytes(os.urandom(4), "little")  # a fresh draw, printed for replay
-            print(f"init seed {seed}")
+            tight = rep == 0
+            # pinned, or a fresh draw printed for replay
+            seed = PINNED_INIT_SEED if tight else int.from_bytes(os.urandom(4), "little")
+            print(f"init seed {seed} ({'pinned, tight bounds' if tight else 'fresh draw'})")
             tf.set_seed(seed)
             m = _small_resnet()
             lr = 0.1
@@ -234,14 +241,16 @@ def test_small_resnet_step_matches_bf16_emulated_reference():
                 nref = d_ref.norm().item()
                 rel = (d_native - d_ref).norm().item() / max(nref, 1e-12)
                 cos = float(d_native @ d_ref / max(d_native.norm().item() * nref, 1e-30))
-                assert cos > 0.93 and rel < 0.45, f"{v.name}: rel err {rel:.4f} cos {cos:.4f} (|d| {nref:.3e})"
+                c_min, r_max = (0.97, 0.25) if tight else (0.93, 0.45)
+                assert cos > c_min and rel < r_max, f"{v.name}: rel err {rel:.4f} cos {cos:.4f} (|d| {nref:.3e})"
                 rels.append(rel)
                 dn.append(d_native)
                 dr.append(d_ref)
-            assert sorted(rels)[len(rels) // 2] < 0.25, rels
+            assert sorted(rels)[len(rels) // 2] < (0.1 if tight else 0.25), rels
             assert rels[-2] < 3e-2, rels  # the head (predictions kernel): no BN below it
             a, b = torch.cat(dn), torch.cat(dr)
-            assert float(a @ b / (a.norm() * b.norm())) > 0.97 and float((a - b).norm() / b.norm()) < 0.3
+            c_all, r_all = (0.99, 0.15) if tight else (0.97, 0.3)
+            assert float(a @ b / (a.norm() * b.norm())) > c_all and float((a - b).norm() / b.norm()) < r_all
     finally:
         os.environ.pop("DAMD_FUSED", None)
 
