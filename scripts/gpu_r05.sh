@@ -46,6 +46,10 @@ for s in ${STAGES:-xtests bench}; do
     c3deep)  # direct conv weight ring: default vs two more stages
       step c3base 300 python scripts/conv3_probe.py 64
       DAMD_CONV3_DEEP=1 step c3deep 300 python scripts/conv3_probe.py 64 ;;
+    shdiag)  # the sharded exchange at N = 2 sharing the GPU: pinned, with / without the self-test
+      DAMD_COMM=gloo DAMD_ALLREDUCE=sharded step sh_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20
+      DAMD_COMM=gloo DAMD_ALLREDUCE=sharded DAMD_XCHG_SELFTEST=0 step sh_noself 300 python bench.py --gpus 2 --steps 200 --warmup 20
+      DAMD_COMM=gloo DAMD_ALLREDUCE=xgmi step xg_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20 ;;
     resnet)
       step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5 ;;
   esac

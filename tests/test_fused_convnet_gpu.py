@@ -436,3 +436,40 @@ def test_nonfinite_weight_reports_nan_loss(where, monkeypatch):
     m.set_weights(_model(lr=0.1).get_weights())
     h = m.fit(x, y, batch_size=64, epochs=1, steps_per_epoch=2, verbose=0)
     assert np.isfinite(h.history["loss"][0])
+
+
+@pytest.mark.parametrize("B", [64, 40])
+def test_prefetch_and_parity_hints_are_bitwise_neutral(B, monkeypatch):
+    """The next-batch prefetch (bwd copies the next step's rows, tagged; the fwd stages this
+    step's rows / labels for the bwd) and the host-known step parity passed to the kernels
+    (graphs captured per parity) change only WHERE loads come from: the same bits as the
+    plain path (DAMD_XPREFETCH=0 DAMD_PAR_HINT=0), over odd-length graph replays, eager
+    steps, an epoch change (new rows: the prefetch must miss) and the final-graph path; and
+    no parity mismatch is ever flagged (ctrl.bad stays 0: the loss is finite)."""
+    _need_gpu()
+    x, y = _data(1000)  # 1000 / B: a short last batch at B = 64
+    outs = []
+    for plain in (False, True):
+        monkeypatch.setenv("DAMD_XPREFETCH", "0" if plain else "1")
+        monkeypatch.setenv("DAMD_PAR_HINT", "0" if plain else "1")
+        monkeypatch.setenv("DAMD_GRAPH_STEPS", "3")
+        m = _model(lr=0.05, momentum=0.9, seed=17)
+        eng = _engine(m, B)
+        eng.bind(x, y)
+        mets = []
+        for ep in range(2):
+            eng.start_epoch(ep, shuffle=True)
+            eng.prepare(3)
+            eng.run(7)        # 2 replays of the 3-step graph (parities 0 / 1) + 1 eager step
+            eng.trainer.step(2)
+            eng._pending = True
+            mets.append(eng.end_epoch())
+        eng.start_epoch(2, shuffle=True)
+        if eng.prepare_final(5):
+            eng.run_and_flush(5)
+        mets.append(eng.metrics())
+        eng.finish()
+        assert all(np.isfinite(mt["loss"]) for mt in mets), mets
+        outs.append((np.concatenate([w.ravel() for w in m.get_weights()]), [mt["loss"] for mt in mets]))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
