@@ -1050,13 +1050,21 @@ __global__ __launch_bounds__(1024) void flush(float* __restrict__ P, float* __re
     if (mom) V[i] = vn;
     if (w1) w1bf[i - OFF_W1] = f2bf(wn);
   }
-  // both parities of the fixed-point accumulators start the next step at zero
+  // the fixed-point accumulators start the next step at zero -- except the conv-gradient
+  // parity read above (hg): other threads / blocks of THIS launch may not have loaded it
+  // yet, and zeroing it here raced with them (a lost conv gradient on one rank, seen as
+  // replicas whose conv parameters differed after an epoch flush).  That parity needs no
+  // zero: after the flush nothing pending reads it, and the step that next writes it
+  // zeroes it first (fwd's owner block).
+  const int rp = c.wpar ^ 1;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 2 * NCONV + 2 * B * HID; i += gridDim.x * blockDim.x) {
     if (i < 2 * NCONV) {
-      hconv[i] = 0;
-      hconv_w[i] = 0;
+      const bool read_parity = i / NCONV == rp;
+      if (!read_parity) hconv[i] = 0;
+      if (!read_parity || hconv_w != hconv) hconv_w[i] = 0;
+    } else {
+      hacc[i - 2 * NCONV] = 0;
     }
-    else hacc[i - 2 * NCONV] = 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && pend) {
     ctrl->acc_loss = c.acc_loss + G[OFF_LOSS];

@@ -41,7 +41,15 @@ def main():
             kw = {"xgmi": dict(DAMD_ALLREDUCE="xgmi"), "sharded": dict(DAMD_ALLREDUCE="sharded"),
                   "injected": dict(DAMD_ALLREDUCE="auto", DAMD_XCHG_SELFTEST_INJECT="xgmi-sharded:1"),
                   "noselftest": dict(DAMD_ALLREDUCE="xgmi", DAMD_XCHG_SELFTEST="0"),
-                  "nofold": dict(DAMD_ALLREDUCE="xgmi", DAMD_PEER_FOLD="0")}[c]
+                  "nofold": dict(DAMD_ALLREDUCE="xgmi", DAMD_PEER_FOLD="0"),
+                  "sharded_nopf": dict(DAMD_ALLREDUCE="sharded", DAMD_XPREFETCH="0"),
+                  "sharded_nohint": dict(DAMD_ALLREDUCE="sharded", DAMD_PAR_HINT="0"),
+                  "sharded_plain": dict(DAMD_ALLREDUCE="sharded", DAMD_PAR_HINT="0", DAMD_XPREFETCH="0"),
+                  "xgmi_plain": dict(DAMD_ALLREDUCE="xgmi", DAMD_PAR_HINT="0", DAMD_XPREFETCH="0"),
+                  "sharded_nograph": dict(DAMD_ALLREDUCE="sharded", DAMD_GRAPH="0"),
+                  "xgmi_nograph": dict(DAMD_ALLREDUCE="xgmi", DAMD_GRAPH="0"),
+                  "sharded_nopc": dict(DAMD_ALLREDUCE="sharded", DEBUG_CLR_GRAPH_PACKET_CAPTURE="0"),
+                  "xgmi_nopc": dict(DAMD_ALLREDUCE="xgmi", DEBUG_CLR_GRAPH_PACKET_CAPTURE="0")}[c]
             r = run(td / f"{c}{i}", DAMD_TEST_INIT_FROM=init, **kw)
             if r is None:
                 print(c, "FAILED to run", flush=True)
