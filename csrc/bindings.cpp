@@ -119,8 +119,7 @@ class ConvNetTrainer : public StepExecutor {
         throw std::invalid_argument("peer all-reduce capacity too small for the folded step");
       b_.G = p->in_local();
       // the conv-gradient int64 sums stay in the engine's own (cached) buffer: bwd adds into
-      // them with atomics, which must not target the uncached staging (measured: replicas
-      // diverged in the conv parameters now and then); the peer kernel copies them in
+      // them with atomics, kept off the uncached staging; the peer kernel copies them in
       b_.hconv = hconv_own_;
       b_.Gr = p->out_local();
       b_.hconv_r = reinterpret_cast<long long*>(p->out_local() + nfp);
