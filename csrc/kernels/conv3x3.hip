@@ -371,17 +371,6 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
 
 template <int BN>
 constexpr int conv3_stages() { return BN == 64 ? 4 : 3; }
-// DAMD_CONV3_DEEP=1: two more weight stages (a deeper ring, fewer blocks per CU when the LDS
-// no longer fits two) -- an A/B switch for the latency-hiding question
-static int conv3_deep() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("DAMD_CONV3_DEEP");
-    v = (e && e[0] == '1') ? 1 : 0;
-  }
-  return v;
-}
-
 int halo_bytes_of(int R, int W) { return (((R + 2) * (W + 2)) * 128 + 1023) & ~1023; }
 
 template <int BN, bool DG, int EPI, int ST>
@@ -418,9 +407,11 @@ hipError_t launch3_st(const GemmArgs& a, int R, hipStream_t s) {
   return hipGetLastError();
 }
 
+// (two more weight stages -- a deeper ring, one block per CU where two no longer fit --
+// measured slower in round 5: layer-3 forward 39.1 -> 40.2 us, backprop-input 27.8 -> 29.9
+// us; scripts/conv3_probe.py)
 template <int BN, bool DG, int EPI>
 hipError_t launch3(const GemmArgs& a, int R, hipStream_t s) {
-  if (conv3_deep()) return launch3_st<BN, DG, EPI, conv3_stages<BN>() + 2>(a, R, s);
   return launch3_st<BN, DG, EPI, conv3_stages<BN>()>(a, R, s);
 }
 

@@ -40,12 +40,20 @@ for s in ${STAGES:-xtests bench}; do
       step gprobe 300 python scripts/probe_graph_branches.py 4 8 ;;
     dpprof)  # ResNet-18 N = 2 sharing the GPU: bucket all-reduce overlap (peer transport)
       step dpprof 500 bash scripts/prof_resnet_dp.sh
-      python scripts/dp_overlap.py "$(ls gpurun_out/prof_rn_dp/*/rn_kernel_trace.csv 2>/dev/null | head -1 || ls gpurun_out/prof_rn_dp/rn_kernel_trace.csv)" gpurun_out/dp_overlap.txt || true ;;
+      python scripts/dp_overlap.py gpurun_out/prof_rn_dp/rn_kernel_trace.csv gpurun_out/dp_overlap.txt || true ;;
     ngpeer)
       step ngpeer 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_peer_allreduce_gpu.py -k native_graph ;;
-    c3deep)  # direct conv weight ring: default vs two more stages
-      step c3base 300 python scripts/conv3_probe.py 64
-      DAMD_CONV3_DEEP=1 step c3deep 300 python scripts/conv3_probe.py 64 ;;
+    c3)  # direct conv kernels on the ResNet-18 shapes
+      step c3base 300 python scripts/conv3_probe.py 64 ;;
+    mab)  # MNIST step A/B on one box: prefetch + parity hints on / off, alternating
+      for i in 1 2; do
+        step mab_on$i 200 python bench.py --gpus 1 --steps 20 --warmup 5
+        DAMD_XPREFETCH=0 DAMD_PAR_HINT=0 step mab_off$i 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      done
+      step mab_on_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      DAMD_XPREFETCH=0 DAMD_PAR_HINT=0 step mab_off_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      DAMD_XPREFETCH=0 DAMD_PAR_HINT=0 step stamps_off 200 python scripts/stamps.py 64
+      step stamps_on 200 python scripts/stamps.py 64 ;;
     shdiag)  # the sharded exchange at N = 2 sharing the GPU: pinned, with / without the self-test
       DAMD_COMM=gloo DAMD_ALLREDUCE=sharded step sh_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20
       DAMD_COMM=gloo DAMD_ALLREDUCE=sharded DAMD_XCHG_SELFTEST=0 step sh_noself 300 python bench.py --gpus 2 --steps 200 --warmup 20
