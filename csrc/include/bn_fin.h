@@ -21,15 +21,15 @@ __device__ inline void acc_sums(const long long* acc, int reps, int C, int c, do
   s = bnacc_value1(ws);
   q = bnacc_value1(wq);
 }
-// Backward sums: acc[r][2][C][2] (hi, lo words), the same way.
+// Backward sums: acc[r][4][C] (planes: sum hi, sum lo, second hi, second lo), the same way.
 __device__ inline void acc_sums2(const long long* acc, int reps, int C, int c, double& s, double& q) {
   long long sh = 0, sl = 0, qh = 0, ql = 0;
   for (int r = 0; r < max(reps, 1); ++r) {
     const long long* a = acc + (size_t)r * 4 * C;
-    sh += a[2 * c];
-    sl += a[2 * c + 1];
-    qh += a[2 * (C + c)];
-    ql += a[2 * (C + c) + 1];
+    sh += a[c];
+    sl += a[C + c];
+    qh += a[2 * C + c];
+    ql += a[3 * C + c];
   }
   s = bnacc_value2(sh, sl);
   q = bnacc_value2(qh, ql);

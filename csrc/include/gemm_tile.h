@@ -208,9 +208,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
         if (a.stats_acc) {
           const size_t rep = a.stats_reps > 1 ? tm % a.stats_reps : 0;
           if constexpr (EPI & E_BNRED) {  // BN-backward sums: two words per value
-            long long* acc = a.stats_acc + rep * 4 * a.N;
-            bnacc_add2(acc + 2 * n, s);
-            bnacc_add2(acc + 2 * (a.N + n), q);
+            long long* acc = a.stats_acc + rep * 4 * a.N;  // hi / lo planes
+            bnacc_add2(acc + n, acc + a.N + n, s);
+            bnacc_add2(acc + 2 * a.N + n, acc + 3 * a.N + n, q);
           } else {  // forward statistics: one word per value
             long long* acc = a.stats_acc + rep * 2 * a.N;
             bnacc_add1(acc + n, s);

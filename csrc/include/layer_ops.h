@@ -32,7 +32,7 @@ struct BNFin {
   int reps;            // replicas of acc (0 / 1: one)
 };
 struct BNBwdFin {
-  const long long* acc;  // [reps][2][C][2 words] sum dz, sum dz * xhat (bnacc_add2); null: reads co
+  const long long* acc;  // [reps][4][C] sum dz / sum dz * xhat, hi / lo planes (bnacc_add2); null: co
   float* dgamma;       // += (block 0), may be null
   float* dbeta;
   float* co;           // [3][C] out (block 0)

@@ -257,20 +257,23 @@ def acc_reps(acc):
 # Fixed-point BatchNorm accumulators (csrc/include/damd_common.h bnacc_add1 / bnacc_add2):
 # integer atomics, so the statistics are bitwise independent of the producer blocks'
 # arrival order.  Forward sums: one int64 word per value (unit 2^-24); backward sums: two
-# (hi = floor(v 2^24), lo = floor((v 2^24 - hi) 2^40)).
+# (hi = floor(v 2^24), lo = floor((v 2^24 - hi) 2^40)) in planes [s hi | s lo | q hi | q lo].
 ACC_UNIT = 2.0 ** -24
 
 
 def bn_acc_encode(values: torch.Tensor, words: int = 1) -> torch.Tensor:
-    """Host encoding of fp64 sums into accumulator words (tests / diagnostics): [..., K]
-    doubles -> [..., K] (words 1) or [..., 2K] (words 2, (hi, lo) interleaved) int64."""
+    """Host encoding of fp64 sums into accumulator words (tests / diagnostics): [..., 2C]
+    doubles (sums, second statistics) -> [..., 2C] (words 1) or [..., 4C] (words 2: planes
+    s hi | s lo | q hi | q lo) int64."""
     v = values.double().cpu()
     if words == 1:
         return torch.round(v * 2.0 ** 24).to(torch.int64)
     d = v * 2.0 ** 24
     hi = torch.floor(d)
     lo = torch.floor((d - hi) * 2.0 ** 40)
-    return torch.stack([hi.to(torch.int64), lo.to(torch.int64)], -1).reshape(*v.shape[:-1], 2 * v.shape[-1])
+    C = v.shape[-1] // 2
+    parts = [hi[..., :C], lo[..., :C], hi[..., C:], lo[..., C:]]
+    return torch.cat([p.to(torch.int64) for p in parts], -1)
 
 
 def bn_acc_decode(acc: torch.Tensor, words: int = 1) -> torch.Tensor:
@@ -281,8 +284,10 @@ def bn_acc_decode(acc: torch.Tensor, words: int = 1) -> torch.Tensor:
     a = a.sum(0)
     if words == 1:
         return a.double() * ACC_UNIT
-    a = a.view(-1, 2)
-    return a[:, 0].double() * ACC_UNIT + a[:, 1].double() * 2.0 ** -64
+    C = a.numel() // 4
+    s = a[:C].double() * ACC_UNIT + a[C:2 * C].double() * 2.0 ** -64
+    q = a[2 * C:3 * C].double() * ACC_UNIT + a[3 * C:].double() * 2.0 ** -64
+    return torch.cat([s, q])
 
 
 def _stats_ptrs(stats):

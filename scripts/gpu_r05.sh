@@ -59,7 +59,10 @@ for s in ${STAGES:-xtests bench}; do
       DAMD_COMM=gloo DAMD_ALLREDUCE=sharded DAMD_XCHG_SELFTEST=0 step sh_noself 300 python bench.py --gpus 2 --steps 200 --warmup 20
       DAMD_COMM=gloo DAMD_ALLREDUCE=xgmi step xg_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20 ;;
     resnet)
-      step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5 ;;
+      step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5
+      step resnet_long 300 python bench.py --model resnet18 --steps 100 --warmup 10 ;;
+    rnprof)
+      step rnprof 400 bash scripts/prof_resnet.sh ;;
   esac
 done
 echo stages-done
