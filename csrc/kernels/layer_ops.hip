@@ -7,6 +7,8 @@
 // 16-byte vector of 8 channels (global_load_dwordx4) and keeps the 8 per-channel
 // parameters in registers.  Statistics are reduced in fp32 per block (LDS), then across
 // blocks in double by a finalize kernel (deterministic, no atomics on the hot reductions).
+#include <cstdlib>
+
 #include "bn_fin.h"
 #include "damd_common.h"
 #include "layer_ops.h"
@@ -1740,8 +1742,17 @@ hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const
 }
 
 int bn_bwd_blocks(long M, int C) {
+  // target grid (DAMD_BN_BWD_BLOCKS, default 512): fewer blocks = fewer per-block partials
+  // added into the fixed-point accumulators (4 atomics per channel and block).  ResNet-18
+  // step, one box: 1024 blocks 2.736 ms, 512 2.718, 256 2.757
+  static long target = 0;
+  if (!target) {
+    const char* e = getenv("DAMD_BN_BWD_BLOCKS");
+    target = e ? atol(e) : 512;
+    if (target < 64) target = 512;
+  }
   const int rpi = NT / (C / 8);
-  long rows = (M + 1023) / 1024;
+  long rows = (M + target - 1) / target;
   if (rows < rpi) rows = rpi;
   return (int)((M + rows - 1) / rows);
 }

@@ -61,6 +61,10 @@ for s in ${STAGES:-xtests bench}; do
     resnet)
       step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5
       step resnet_long 300 python bench.py --model resnet18 --steps 100 --warmup 10 ;;
+    bnab)  # bn_bwd_reduce grid size A/B (fixed-point accumulator atomics vs memory parallelism)
+      for t in 1024 512 256; do
+        DAMD_BN_BWD_BLOCKS=$t step rn_bnt$t 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done ;;
     rnprof)
       step rnprof 400 bash scripts/prof_resnet.sh ;;
   esac
