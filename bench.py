@@ -264,12 +264,15 @@ def main():
     # config 3's "RCCL ring all-reduce" gets its own number on the same ranks.
     transports = {}
     model, engine = None, None
+    keep = []  # every candidate engine stays alive until the end: no destructor (device syncs,
+    # IPC unmaps, frees) may run inside a timed window
     tune = (n > 1 and args.model == "mnist" and args.engine in ("auto", "fused") and "DAMD_ALLREDUCE" not in os.environ
             and os.environ.get("DAMD_BENCH_TUNE", "1") != "0" and args.steps > 0)
     if tune:
         best = None
         for cand in ("sharded", "xgmi", "rccl"):
             m_c, e_c = make_engine(cand)
+            keep.append((m_c, e_c))
             kind = getattr(e_c, "allreduce_kind", cand)
             if e_c.name != "fused_convnet" or kind in transports:
                 continue  # fell back onto a transport already measured
@@ -290,6 +293,9 @@ def main():
              and os.environ.get("DAMD_BENCH_FINAL_GRAPH", "1") != "0" and engine.prepare_final(args.steps))
     run(engine, args.warmup)
     engine.sync()
+    import gc
+
+    gc.collect()  # nothing left for the collector to finalize inside the window
     dt = timed(engine, args.steps, final)
     phases = engine.phase_times(args.phases) if args.phases > 0 else None
     m = engine.metrics()
