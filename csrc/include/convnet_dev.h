@@ -21,10 +21,12 @@ constexpr int OFF_LOSS = NPARAM, OFF_CORR = NPARAM + 1, OFF_CNT = NPARAM + 2;
 constexpr int NGRAD = NPARAM + 6;            // padded to 16 B: 347152
 constexpr int NSMALL = HID + HID * NCLS + NCLS;  // b1, W2, b2 contiguous: 714
 constexpr int CH = 64;                       // images per chunk
+constexpr int LG_CH = 6;                     // log2(CH)
 constexpr int XR = 6;                        // staged input rows per image
 constexpr int MAXPP = 4;                     // max pooled positions per fwd / bwd block
 constexpr int XS_BYTES = CH * XR * IMG * 4;  // 43008
 constexpr int HP = 72;                       // bf16 pitch of 64-wide tiles (conflict-free)
+static_assert(CH == 1 << LG_CH, "chunk size");
 static_assert(NPARAM == kConvNetNParam && NGRAD == kConvNetNGrad, "param count");
 
 __host__ __device__ constexpr int kpitch(int pp) { return pp * 32 + 8; }
@@ -40,51 +42,51 @@ __device__ __forceinline__ int next_cursor(const Ctrl& c, int cur) {
 }
 
 // ---- staged input rows: registers first (loads in flight early), LDS later ------------
-// One unit = 16 B (fp32) or 4 B (u8) of an input row; `off` is its LDS float offset in the
-// [nimg][XR][28] staging tile, computed once at load time (-1: no unit for this thread).
+// A block stages rows [r0, r0 + nrows) of nimg = 2^lgi images (16 or 64) into the
+// [nimg][XR][28] LDS tile.  One unit = 4 pixels: 4 B (u8) or 16 B (fp32).  Thread t owns
+// column unit q = t & 7 (q = 7: idle) of rows rg, rg + RG, ... of image t >> (9 - lgi),
+// where 512 / nimg threads share an image in RG = 2^(6 - lgi) row groups (64 images: all 6
+// rows per thread; 16: rows rg, rg + 4).  Shifts only: the former linear unit index took a
+// division per unit -- ~20 VALU each, quarter-rate multiplies among them -- and the
+// prologue of both step kernels is VALU-issue bound (two waves per SIMD, wave64 over 16
+// lanes: 4 clocks per VALU instruction).
 template <bool U8>
 struct XStage;
 template <>
 struct XStage<true> {
-  uint32_t w[6];
-  int off[6];
+  uint32_t w[XR];
+  int off, rg;  // LDS float offset of (image, row rg, unit q), -1: idle lane; row group
 };
 template <>
 struct XStage<false> {
-  float4 v[6];
-  int off[6];
+  float4 v[XR];
+  int off, rg;
 };
-// Input rows [r0, r0+nrows) of images b < nimg (valid if b < nvalid and row_base+b <
-// nsamples).  U8: the dataset is kept as uint8 (inputs that are exactly k/255, e.g.
-// MNIST) -- 4x fewer bytes -- and k/255.f (correctly rounded, == float32(k/255.0)) is
-// formed when staging; otherwise fp32 rows.
+// Images b < nvalid with row_base + b < nsamples are loaded, others staged as zeros.
+// U8: the dataset is kept as uint8 (inputs that are exactly k/255, e.g. MNIST) -- 4x fewer
+// bytes -- and k/255.f (correctly rounded, == float32(k/255.0)) is formed when staging;
+// otherwise fp32 rows.  32-bit sample indices and byte offsets (the engine keeps the
+// dataset below 2^31 bytes), so the loads take the scalar-base + 32-bit-offset form.
 template <bool U8>
 __device__ __forceinline__ void x_load(XStage<U8>& st, const void* __restrict__ X, long row_base, int nsamples,
-                                       int nvalid, int nimg, int r0, int nrows) {
-  const int per_img = nrows * 7, total = nimg * per_img;
-  // i / per_img through a float reciprocal (exact here: i < 3072, per_img <= 42, so the
-  // quotient's fraction stays >= 0.5 / per_img away from an integer, far above the float
-  // error): an integer division by a runtime divisor is ~30 instructions per unit
-  const float rinv = 1.f / (float)per_img;
-  // 32-bit sample indices and byte offsets (the engine keeps the dataset below 2^31 bytes):
-  // 64-bit clamps and multiplies doubled the address math of every unit
-  const int rb = (int)row_base;
+                                       int nvalid, int lgi, int r0, int nrows) {
+  const int t = (int)threadIdx.x, sh = 9 - lgi, b = t >> sh, rg = (t & ((1 << sh) - 1)) >> 3, q = t & 7;
+  const int RG = 1 << (6 - lgi);
+  const int g = (int)row_base + b;
+  const bool ok = b < nvalid && g < nsamples && q < 7;
+  st.off = q < 7 ? (b * XR + rg) * IMG + 4 * q : -1;
+  st.rg = rg;
+  // element offset of (row r0 + rg, unit q); rows advance by RG * IMG elements
+  const unsigned eo = __umul24((unsigned)max(0, min(g, nsamples - 1)), (unsigned)NPIX) + (unsigned)((r0 + rg) * IMG + 4 * q);
 #pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    const int idx = (int)threadIdx.x + u * 512;
-    const int i = min(idx, total - 1);
-    const int b = (int)(((float)i + 0.5f) * rinv), rem = i - b * per_img, r = rem / 7, q = rem - r * 7;
-    const int g = rb + b;
-    const bool ok = idx < total && b < nvalid && g < nsamples;
-    const int gs = max(0, min(g, nsamples - 1));
-    const unsigned eo = (unsigned)(gs * NPIX + (r0 + r) * IMG);  // element offset of the row
-    st.off[u] = idx < total ? (b * XR + r) * IMG + 4 * q : -1;
-    if constexpr (U8) {
-      const uint32_t w = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + (eo + 4u * q));
-      st.w[u] = ok ? w : 0u;
-    } else {
-      const float4 v = *reinterpret_cast<const float4*>(static_cast<const char*>(X) + (4u * eo + 16u * q));
-      st.v[u] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < XR; ++j) {
+    if constexpr (U8) st.w[j] = 0u;
+    else st.v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (j * RG >= XR) continue;  // (uniform)
+    if (ok && rg + j * RG < nrows) {
+      const unsigned e = eo + (unsigned)(j * RG * IMG);
+      if constexpr (U8) st.w[j] = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + e);
+      else st.v[j] = *reinterpret_cast<const float4*>(static_cast<const char*>(X) + 4u * e);
     }
   }
 }
@@ -97,22 +99,23 @@ __device__ __forceinline__ float u8_over_255(uint32_t k) {
   const float r = 1.f / 255.f, x = (float)k, q = x * r;
   return fmaf(fmaf(-q, 255.f, x), r, q);
 }
-// (lut: unused, kept for the callers that still stage a k / 255 table)
 template <bool U8>
-__device__ __forceinline__ void x_store(const XStage<U8>& st, float* xs, const float* lut = nullptr) {
-  (void)lut;
+__device__ __forceinline__ void x_store(const XStage<U8>& st, float* xs, int lgi, int nrows) {
+  const int RG = 1 << (6 - lgi);
+  if (st.off < 0) return;
 #pragma unroll
-  for (int u = 0; u < 6; ++u) {
-    if (st.off[u] >= 0) {
+  for (int j = 0; j < XR; ++j) {
+    if (j * RG >= XR) continue;  // (uniform)
+    if (st.rg + j * RG < nrows) {
       float4 v;
       if constexpr (U8) {
-        const uint32_t w = st.w[u];
+        const uint32_t w = st.w[j];
         v = make_float4(u8_over_255(w & 0xff), u8_over_255((w >> 8) & 0xff), u8_over_255((w >> 16) & 0xff),
                         u8_over_255(w >> 24));
       } else {
-        v = st.v[u];
+        v = st.v[j];
       }
-      *reinterpret_cast<float4*>(xs + st.off[u]) = v;
+      *reinterpret_cast<float4*>(xs + st.off + j * RG * IMG) = v;
     }
   }
 }
@@ -217,7 +220,14 @@ __device__ __forceinline__ long long to_fix(float v, float scale, int* bad) {
   }
   return (long long)__builtin_rintf(q);
 }
-__device__ __forceinline__ float from_fix(long long q, double inv) { return (float)((double)q * inv); }
+// fixed point -> float as high word * 2^32 + unsigned low word in one fma: f32 only (the
+// former (float)((double)q * inv) took ~6 half-rate f64 instructions per value, and the
+// head converts 8 per thread); within ~1 ulp of the exact value (the low word's rounding
+// is at most 2^-25 of 2^32 units), deterministic.  inv is a power of two.
+__device__ __forceinline__ float from_fix(long long q, double inv) {
+  const float fi = (float)inv;
+  return fmaf((float)(int)(q >> 32), fi * 4294967296.f, (float)(unsigned)q * fi);
+}
 
 __device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {
   __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(p), (unsigned long long)v, __ATOMIC_RELAXED,

@@ -174,7 +174,7 @@ __device__ __forceinline__ bool last_arriver(int* counter, int nblocks, int* fla
 // and written once at kernel end (a mid-kernel store makes hipcc wait vmcnt(0) and
 // distorts what it measures).  `st` is null unless DAMD_STAMPS is set on the host.
 struct Stamps {
-  unsigned long long t[12];
+  unsigned long long t[13];
 };
 __device__ __forceinline__ void stamp(Stamps& s, unsigned long long* st, int idx) {
   if (st != nullptr) s.t[idx] = __builtin_amdgcn_s_memrealtime();

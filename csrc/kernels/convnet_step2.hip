@@ -145,7 +145,6 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   uint16_t* as = reinterpret_cast<uint16_t*>(smem + IB * XR * IMG * 4);    // [IB][KP] pooled tile
   uint16_t* w1t = as + IB * KP;                                            // [HID][KP] W1 slice^T
   float* cw = reinterpret_cast<float*>(w1t + HID * KP);                    // [320] conv params
-  const float* lut = nullptr;  // (x_store converts k / 255 arithmetically)
   const int n4 = K * HID / 4;  // <= 2048
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
@@ -154,7 +153,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   XStage<U8> xst;
   long long xt = 0;
   if (xnext != nullptr) {
-    x_load<U8>(xst, xnext, img0, B, B - img0, IB, r0, nrows);
+    x_load<U8>(xst, xnext, img0, B, B - img0, lg, r0, nrows);
     xt = *xtag;
   }
   // ---- first the loads whose addresses do not depend on the ctrl block: the bf16 W1 slice
@@ -198,7 +197,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // ---- then the ctrl-dependent loads: the batch rows unless prefetched (and, deferred
   // update, W1 by parity) ----
   const bool xhit = xnext != nullptr && xt == (((long long)c.xgen << 32) | (long long)(unsigned)(c.cursor + 1));
-  if (!xhit) x_load<U8>(xst, X, row_base, c.nsamples, B - img0, IB, r0, nrows);
+  if (!xhit) x_load<U8>(xst, X, row_base, c.nsamples, B - img0, lg, r0, nrows);
   // this step's rows and labels for the backward (xcur / ycur): a share per block, from the
   // prefetch when it hit (L2-hot), else from the dataset; stored at the end of the kernel
   constexpr int UPI = U8 ? NPIX / 16 : NPIX / 4;  // 16-byte units per image
@@ -212,7 +211,8 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
       const int b = xcu / UPI, q = xcu - b * UPI;
       if (xhit) xcv = reinterpret_cast<const uint4*>(xnext)[xcu];
       else if (rb0 + b < c.nsamples)
-        xcv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + (rb0 + b) * (U8 ? NPIX : 4 * NPIX))[q];
+        xcv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) +
+                                             __umul24((unsigned)(rb0 + b), U8 ? NPIX : 4 * NPIX))[q];
     }
     if (xcur != nullptr && lin == 0 && tid < B && rb0 + tid < c.nsamples) ycv = labels[rb0 + tid];
   }
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     hconv[par * NCONV + tid] = 0;
   }
   stamp(sts, st, 1);
-  x_store<U8>(xst, xs, lut);
+  x_store<U8>(xst, xs, lg, nrows);
   lds_barrier();
   stamp(sts, st, 2);
 
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     uint16_t v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = as[(bo + e) * KP + kk];
-    uint16_t* dst = pooled + (long)(p0 * NF + kk) * BP + img0 + bo;
+    uint16_t* dst = pooled + (unsigned)((p0 * NF + kk) * BP + img0 + bo);
     if (img0 + bo + 3 < B) {
       *reinterpret_cast<uint2*>(dst) = make_uint2((uint32_t)v[0] | ((uint32_t)v[1] << 16),
                                                  (uint32_t)v[2] | ((uint32_t)v[3] << 16));
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   for (int i = tid; i < IB * (K / 4); i += 512) {
     const int bo = i / (K / 4), w = i - bo * (K / 4);
     if (img0 + bo < B)
-      *reinterpret_cast<uint32_t*>(code + (long)(img0 + bo) * FEAT + p0 * NF + 4 * w) =
+      *reinterpret_cast<uint32_t*>(code + (unsigned)((img0 + bo) * FEAT + p0 * NF + 4 * w)) =
           reinterpret_cast<const uint32_t*>(csl + bo * K)[w];
   }
   if (sh) {
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // one wave instruction = one 512-B row of 64 int64 adds
   long long* hp = hacc + (long)par * B * HID;
   for (int r = wave; r < (hprobe == 1 ? 0 : hprobe == 2 ? IB / 2 : IB); r += 8)
-    if (img0 + r < B) atomic_add_i64(hp + (long)(img0 + r) * HID + lane, to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
+    if (img0 + r < B) atomic_add_i64(hp + (unsigned)((img0 + r) * HID + lane), to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
   if (xcp) reinterpret_cast<uint4*>(xcur)[xcu] = xcv;
   if (xcur != nullptr && lin == 0 && tid < B) ycur[tid] = ycv;
   stamp(sts, st, 4);
@@ -533,7 +533,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
                                            unsigned long long* st, const float* __restrict__ Gr, const XArgs xa,
                                            void* __restrict__ xnext, long long* __restrict__ xtag,
-                                           const void* __restrict__ xcur, const int* __restrict__ ycur, int phint) {
+                                           const void* __restrict__ xcur, const int* __restrict__ ycur, int phint,
+                                           int auxm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   constexpr int cprobe = DAMD_PROBE_HCONV;  // 0 in every product build (see the top of the file)
@@ -560,16 +561,16 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   float* rc = rl + CH;             // [CH] per-row correct
   float* db1p = rc + CH;           // [16][64] db1 partials
   int* ylds = reinterpret_cast<int*>(db1p + 16 * HID);  // [CH] label of the row, -1 if invalid
-  const float* lut = nullptr;  // (x_store converts k / 255 arithmetically)
   const int r0 = 2 * (p0 / PO);
   const int nrows = 2 * ((p1 - 1) / PO) + 4 - r0;
   const int wave = tid >> 6, lane = tid & 63;
   const int ko = 8 * (lane >> 4), lr16 = lane & 15;
 
   // ---- this block's aux elements ----
-  const int chunk_aux = (NAUX2 + NS - 1) / NS;
-  const int tpe = max(1, min(512 / chunk_aux, 64));  // threads per aux element
-  const int ae_local = tid / tpe, aq = tid - ae_local * tpe;
+  // (auxm, from the host: chunk_aux | log2(threads per element) << 16 -- the divisions
+  // that derive them from the grid cost ~40 VALU of the prologue on the device)
+  const int chunk_aux = auxm & 0xffff, ltpe = auxm >> 16, tpe = 1 << ltpe;
+  const int ae_local = tid >> ltpe, aq = tid & (tpe - 1);
   const int ae = s * chunk_aux + ae_local;
   const bool aux_on = ae_local < chunk_aux && ae < NAUX2;
   const int aec = min(ae, NAUX2 - 1);
@@ -589,7 +590,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   auto load_hq = [&](int chunk, int p) __attribute__((always_inline)) {
     const int r = tid >> 3, q = tid & 7;
     const int row = min(chunk * CH + r, B - 1);
-    const uint4* hp = reinterpret_cast<const uint4*>(hacc + (long)p * B * HID + (long)row * HID + q * 8);
+    const uint4* hp = reinterpret_cast<const uint4*>(hacc + (unsigned)((p * B + row) * HID + q * 8));
     hq0 = hp[0];
     hq1 = hp[1];
     hq2 = hp[2];
@@ -607,23 +608,29 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   int ylab = 0;
   bool yval = false;
   const int BP = (B + CH - 1) / CH * CH;
-  const int kc = K / 16;
+  const int kc = K / 16;  // = 2 np, np in 1..MAXPP
+  // i / kc for i < 512 without a division sequence: (i / 2) / np, np = 3 by a multiply
+  auto div_kc = [&](int i) __attribute__((always_inline)) {
+    return np == 3 ? (int)(((unsigned)(i >> 1) * 21846u) >> 16) : (i >> 1) >> (np >> 1);
+  };
+  static_assert(MAXPP == 4, "div_kc covers np = 1..4");
   auto load_indep = [&](int chunk) __attribute__((always_inline)) {
     {
       const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
-      pv0 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i0 >> 3)) * BP + chunk * CH + (i0 & 7) * 8);
-      pv1 = *reinterpret_cast<const uint4*>(pooled + (long)(p0 * NF + (i1 >> 3)) * BP + chunk * CH + (i1 & 7) * 8);
+      // (32-bit element offsets: the pooled tile is FEAT x BP bf16, far below 2^31)
+      pv0 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i0 >> 3), BP) + chunk * CH + (i0 & 7) * 8));
+      pv1 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i1 >> 3), BP) + chunk * CH + (i1 & 7) * 8));
     }
     {
-      const int i = tid, bb = i / kc, q = i - bb * kc, lb = chunk * CH + bb;
+      const int i = tid, bb = div_kc(i), q = i - bb * kc, lb = chunk * CH + bb;
       cok = i < CH * kc && lb < B;
-      cv = *reinterpret_cast<const uint4*>(code + (long)min(lb, B - 1) * FEAT + p0 * NF + min(q, kc - 1) * 16);
+      cv = *reinterpret_cast<const uint4*>(code + (__umul24(min(lb, B - 1), FEAT) + p0 * NF + min(q, kc - 1) * 16));
     }
     if (ycur != nullptr) {  // labels and rows as this step's fwd read them: no cursor needed
       const int b = chunk * CH + min(tid, CH - 1);
       ylab = ycur[min(b, B - 1)];
       yval = tid < CH && b < B && ylab >= 0;
-      x_load<U8>(xst, xcur, chunk * CH, B, B - chunk * CH, CH, r0, nrows);
+      x_load<U8>(xst, xcur, chunk * CH, B, B - chunk * CH, LG_CH, r0, nrows);
     }
   };
   load_indep(0);
@@ -664,7 +671,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
         yval = tid < CH && b < B && g < c.nsamples;
         ylab = labels[max(0L, min(g, (long)c.nsamples - 1))];
       }
-      x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, CH, r0, nrows);
+      x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, LG_CH, r0, nrows);
     }
   };
   auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
@@ -684,10 +691,10 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     if (tid < K * 8) *reinterpret_cast<uint4*>(pt + (tid >> 3) * HP + (tid & 7) * 8) = pv0;
     if (tid + 512 < K * 8) *reinterpret_cast<uint4*>(pt + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = pv1;
     if (tid < CH * kc) {
-      const int bb = tid / kc, q = tid - bb * kc;
+      const int bb = div_kc(tid), q = tid - bb * kc;
       *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cok ? cv : make_uint4(0u, 0u, 0u, 0u);
     }
-    x_store<U8>(xst, xs, lut);
+    x_store<U8>(xst, xs, LG_CH, nrows);
   };
   auto store_chunk = [&](int chunk) __attribute__((always_inline)) {
     store_body();
@@ -697,9 +704,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   // the next step's rows for its fwd (issued after this step's own loads: in-order vmcnt)
   if (xpf) {
     const int b = xpu / UPI, q = xpu - b * UPI;
-    const long g = (long)ncur * c.global_batch + c.row0 + b;
+    const int g = (int)((long)ncur * c.global_batch + c.row0) + b;  // (dataset < 2^31 bytes: 32-bit)
     if (g < c.nsamples)
-      xnv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + g * (U8 ? NPIX : 4 * NPIX))[q];
+      xnv = reinterpret_cast<const uint4*>(static_cast<const char*>(X) + __umul24((unsigned)g, U8 ? NPIX : 4 * NPIX))[q];
   }
   // (w1s is read only by the dP MFMAs, several barriers later)
   if (tid < n8) *reinterpret_cast<uint4*>(w1s + (tid >> 3) * HP + (tid & 7) * 8) = wv0;
@@ -714,7 +721,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   // ---- sharded exchange: this wave's dW1 tiles form half of unit u = 4 s + dn (rows of
   // tiles dm0 + 2 i, 16 columns), owned by rank u % world ----
   const int NU = 4 * NS, xu = 4 * s + dn;
-  const int xo = sh ? xu % xa.world : 0;
+  const int xo = !sh ? 0 : (xa.world & (xa.world - 1)) == 0 ? xu & (xa.world - 1) : xu % xa.world;
   const bool xown = sh && xo == xa.rank;
   auto push_partials = [&]() __attribute__((always_inline)) {
     if (!sh || xown) return;
@@ -753,11 +760,14 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       for (int i = 0; i < MAXPP; ++i) {
         if (i >= np) break;
         const int mt = dm0 + 2 * i;
+        // (one address per tile, the 4 rows at immediate offsets)
+        const unsigned e0 = OFF_W1 + (unsigned)((p0 * 32 + 16 * mt + 4 * (lane >> 4)) * HID + 16 * dn + lr16);
+        const float* pw = Pw + e0;
+        const float* vw = Vw + e0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const long e = OFF_W1 + (long)(p0 * 32 + 16 * mt + 4 * (lane >> 4) + j) * HID + 16 * dn + lr16;
-          ew[i][j] = Pw[e];
-          ev[i][j] = mom ? Vw[e] : 0.f;
+          ew[i][j] = pw[j * HID];
+          ev[i][j] = mom ? vw[j * HID] : 0.f;
         }
       }
     }
@@ -777,7 +787,10 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     }
     lds_barrier();
     stamp(sts, st, 6);
-    if (ONE && wave >= 4) store_body();  // (waves 4-7 have no logits to compute)
+    if (ONE && wave >= 4) {  // (waves 4-7 have no logits to compute)
+      store_body();
+      stamp(sts, st, 12);
+    }
     // logits on f32 MFMA (wave mt: rows 16 mt .. 16 mt + 15, 16 columns, 10 used), then
     // softmax-xent / accuracy / dz over each row's 16 lanes (DPP row reductions); the four
     // rows j of a lane are independent chains, interleaved
@@ -790,7 +803,13 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
         av[ks] = hs[(16 * mt + lr) * HPITCH + k];
         bv[ks] = spl[HID + k * NCLS + min(lr, NCLS - 1)];
       }
+      // the labels of this lane's 4 rows, read with the operands (read after the softmax, they
+      // were 4 serial LDS round trips on the critical path)
+      int yv4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) yv4[j] = ylds[16 * mt + 4 * kq + j];
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (ONE) stamp(sts, st, 9);  // (sub-phase stamps, single chunk: wave 0's view)
 #pragma unroll
       for (int ks = 0; ks < HID / 4; ++ks) acc = mfma4(av[ks], lr < NCLS ? bv[ks] : 0.f, acc);
       const float b2v = lr < NCLS ? spl[HID + HID * NCLS + lr] : 0.f;
@@ -804,15 +823,17 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       for (int j = 0; j < 4; ++j) e[j] = lr < NCLS ? __expf(v[j] - m[j]) : 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) e[j] = row16_sum(e[j]);
+      if (ONE) stamp(sts, st, 10);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         lse[j] = m[j] + __logf(e[j]);
         am[j] = row16_min(v[j] == m[j] ? lr : 16);
       }
+      if (ONE) stamp(sts, st, 11);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 16 * mt + 4 * kq + j;
-        const int yv = ylds[r];
+        const int yv = yv4[j];
         const bool valid = yv >= 0;
         const int y = valid ? yv : 0;
         if (lr < NCLS) zs[r * ZP + lr] = valid ? (__expf(v[j] - lse[j]) - (lr == y ? 1.f : 0.f)) * inv : 0.f;
@@ -820,7 +841,10 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
         if (lr == 0) rc[r] = (valid && am[j] == y) ? 1.f : 0.f;
       }
     }
-    if (ONE && wave < 4) store_body();
+    if (ONE && wave < 4) {
+      store_body();
+      stamp(sts, st, 12);
+    }
     lds_barrier();
     stamp(sts, st, 7);
     // dh = (dz W2^T) * [h > 0] on f32 MFMA: 16 tiles of 16x16, two per wave, K = 10 (three
@@ -904,14 +928,17 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
       for (int i = 0; i < MAXPP; ++i) {
         if (i >= np) break;
         const int mt = dm0 + 2 * i;
+        const unsigned e0 = OFF_W1 + (unsigned)((p0 * 32 + 16 * mt + 4 * (lane >> 4)) * HID + 16 * dn + lr16);
+        float* pw = Pw + e0;
+        float* vw = Vw + e0;
+        uint16_t* bw = w1bf_out + (e0 - OFF_W1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const long e = OFF_W1 + (long)(p0 * 32 + 16 * mt + 4 * (lane >> 4) + j) * HID + 16 * dn + lr16;
           float wn, vn;
           sgd_update(ew[i][j], accw[i][j], ev[i][j], c.lr, c.momentum, c.nesterov, wn, vn);
-          Pw[e] = wn;
-          if (mom) Vw[e] = vn;
-          w1bf_out[e - OFF_W1] = f2bf(wn);
+          pw[j * HID] = wn;
+          if (mom) vw[j * HID] = vn;
+          bw[j * HID] = f2bf(wn);
         }
       }
     }
@@ -968,7 +995,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = 16 * mt + 4 * (lane >> 4) + j;
-      G[OFF_W1 + (long)(p0 * 32 + k) * HID + 16 * dn + lr16] = accw[i][j];
+      G[OFF_W1 + (unsigned)((p0 * 32 + k) * HID + 16 * dn + lr16)] = accw[i][j];
     }
   }
   lds_barrier();  // pt/dht region becomes `red`, dps becomes `ared`
@@ -1014,7 +1041,8 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   if (ONE && xnext != nullptr && s == 0 && tid == 0) *xtag = ((long long)c.xgen << 32) | (long long)(unsigned)(ncur + 1);
   if (sh) exchange_tail(xa, ctrl, G, hconv + par * NCONV, accw, xe, s, NS, np, p0, dn, dm0, lane, tid, xown, xo, xu);
   stamp(sts, st, 5);
-  stamp_flush(sts, st, 9);
+  stamp_flush(sts, st, 13);
+  if (st != nullptr && tid == 256) st[blockIdx.x * 16 + 13] = sts.t[12];  // wave 4's view
 }
 
 // =================================================================================
@@ -1191,20 +1219,26 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
   using namespace convnet;
   const int PP = ppb_of(b, PPf);
   const int NS = convnet_num_slices(PP);
+  // aux elements (b1/W2/b2 gradients + metric tail) per block, and a power-of-two thread
+  // count per element (<= 64) that fits them in 512 threads
+  const int chunk_aux = (convnet2::NAUX2 + NS - 1) / NS;
+  int ltpe = 0;
+  while (ltpe < 6 && (2 << ltpe) * chunk_aux <= 512) ++ltpe;
+  const int auxm = chunk_aux | (ltpe << 16);
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
                        b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
                        xargs(b), b.xnext, b.xtag, B <= CH ? b.xcur : nullptr, B <= CH ? b.ycur : nullptr,
-                       b.par_hint);
+                       b.par_hint, auxm);
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
                        b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
                        eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
                        xargs(b), b.xnext, b.xtag, B <= CH ? b.xcur : nullptr, B <= CH ? b.ycur : nullptr,
-                       b.par_hint);
+                       b.par_hint, auxm);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
