@@ -291,12 +291,24 @@ def main():
     # fused engine: the K timed steps and the final flush as one graph (setup, untimed)
     final = (engine.name == "fused_convnet" and 0 < args.steps <= 64
              and os.environ.get("DAMD_BENCH_FINAL_GRAPH", "1") != "0" and engine.prepare_final(args.steps))
-    run(engine, args.warmup)
-    engine.sync()
     import gc
 
-    gc.collect()  # nothing left for the collector to finalize inside the window
+    # nothing left for the collector to finalize inside the window -- collected BEFORE the
+    # warmup: a collection right before the window left the host's caches cold for the
+    # graph launch (first window +2 us/step at K = 20 against the same window repeated)
+    gc.collect()
+    run(engine, args.warmup)
+    engine.sync()
     dt = timed(engine, args.steps, final)
+    # diagnostics only (stderr, never the reported value): DAMD_BENCH_EXTRA=n repeats the
+    # warmup + timed window n more times, to separate a first-window cost from the steady one
+    for _ in range(int(os.environ.get("DAMD_BENCH_EXTRA", "0"))):
+        if final:
+            engine.prepare_final(args.steps)  # (the variant for the current step phase)
+        run(engine, args.warmup)
+        engine.sync()
+        print(f"[bench] extra window: {timed(engine, args.steps, final) * 1e3 / args.steps:.5f} ms/step",
+              file=sys.stderr, flush=True)
     phases = engine.phase_times(args.phases) if args.phases > 0 else None
     m = engine.metrics()
     # MirrorCheck after the window: every rank holds bitwise the same parameters

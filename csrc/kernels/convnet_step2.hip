@@ -162,9 +162,15 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   // and waited for it with the kernel arguments, then sank these below further waits) ----
   uint4 bq[2];  // eager: the bf16 W1 slice (bwd already applied the update)
   if (eager) {
+    // (lanes past the slice load nothing: at PP = 2 the second unit is all out of range, and
+    // its clamped duplicate loads were 8 KB per block of wasted load bandwidth.  Written as a
+    // conditional load, not a select between pointers: hipcc turns the latter into a flat
+    // load from a zero vector in scratch)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-      bq[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + u * 512, n4 / 2 - 1)];
+    for (int u = 0; u < 2; ++u) {
+      bq[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (tid + u * 512 < n4 / 2) bq[u] = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[tid + u * 512];
+    }
   }
   // conv parameters: current buffer by parity; their gradient is the previous step's
   // (bwd added it into hconv[par ^ 1])
@@ -582,7 +588,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   // previous step's reduced metric (sharded: fwd folds it from the small messages)
   const float ag_old = sh ? 0.f : Gr[OFF_LOSS + max(0, min(aec - NSMALL, 2))];
   // small parameters (b1/W2/b2, updated by fwd): 2 per thread, re-staged every chunk
-  const float spv0 = P[OFF_B1 + tid], spv1 = P[OFF_B1 + min(tid + 512, NSMALL - 1)];
+  const float spv0 = P[OFF_B1 + tid];
+  float spv1 = 0.f;
+  if (tid + 512 < NSMALL) spv1 = P[OFF_B1 + tid + 512];
   uint4 hq0, hq1, hq2, hq3;  // hacc row (tid >> 3), columns 8 (tid & 7) .. + 8
   // known parity (single chunk): the head's first operand -- this step's dense-1 sums --
   // right behind b1 / W2 / b2, before the ctrl block
@@ -599,8 +607,12 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   if (hq_early) load_hq(0, phint);
   const int n8 = K * HID / 8;
   uint4 wv0, wv1;
-  wv0 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid, n8 - 1)];
-  wv1 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[min(tid + 512, n8 - 1)];
+  // (only in-range units are loaded: clamped duplicates cost load bandwidth -- at PP = 2 the
+  // whole second unit is out of range)
+  // (conditional loads, not selects between pointers: see fwd's bq)
+  wv0 = wv1 = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < n8) wv0 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[tid];
+  if (tid + 512 < n8) wv1 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[tid + 512];
   XStage<U8> xst;
   uint4 pv0, pv1;
   uint4 cv;                  // argmax codes, zeroed at the LDS store unless cok
@@ -618,8 +630,11 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     {
       const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
       // (32-bit element offsets: the pooled tile is FEAT x BP bf16, far below 2^31)
-      pv0 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i0 >> 3), BP) + chunk * CH + (i0 & 7) * 8));
-      pv1 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i1 >> 3), BP) + chunk * CH + (i1 & 7) * 8));
+      pv0 = pv1 = make_uint4(0u, 0u, 0u, 0u);
+      if (tid < K * 8)
+        pv0 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i0 >> 3), BP) + chunk * CH + (i0 & 7) * 8));
+      if (tid + 512 < K * 8)
+        pv1 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i1 >> 3), BP) + chunk * CH + (i1 & 7) * 8));
     }
     {
       const int i = tid, bb = div_kc(i), q = i - bb * kc, lb = chunk * CH + bb;
