@@ -232,6 +232,8 @@ def main():
         else:
             eng.run(k)
 
+    diag_extra = int(os.environ.get("DAMD_BENCH_EXTRA", "0")) > 0
+
     def timed(eng, k, final):
         """Seconds for k full steps (the last deferred SGD update included), bracketed by a
         barrier + device synchronize on both sides, max over ranks."""
@@ -244,6 +246,8 @@ def main():
             run(eng, k)
             if eng.name == "fused_convnet":
                 eng._flush()  # the last deferred SGD update is part of the timed work
+        if diag_extra:
+            print(f"[bench] host launch call {(time.perf_counter() - t0) * 1e6:.1f} us", file=sys.stderr)
         if not on_gpu:
             eng.sync()
         # on the GPU the device-wide synchronize waits for every stream, the engines' own

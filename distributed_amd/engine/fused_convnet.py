@@ -434,7 +434,8 @@ class FusedConvNetEngine(Engine):
             # one replay with every node disabled: the graph's first-launch cost (~9 us
             # measured, scripts/probe_cold_graph.py) is paid here, outside the timed window.
             # A graph whose nodes cannot be toggled is only not pre-warmed.
-            self.trainer.warm_final(int(n_steps))
+            if env.get_bool("DAMD_WARM_FINAL", True):
+                self.trainer.warm_final(int(n_steps))
         except RuntimeError as e:
             dlog.warning("final-graph capture unavailable (%s): timed run replays step graphs + flush", e)
             return False

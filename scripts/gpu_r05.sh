@@ -35,7 +35,7 @@ for s in ${STAGES:-xtests bench}; do
     fused)
       step fused 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_convnet_gpu.py ;;
     bextra)  # the bench's window repeated (stderr): first-window vs steady cost at K = 20
-      DAMD_BENCH_EXTRA=6 step bench_extra 200 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+      DAMD_BENCH_EXTRA=3 step bench_extra 200 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     ovh)  # fixed cost of a timed window (launch, flush, sync): fit over K
       step overhead 300 python scripts/overhead_probe.py ;;
     stamps)
