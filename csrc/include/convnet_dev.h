@@ -67,10 +67,11 @@ struct XStage<false> {
 // bytes -- and k/255.f (correctly rounded, == float32(k/255.0)) is formed when staging;
 // otherwise fp32 rows.  32-bit sample indices and byte offsets (the engine keeps the
 // dataset below 2^31 bytes), so the loads take the scalar-base + 32-bit-offset form.
+// t: the staging slot (thread index by default; a block may give one thread two slots)
 template <bool U8>
 __device__ __forceinline__ void x_load(XStage<U8>& st, const void* __restrict__ X, long row_base, int nsamples,
-                                       int nvalid, int lgi, int r0, int nrows) {
-  const int t = (int)threadIdx.x, sh = 9 - lgi, b = t >> sh, rg = (t & ((1 << sh) - 1)) >> 3, q = t & 7;
+                                       int nvalid, int lgi, int r0, int nrows, int t = (int)threadIdx.x) {
+  const int sh = 9 - lgi, b = t >> sh, rg = (t & ((1 << sh) - 1)) >> 3, q = t & 7;
   const int RG = 1 << (6 - lgi);
   const int g = (int)row_base + b;
   const bool ok = b < nvalid && g < nsamples && q < 7;

@@ -58,7 +58,7 @@ using namespace convnet;
 
 constexpr int NAUX2 = NSMALL + 3;               // b1/W2/b2 gradients + [loss, correct, count]
 constexpr int HPITCH = HID + 1;                 // fp32 pitch of the h tile in LDS
-constexpr int ZP = 11;                          // pitch of the logit / dz rows
+constexpr int ZP = 17;                          // pitch of the logit / dz rows (16 lanes store, odd: no conflicts)
 constexpr int HEAD_FLOATS = CH * HPITCH + 716 + CH * ZP + 2 * CH + 16 * HID + CH;
 constexpr int HEAD_BYTES = HEAD_FLOATS * 4;
 
@@ -613,10 +613,18 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   wv0 = wv1 = make_uint4(0u, 0u, 0u, 0u);
   if (tid < n8) wv0 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[tid];
   if (tid + 512 < n8) wv1 = reinterpret_cast<const uint4*>(w1bf + p0 * 32 * HID)[tid + 512];
-  XStage<U8> xst;
-  uint4 pv0, pv1;
-  uint4 cv;                  // argmax codes, zeroed at the LDS store unless cok
-  bool cok = false;
+  // the body -- pooled tile, argmax codes, input rows, read only by the MFMAs and the conv
+  // gradient -- is staged by NB threads with two slots each: all 512 when chunked; in the
+  // single-chunk step only waves 4-7 (slots bt and bt + 256), which have no logits to
+  // compute and store it while waves 0-3 run the logits / softmax (staged by waves 0-3 too,
+  // it sat on the head's critical path)
+  constexpr int NB = ONE ? 256 : 512;
+  const int bt = ONE ? tid - 256 : tid;  // (< 0: no body slots)
+  const bool bw = !ONE || bt >= 0;
+  XStage<U8> xst, xst1;      // input rows: slot bt, and (single chunk) bt + 256
+  uint4 pv0, pv1, pv2, pv3;  // pooled tile units bt + j NB (K * 8 <= 1024 units)
+  uint4 cv, cv1;             // argmax codes, units bt (+ NB), zeroed at the LDS store unless cok
+  bool cok = false, cok1 = false;
   int ylab = 0;
   bool yval = false;
   const int BP = (B + CH - 1) / CH * CH;
@@ -626,26 +634,37 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     return np == 3 ? (int)(((unsigned)(i >> 1) * 21846u) >> 16) : (i >> 1) >> (np >> 1);
   };
   static_assert(MAXPP == 4, "div_kc covers np = 1..4");
+  // (32-bit element offsets: the pooled tile is FEAT x BP bf16, far below 2^31; only
+  // in-range units load -- conditional loads, not pointer selects, see fwd's bq)
+  auto load_pv = [&](uint4& v, int i, int chunk) __attribute__((always_inline)) {
+    v = make_uint4(0u, 0u, 0u, 0u);
+    if (i < K * 8) v = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i >> 3), BP) + chunk * CH + (i & 7) * 8));
+  };
+  auto load_cv = [&](uint4& v, bool& ok, int i, int chunk) __attribute__((always_inline)) {
+    const int bb = div_kc(i), q = i - bb * kc, lb = chunk * CH + bb;
+    ok = i < CH * kc && lb < B;
+    v = make_uint4(0u, 0u, 0u, 0u);
+    if (i < CH * kc) v = *reinterpret_cast<const uint4*>(code + (__umul24(min(lb, B - 1), FEAT) + p0 * NF + q * 16));
+  };
   auto load_indep = [&](int chunk) __attribute__((always_inline)) {
-    {
-      const int i0 = min(tid, K * 8 - 1), i1 = min(tid + 512, K * 8 - 1);
-      // (32-bit element offsets: the pooled tile is FEAT x BP bf16, far below 2^31)
-      pv0 = pv1 = make_uint4(0u, 0u, 0u, 0u);
-      if (tid < K * 8)
-        pv0 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i0 >> 3), BP) + chunk * CH + (i0 & 7) * 8));
-      if (tid + 512 < K * 8)
-        pv1 = *reinterpret_cast<const uint4*>(pooled + (__umul24(p0 * NF + (i1 >> 3), BP) + chunk * CH + (i1 & 7) * 8));
-    }
-    {
-      const int i = tid, bb = div_kc(i), q = i - bb * kc, lb = chunk * CH + bb;
-      cok = i < CH * kc && lb < B;
-      cv = *reinterpret_cast<const uint4*>(code + (__umul24(min(lb, B - 1), FEAT) + p0 * NF + min(q, kc - 1) * 16));
+    if (bw) {
+      load_pv(pv0, bt, chunk);
+      load_pv(pv1, bt + NB, chunk);
+      if (ONE) {
+        load_pv(pv2, bt + 2 * NB, chunk);
+        load_pv(pv3, bt + 3 * NB, chunk);
+      }
+      load_cv(cv, cok, bt, chunk);
+      if (ONE) load_cv(cv1, cok1, bt + NB, chunk);
     }
     if (ycur != nullptr) {  // labels and rows as this step's fwd read them: no cursor needed
       const int b = chunk * CH + min(tid, CH - 1);
       ylab = ycur[min(b, B - 1)];
       yval = tid < CH && b < B && ylab >= 0;
-      x_load<U8>(xst, xcur, chunk * CH, B, B - chunk * CH, LG_CH, r0, nrows);
+      if (bw) {
+        x_load<U8>(xst, xcur, chunk * CH, B, B - chunk * CH, LG_CH, r0, nrows, bt);
+        if (ONE) x_load<U8>(xst1, xcur, chunk * CH, B, B - chunk * CH, LG_CH, r0, nrows, bt + NB);
+      }
     }
   };
   load_indep(0);
@@ -686,7 +705,10 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
         yval = tid < CH && b < B && g < c.nsamples;
         ylab = labels[max(0L, min(g, (long)c.nsamples - 1))];
       }
-      x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, LG_CH, r0, nrows);
+      if (bw) {
+        x_load<U8>(xst, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, LG_CH, r0, nrows, bt);
+        if (ONE) x_load<U8>(xst1, X, row_base + chunk * CH, c.nsamples, B - chunk * CH, LG_CH, r0, nrows, bt + NB);
+      }
     }
   };
   auto load_chunk = [&](int chunk) __attribute__((always_inline)) {
@@ -702,14 +724,27 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     if (tid + 512 < NSMALL) spl[tid + 512] = spv1;
     if (tid < CH) ylds[tid] = yval ? ylab : -1;
   };
-  auto store_body = [&]() __attribute__((always_inline)) {
-    if (tid < K * 8) *reinterpret_cast<uint4*>(pt + (tid >> 3) * HP + (tid & 7) * 8) = pv0;
-    if (tid + 512 < K * 8) *reinterpret_cast<uint4*>(pt + ((tid + 512) >> 3) * HP + (tid & 7) * 8) = pv1;
-    if (tid < CH * kc) {
-      const int bb = div_kc(tid), q = tid - bb * kc;
-      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = cok ? cv : make_uint4(0u, 0u, 0u, 0u);
+  auto store_pv = [&](const uint4& v, int i) __attribute__((always_inline)) {
+    if (i < K * 8) *reinterpret_cast<uint4*>(pt + (i >> 3) * HP + (i & 7) * 8) = v;
+  };
+  auto store_cv = [&](const uint4& v, bool ok, int i) __attribute__((always_inline)) {
+    if (i < CH * kc) {
+      const int bb = div_kc(i), q = i - bb * kc;
+      *reinterpret_cast<uint4*>(cs + bb * KC + q * 16) = ok ? v : make_uint4(0u, 0u, 0u, 0u);
     }
+  };
+  auto store_body = [&]() __attribute__((always_inline)) {
+    if (!bw) return;
+    store_pv(pv0, bt);
+    store_pv(pv1, bt + NB);
+    if (ONE) {
+      store_pv(pv2, bt + 2 * NB);
+      store_pv(pv3, bt + 3 * NB);
+    }
+    store_cv(cv, cok, bt);
+    if (ONE) store_cv(cv1, cok1, bt + NB);
     x_store<U8>(xst, xs, LG_CH, nrows);
+    if (ONE) x_store<U8>(xst1, xs, LG_CH, nrows);
   };
   auto store_chunk = [&](int chunk) __attribute__((always_inline)) {
     store_body();
@@ -802,7 +837,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     }
     lds_barrier();
     stamp(sts, st, 6);
-    if (ONE && wave >= 4) {  // (waves 4-7 have no logits to compute)
+    if (ONE && wave >= 4) {  // (waves 4-7 stage the whole body: see NB above)
       store_body();
       stamp(sts, st, 12);
     }
@@ -839,27 +874,30 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
 #pragma unroll
       for (int j = 0; j < 4; ++j) e[j] = row16_sum(e[j]);
       if (ONE) stamp(sts, st, 10);
+      // log-sum-exp: the sum is in [1, 10], so the hardware log2 (v_log_f32) is accurate here;
+      // __logf's denormal-safe expansion was ~15 instructions per row on the critical path
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        lse[j] = m[j] + __logf(e[j]);
+        lse[j] = m[j] + __builtin_amdgcn_logf(e[j]) * 0.693147180559945f;
         am[j] = row16_min(v[j] == m[j] ? lr : 16);
       }
       if (ONE) stamp(sts, st, 11);
+      // dz for all 16 lanes of a row (lanes >= NCLS: v = -inf, so 0 -- the padding of the
+      // zs row), no per-store exec masks; the label's lane writes the row's loss and hit
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 16 * mt + 4 * kq + j;
         const int yv = yv4[j];
         const bool valid = yv >= 0;
         const int y = valid ? yv : 0;
-        if (lr < NCLS) zs[r * ZP + lr] = valid ? (__expf(v[j] - lse[j]) - (lr == y ? 1.f : 0.f)) * inv : 0.f;
-        if (lr == y) rl[r] = valid ? (lse[j] - v[j]) : 0.f;
-        if (lr == 0) rc[r] = (valid && am[j] == y) ? 1.f : 0.f;
+        zs[r * ZP + lr] = valid ? (__expf(v[j] - lse[j]) - (lr == y ? 1.f : 0.f)) * inv : 0.f;
+        if (lr == y) {
+          rl[r] = valid ? (lse[j] - v[j]) : 0.f;
+          rc[r] = (valid && am[j] == y) ? 1.f : 0.f;
+        }
       }
     }
-    if (ONE && wave < 4) {
-      store_body();
-      stamp(sts, st, 12);
-    }
+    if (ONE && wave < 4) stamp(sts, st, 12);
     lds_barrier();
     stamp(sts, st, 7);
     // dh = (dz W2^T) * [h > 0] on f32 MFMA: 16 tiles of 16x16, two per wave, K = 10 (three

@@ -36,7 +36,7 @@ def main():
     grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, eng.trainer.num_slices_bwd)}
     names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued"],
              "bwd": ["start", "loads staged", "head done", "mfma", "convgrad", "end", "h", "softmax", "dh",
-                     "logit operands", "logit mfma+max/sum", "lse/argmax", "w0 body stored",
+                     "logit operands", "logit mfma+max/sum", "lse/argmax", "w0 softmax stored",
                      "w4 body stored"]}
     t0 = None
     for kn, (k, n) in grids.items():
