@@ -139,22 +139,29 @@ struct ConvFrag {
 };
 __device__ __forceinline__ void conv_setup(ConvFrag& f, const float* cw, int lane) {
   const int kg = lane >> 4;
+  // slot k = 8 kg + j: tap (8 kg + j) mod 9 = (j - kg) mod 9; the x-lo slots (part 1, k in
+  // [9, 18)), w-lo slots (part 2, [18, 27)) and zero slots (k >= 27) of group kg as bit masks
+  // over j -- shifts and selects, not the divisions by 9 and 3 (~10 VALU per slot, sunk by
+  // hipcc into the conv loop)
+  const unsigned xlo = (0x0003FE00u >> (8 * kg)) & 0xffu, wlo = (0x07FC0000u >> (8 * kg)) & 0xffu;
+  const unsigned zer = kg == 3 ? 0xF8u : 0u;
+  int tapj[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
-    f.toff[j] = (tap / 3) * IMG + (tap % 3);
-    f.lomask[j] = part == 1 ? 0xffffu : 0u;
-    f.zmask[j] = k >= 27 ? 0u : 0xffffu;
+    const int t = j - kg;
+    tapj[j] = t < 0 ? t + 9 : t;
+    f.toff[j] = tapj[j] + (IMG - 3) * ((tapj[j] * 11) >> 5);  // (tap / 3) * IMG + tap % 3, tap < 9
+    f.lomask[j] = (xlo >> j) & 1u ? 0xffffu : 0u;
+    f.zmask[j] = (zer >> j) & 1u ? 0u : 0xffffu;
   }
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     s16x8 t;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 8 * kg + j, part = k / 9, tap = k - 9 * part;
-      const float w32 = cw[min(tap, 8) * NF + 16 * nt + (lane & 15)];
+      const float w32 = cw[tapj[j] * NF + 16 * nt + (lane & 15)];
       const uint32_t hi = f2bf(w32), lo = bf16_lo(w32, (uint16_t)hi);
-      const uint32_t wlomask = part == 2 ? 0xffffu : 0u;
+      const uint32_t wlomask = (wlo >> j) & 1u ? 0xffffu : 0u;
       t[j] = (short)((hi ^ ((hi ^ lo) & wlomask)) & f.zmask[j]);
     }
     f.w[nt] = __builtin_bit_cast(bf16x8, t);

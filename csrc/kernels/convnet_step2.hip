@@ -342,11 +342,13 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
 
   ConvFrag cf;
   conv_setup(cf, cw, lane);
+  stamp(sts, st, 5);
   uint8_t* csl = reinterpret_cast<uint8_t*>(cw + NCONV);  // [IB][K] argmax codes
   conv_pool(cf, xs, p0, np, r0, lg, wave, lane, [&](int bo, int plo, int ch, uint16_t hb, uint8_t cd) {
     as[bo * KP + plo * 32 + ch] = hb;
     csl[bo * K + plo * 32 + ch] = cd;
   });
+  stamp(sts, st, 6);
   lds_barrier();
   stamp(sts, st, 3);
   // pooled tile (feature-major [k][b]: bwd's dW1 operand) and argmax codes ([b][k]) for
@@ -372,6 +374,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
       *reinterpret_cast<uint32_t*>(code + (unsigned)((img0 + bo) * FEAT + p0 * NF + 4 * w)) =
           reinterpret_cast<const uint32_t*>(csl + bo * K)[w];
   }
+  stamp(sts, st, 7);
   if (sh) {
     // sharded: the slice's reduced dW1 arrives as 4 units (2 halves each) from their owners,
     // pushed at the end of every owner's bwd -- waited for only now, after the conv
@@ -409,7 +412,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
 #pragma unroll
     for (int j = 0; j < 4; ++j) part[(16 * mt + 4 * (lane >> 4) + j) * HID + bn] = acc[j];
   }
+  stamp(sts, st, 8);
   lds_barrier();
+  stamp(sts, st, 9);
   // one wave instruction = one 512-B row of 64 int64 adds
   long long* hp = hacc + (long)par * B * HID;
   for (int r = wave; r < (hprobe == 1 ? 0 : hprobe == 2 ? IB / 2 : IB); r += 8)
@@ -418,7 +423,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   if (xcur != nullptr && lin == 0 && tid < B) ycur[tid] = ycv;
   stamp(sts, st, 4);
   if (st != nullptr && tid == 0 && lin < 256)
-    for (int i = 0; i < 5; ++i) st[lin * 16 + i] = sts.t[i];
+    for (int i = 0; i < 10; ++i) st[lin * 16 + i] = sts.t[i];
 }
 
 // =================================================================================

@@ -43,6 +43,10 @@ for s in ${STAGES:-xtests bench}; do
         step ab_A_short$i 200 bash -c "cd build/ab/A && python bench.py --gpus 1 --steps 20 --warmup 5"
         step ab_B_short$i 200 python bench.py --gpus 1 --steps 20 --warmup 5
       done ;;
+    ppsweep)  # slice sizes: fwd positions per block (DAMD_PP) x bwd (DAMD_PP_BWD), long runs
+      for pp in 2 3 4; do for pb in 1 2 3; do
+        DAMD_PP=$pp DAMD_PP_BWD=$pb step pp_${pp}_${pb} 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      done; done ;;
     ovh)  # fixed cost of a timed window (launch, flush, sync): fit over K
       step overhead 300 python scripts/overhead_probe.py ;;
     stamps)

@@ -34,7 +34,8 @@ def main():
     st = eng.stamps.cpu().numpy()
     NS = eng.trainer.num_slices
     grids = {"fwd": (0, NS * ((B + 15) // 16)), "bwd": (2, eng.trainer.num_slices_bwd)}
-    names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued"],
+    names = {"fwd": ["start", "loads+sgd", "xs staged", "conv done", "atomics issued", "conv setup", "conv pool",
+                     "pooled/code out", "dense-1 mfma", "dense-1 barrier"],
              "bwd": ["start", "loads staged", "head done", "mfma", "convgrad", "end", "h", "softmax", "dh",
                      "logit operands", "logit mfma+max/sum", "lse/argmax", "w0 softmax stored",
                      "w4 body stored"]}
