@@ -35,7 +35,10 @@ for s in ${STAGES:-xtests bench}; do
     fused)
       step fused 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_convnet_gpu.py ;;
     bextra)  # the bench's window repeated (stderr): first-window vs steady cost at K = 20
-      DAMD_BENCH_EXTRA=3 step bench_extra 200 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+      DAMD_BENCH_EXTRA=3 step bench_extra 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      DAMD_GRAPH_STEPS=5 DAMD_BENCH_EXTRA=3 step bench_extra_g5 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      DAMD_BENCH_EXTRA=3 step bench_extra_b 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      DAMD_GRAPH_STEPS=5 DAMD_BENCH_EXTRA=3 step bench_extra_g5b 200 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     ab)  # same-box A/B: build/ab/A (scripts/ab_build.sh) against the working tree, alternating
       for i in 1 2 3; do
         step ab_A_long$i 200 bash -c "cd build/ab/A && python bench.py --gpus 1 --steps 2000 --warmup 200"
