@@ -267,6 +267,7 @@ def main():
     # metric steps; the fastest carries the measured run.  This is also where BASELINE
     # config 3's "RCCL ring all-reduce" gets its own number on the same ranks.
     transports = {}
+    failed_selftest = []  # candidate transports whose start-up self-test failed (skipped)
     model, engine = None, None
     keep = []  # every candidate engine stays alive until the end: no destructor (device syncs,
     # IPC unmaps, frees) may run inside a timed window
@@ -274,8 +275,17 @@ def main():
             and os.environ.get("DAMD_BENCH_TUNE", "1") != "0" and args.steps > 0)
     if tune:
         best = None
+        from distributed_amd.engine.fused_convnet import ExchangeSelfTestError
+
         for cand in ("sharded", "xgmi", "rccl"):
-            m_c, e_c = make_engine(cand)
+            try:
+                m_c, e_c = make_engine(cand)
+            except ExchangeSelfTestError as e:
+                # every rank raises (the self-test outcome is voted), so every rank skips
+                # this candidate; the headline run goes on with the transports that passed
+                print(f"[bench] transport {cand} skipped: {e}", file=sys.stderr, flush=True)
+                failed_selftest.append(cand)
+                continue
             keep.append((m_c, e_c))
             kind = getattr(e_c, "allreduce_kind", cand)
             if e_c.name != "fused_convnet" or kind in transports:
@@ -374,6 +384,8 @@ def main():
             out["fallback_from"] = fb
             if transports:
                 out["transport_ms_per_step"] = transports
+            if failed_selftest:
+                out["transports_failed_selftest"] = failed_selftest
             out["rccl_ms_per_step"] = transports.get("rccl", round(dt * 1e3 / args.steps, 5)
                                                      if getattr(engine, "allreduce_kind", "") == "rccl" else None)
         if phases is not None:

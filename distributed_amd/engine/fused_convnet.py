@@ -24,6 +24,12 @@ from ..utils import logging as dlog
 from .base import Engine
 from .data import DataFeed
 
+
+class ExchangeSelfTestError(RuntimeError):
+    """A pinned device gradient exchange (DAMD_ALLREDUCE=xgmi | sharded) failed its start-up
+    self-test (engine/xchg_selftest.py).  Raised on EVERY rank (the outcome is a collective
+    vote), so a caller may catch it and go on with another transport consistently."""
+
 NPARAM = 347146
 NGRAD = 347152
 HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
@@ -246,7 +252,7 @@ class FusedConvNetEngine(Engine):
                     chosen = cands[0]
                 if chosen is None:
                     if mode in ("xgmi", "sharded"):
-                        raise RuntimeError(f"DAMD_ALLREDUCE={mode}: the exchange failed its start-up self-test")
+                        raise ExchangeSelfTestError(f"DAMD_ALLREDUCE={mode}: the exchange failed its start-up self-test")
                     dlog.warning("fused ConvNet engine: no xGMI exchange passed its self-test; using %s",
                                  "RCCL" if native is not None else "the host (gloo) all-reduce")
                     self.peer = None
