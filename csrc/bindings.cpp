@@ -237,6 +237,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("CONVNET_NCONV") = kConvNetNConv;
   m.def("convnet2_lds_bytes", [](int PP) { return py::make_tuple(convnet2_fwd_lds(PP, 4), convnet2_bwd_lds(PP)); });
   m.def("convnet_num_slices", &convnet_num_slices);
+  m.def("convnet_hacc_elems", &convnet_hacc_elems);
   m.def("convnet_grad_count", &convnet_grad_count);
 
   m.def("device_count", []() { int n = 0; if (hipGetDeviceCount(&n) != hipSuccess) n = 0; return n; });

@@ -42,7 +42,7 @@ struct ConvNetBuffers {
   uint16_t* pooled /* [5408][BP] */; uint8_t* code /* [B][5408] */;
   unsigned long long* stamps;  // optional [3][256][16] phase stamps (diagnostics), may be null
   // fixed-point accumulators of the cross-block sums
-  long long* hacc;   // [2][B][64] dense-1 pre-activations x 2^32, by step parity
+  long long* hacc;   // [2][B] rows of 64 dense-1 pre-activations x 2^32 (pitch HACC_PITCH), by step parity
   long long* hconv;  // [2][320] conv weight/bias gradient x 2^40, by step parity (both all-reduced)
   float* calt;       // [2][320] alternate conv parameters / velocity (double buffer by parity)
   // no gradient all-reduce (world 1): bwd applies the W1 update as soon as its block has
@@ -82,6 +82,7 @@ constexpr int kConvNetNConv = 320;
 constexpr int kConvNetNParam = 347146;
 constexpr int kConvNetNGrad = 347152;
 int convnet_num_slices(int PP);
+long convnet_hacc_elems(int B);
 int convnet_f1_lg(int B);
 size_t convnet2_fwd_lds(int PP, int lg);
 size_t convnet2_bwd_lds(int PP);

@@ -22,11 +22,20 @@ constexpr int NGRAD = NPARAM + 6;            // padded to 16 B: 347152
 constexpr int NSMALL = HID + HID * NCLS + NCLS;  // b1, W2, b2 contiguous: 714
 constexpr int CH = 64;                       // images per chunk
 constexpr int LG_CH = 6;                     // log2(CH)
+// dense-1 accumulator row pitch (int64 elements): one 512-B row of 64 sums per image.
+// Contiguous (64) is the default: rows 4 KB apart, to spread the forward's 57-deep
+// same-address atomic chains over more memory channels, measured +1.1 us per step (the
+// backward started 0.95 us later; same-box A/B, round 5)
+#ifndef DAMD_HACC_PITCH
+#define DAMD_HACC_PITCH 64
+#endif
+constexpr int HACC_PITCH = DAMD_HACC_PITCH;
 constexpr int XR = 6;                        // staged input rows per image
 constexpr int MAXPP = 4;                     // max pooled positions per fwd / bwd block
 constexpr int XS_BYTES = CH * XR * IMG * 4;  // 43008
 constexpr int HP = 72;                       // bf16 pitch of 64-wide tiles (conflict-free)
 static_assert(CH == 1 << LG_CH, "chunk size");
+static_assert(HACC_PITCH >= 64 && HACC_PITCH % 64 == 0, "hacc pitch");
 static_assert(NPARAM == kConvNetNParam && NGRAD == kConvNetNGrad, "param count");
 
 __host__ __device__ constexpr int kpitch(int pp) { return pp * 32 + 8; }

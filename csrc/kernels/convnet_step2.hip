@@ -416,9 +416,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   lds_barrier();
   stamp(sts, st, 9);
   // one wave instruction = one 512-B row of 64 int64 adds
-  long long* hp = hacc + (long)par * B * HID;
+  long long* hp = hacc + (long)par * B * HACC_PITCH;
   for (int r = wave; r < (hprobe == 1 ? 0 : hprobe == 2 ? IB / 2 : IB); r += 8)
-    if (img0 + r < B) atomic_add_i64(hp + (unsigned)((img0 + r) * HID + lane), to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
+    if (img0 + r < B) atomic_add_i64(hp + (unsigned)((img0 + r) * HACC_PITCH + lane), to_fix(part[r * HID + lane], HSCALE, &ctrl->bad));
   if (xcp) reinterpret_cast<uint4*>(xcur)[xcu] = xcv;
   if (xcur != nullptr && lin == 0 && tid < B) ycur[tid] = ycv;
   stamp(sts, st, 4);
@@ -603,7 +603,7 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   auto load_hq = [&](int chunk, int p) __attribute__((always_inline)) {
     const int r = tid >> 3, q = tid & 7;
     const int row = min(chunk * CH + r, B - 1);
-    const uint4* hp = reinterpret_cast<const uint4*>(hacc + (unsigned)((p * B + row) * HID + q * 8));
+    const uint4* hp = reinterpret_cast<const uint4*>(hacc + (unsigned)((p * B + row) * HACC_PITCH + q * 8));
     hq0 = hp[0];
     hq1 = hp[1];
     hq2 = hp[2];
@@ -1092,8 +1092,9 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
   // zero the dead hacc parity (read by the previous step's bwd) for the next fwd,
   // spread over the blocks
   {
-    uint4* h4 = reinterpret_cast<uint4*>(hacc + (long)(par ^ 1) * B * HID);
-    for (int i = s * 512 + tid; i < B * HID / 2; i += NS * 512) h4[i] = make_uint4(0u, 0u, 0u, 0u);
+    long long* hz = hacc + (long)(par ^ 1) * B * HACC_PITCH;
+    for (int i = s * 512 + tid; i < B * HID / 2; i += NS * 512)  // (32 16-B units per row)
+      *reinterpret_cast<uint4*>(hz + (i >> 5) * HACC_PITCH + (i & 31) * 2) = make_uint4(0u, 0u, 0u, 0u);
   }
   if (xpf) reinterpret_cast<uint4*>(xnext)[xpu] = xnv;
   if (ONE && xnext != nullptr && s == 0 && tid == 0) *xtag = ((long long)c.xgen << 32) | (long long)(unsigned)(ncur + 1);
@@ -1149,7 +1150,8 @@ __global__ __launch_bounds__(1024) void flush(float* __restrict__ P, float* __re
       if (!read_parity) hconv[i] = 0;
       if (!read_parity || hconv_w != hconv) hconv_w[i] = 0;
     } else {
-      hacc[i - 2 * NCONV] = 0;
+      const int j = i - 2 * NCONV;  // (row j / HID of both parities, column j % HID)
+      hacc[(j >> 6) * HACC_PITCH + (j & 63)] = 0;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && pend) {
@@ -1225,6 +1227,8 @@ __global__ __launch_bounds__(512) void sh_gather(Ctrl* __restrict__ ctrl, const 
 // Host-side launchers (no allocation / sync: capturable into a hipGraph).
 // ---------------------------------------------------------------------------------
 int convnet_num_slices(int PP) { return (convnet::NPOS + PP - 1) / PP; }
+// int64 elements of the dense-1 accumulator (both parities, rows HACC_PITCH apart)
+long convnet_hacc_elems(int B) { return 2L * B * convnet::HACC_PITCH; }
 size_t convnet_grad_count(int) { return (size_t)convnet::NGRAD; }
 // fwd images per block = 2^lg: 16 up to B = 256 (more blocks, shorter per-block chains),
 // 64 beyond (bounded replication of the W1-slice / conv-parameter loads)

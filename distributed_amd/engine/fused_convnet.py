@@ -117,7 +117,7 @@ class FusedConvNetEngine(Engine):
         self.w1bf = torch.zeros(FEAT * HID, dtype=torch.bfloat16, device=dev)
         self.pooled = torch.zeros(FEAT, BP, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
-        self.hacc = torch.zeros(2 * B * HID, dtype=torch.int64, device=dev)  # by step parity
+        self.hacc = torch.zeros(C.convnet_hacc_elems(B), dtype=torch.int64, device=dev)  # by step parity
         self.hconv = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
         self.calt = torch.zeros(2 * NCONV, **f32)  # alternate conv parameters + velocity
         # next-batch prefetch (B <= 64): bwd copies the next step's rows here for the next fwd,

@@ -60,7 +60,7 @@ class _Scratch:
         self.w1bf = self.P[OFF_W1:OFF_B1].to(torch.bfloat16)
         self.pooled = torch.zeros(FEAT, BP, dtype=torch.bfloat16, device=dev)
         self.code = torch.zeros(B, FEAT, dtype=torch.uint8, device=dev)
-        self.hacc = torch.zeros(2 * B * HID, dtype=torch.int64, device=dev)
+        self.hacc = torch.zeros(C.convnet_hacc_elems(B), dtype=torch.int64, device=dev)
         self.hconv = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
         self.calt = torch.zeros(2 * NCONV, **f32)
         self.hred = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
