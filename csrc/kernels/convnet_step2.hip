@@ -907,24 +907,34 @@ __global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* 
     stamp(sts, st, 7);
     // dh = (dz W2^T) * [h > 0] on f32 MFMA: 16 tiles of 16x16, two per wave, K = 10 (three
     // k-steps of 4, zero-padded); a lane's 4 outputs are 4 consecutive rows of one column,
-    // so dh^T is stored 8 bytes at a time
+    // so dh^T is stored 8 bytes at a time.
+    // Every LDS operand of both tiles first (dz, W2, the ReLU mask of h): one LDS wait
+    // instead of three per tile -- hipcc cannot move reads above the tile's dh stores itself
+    float za[2][3], wb[2][3], hm[2][4];
+#pragma unroll
+    for (int ti = 0; ti < 2; ++ti) {
+      const int t = wave + 8 * ti, mt = t >> 2, nt = t & 3, lr = lane & 15, kq = lane >> 4;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int k = 4 * ks + kq;
+        za[ti][ks] = k < NCLS ? zs[(16 * mt + lr) * ZP + k] : 0.f;
+        wb[ti][ks] = k < NCLS ? spl[HID + (16 * nt + lr) * NCLS + k] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) hm[ti][j] = hs[(16 * mt + 4 * kq + j) * HPITCH + 16 * nt + lr];
+    }
 #pragma unroll
     for (int ti = 0; ti < 2; ++ti) {
       const int t = wave + 8 * ti, mt = t >> 2, nt = t & 3, lr = lane & 15, kq = lane >> 4;
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 3; ++ks) {
-        const int k = 4 * ks + kq;
-        const float a = k < NCLS ? zs[(16 * mt + lr) * ZP + k] : 0.f;
-        const float b = k < NCLS ? spl[HID + (16 * nt + lr) * NCLS + k] : 0.f;
-        acc = mfma4(a, b, acc);
-      }
+      for (int ks = 0; ks < 3; ++ks) acc = mfma4(za[ti][ks], wb[ti][ks], acc);
       const int n = 16 * nt + lr, rb = 16 * mt + 4 * kq;
       uint16_t hi[4], lo[4];
       float dsum = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float d = hs[(rb + j) * HPITCH + n] > 0.f ? acc[j] : 0.f;
+        const float d = hm[ti][j] > 0.f ? acc[j] : 0.f;
         dsum += d;
         hi[j] = f2bf(d);
         lo[j] = bf16_lo(d, hi[j]);
