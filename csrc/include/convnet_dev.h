@@ -88,15 +88,20 @@ __device__ __forceinline__ void x_load(XStage<U8>& st, const void* __restrict__ 
   st.rg = rg;
   // element offset of (row r0 + rg, unit q); rows advance by RG * IMG elements
   const unsigned eo = __umul24((unsigned)max(0, min(g, nsamples - 1)), (unsigned)NPIX) + (unsigned)((r0 + rg) * IMG + 4 * q);
+  // one 64-bit base per thread, rows at a uniform byte stride (per-row 32-bit offsets became
+  // a quarter-rate 64-bit multiply-add per row)
+  constexpr int ES = U8 ? 1 : 4;
+  const char* xb = static_cast<const char*>(X) + (size_t)eo * ES;
+  const int rstride = RG * IMG * ES;
 #pragma unroll
   for (int j = 0; j < XR; ++j) {
     if constexpr (U8) st.w[j] = 0u;
     else st.v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (j * RG >= XR) continue;  // (uniform)
     if (ok && rg + j * RG < nrows) {
-      const unsigned e = eo + (unsigned)(j * RG * IMG);
-      if constexpr (U8) st.w[j] = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(X) + e);
-      else st.v[j] = *reinterpret_cast<const float4*>(static_cast<const char*>(X) + 4u * e);
+      const char* pj = xb + j * rstride;
+      if constexpr (U8) st.w[j] = *reinterpret_cast<const uint32_t*>(pj);
+      else st.v[j] = *reinterpret_cast<const float4*>(pj);
     }
   }
 }

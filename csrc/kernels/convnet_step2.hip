@@ -353,8 +353,9 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
   stamp(sts, st, 3);
   // pooled tile (feature-major [k][b]: bwd's dW1 operand) and argmax codes ([b][k]) for
   // bwd, from LDS as contiguous 8-byte / 4-byte stores instead of scattered 1-2 B stores
+  // (IB / 4 = 2^(lg - 2) and K / 4 = 8 np: shifts and a multiply, not divisions)
   for (int i = tid; i < K * (IB / 4); i += 512) {
-    const int kk = i / (IB / 4), bo = 4 * (i - kk * (IB / 4));
+    const int kk = i >> (lg - 2), bo = 4 * (i & ((1 << (lg - 2)) - 1));
     uint16_t v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = as[(bo + e) * KP + kk];
@@ -369,7 +370,7 @@ __global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* 
     }
   }
   for (int i = tid; i < IB * (K / 4); i += 512) {
-    const int bo = i / (K / 4), w = i - bo * (K / 4);
+    const int i8 = i >> 3, bo = np == 3 ? (int)(((unsigned)i8 * 21846u) >> 16) : i8 >> (np >> 1), w = i - bo * (K / 4);
     if (img0 + bo < B)
       *reinterpret_cast<uint32_t*>(code + (unsigned)((img0 + bo) * FEAT + p0 * NF + 4 * w)) =
           reinterpret_cast<const uint32_t*>(csl + bo * K)[w];
