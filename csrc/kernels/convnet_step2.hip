@@ -537,16 +537,19 @@ __device__ __forceinline__ void exchange_tail(const XArgs& xa, Ctrl* ctrl, const
 // aux element e (parameter order at G + OFF_B1): [0,64) db1, [64,704) dW2
 // (k = (e-64)/10, c = (e-64)%10), [704,714) db2, then 714 loss, 715 correct, 716 count.
 template <bool U8, bool ONE>  // ONE: B <= 64, a single chunk (no loop-carried prefetch registers)
-__global__ __launch_bounds__(512) void bwd(Ctrl* __restrict__ ctrl, const void* __restrict__ X,
-                                           const int* __restrict__ labels, const float* P,
-                                           float* __restrict__ G, const uint16_t* w1bf,
-                                           const uint16_t* __restrict__ pooled, const uint8_t* __restrict__ code,
-                                           long long* __restrict__ hacc, long long* __restrict__ hconv, int B,
+// (the first 16 argument dwords arrive preloaded in SGPRs: they are what the prologue's first
+// loads address -- the dense-1 sums by the known parity, this step's staged labels / rows, b1 /
+// W2 / b2, the bf16 W1 slice, the pooled tile and codes; later arguments come from the
+// kernarg segment, a scalar load's latency behind)
+__global__ __launch_bounds__(512) void bwd(long long* __restrict__ hacc, const int* __restrict__ ycur,
+                                           const void* __restrict__ xcur, int phint, int B, const float* P,
+                                           const uint16_t* w1bf, const uint16_t* __restrict__ pooled,
+                                           const uint8_t* __restrict__ code, Ctrl* __restrict__ ctrl,
+                                           const void* __restrict__ X, const int* __restrict__ labels,
+                                           float* __restrict__ G, long long* __restrict__ hconv,
                                            int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
                                            unsigned long long* st, const float* __restrict__ Gr, const XArgs xa,
-                                           void* __restrict__ xnext, long long* __restrict__ xtag,
-                                           const void* __restrict__ xcur, const int* __restrict__ ycur, int phint,
-                                           int auxm) {
+                                           void* __restrict__ xnext, long long* __restrict__ xtag, int auxm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   constexpr int cprobe = DAMD_PROBE_HCONV;  // 0 in every product build (see the top of the file)
@@ -1299,19 +1302,17 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
   while (ltpe < 6 && (2 << ltpe) * chunk_aux <= 512) ++ltpe;
   const int auxm = chunk_aux | (ltpe << 16);
   if (B <= CH)
-    hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X, b.labels,
-                       b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf,
-                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b), b.xnext, b.xtag, B <= CH ? b.xcur : nullptr, B <= CH ? b.ycur : nullptr,
-                       b.par_hint, auxm);
+    hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.hacc,
+                       B <= CH ? b.ycur : nullptr, B <= CH ? b.xcur : nullptr, b.par_hint, B, b.P, b.w1bf,
+                       b.pooled, b.code, b.ctrl, b.X, b.labels, b.G, b.hconv, PP, eager2(b, B), b.P, b.V, b.w1bf,
+                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G, xargs(b), b.xnext, b.xtag,
+                       auxm);
   else
-    hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.ctrl, b.X,
-                       b.labels, b.P, b.G, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, B, PP,
-                       eager2(b, B), b.P, b.V, b.w1bf,
-                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G,
-                       xargs(b), b.xnext, b.xtag, B <= CH ? b.xcur : nullptr, B <= CH ? b.ycur : nullptr,
-                       b.par_hint, auxm);
+    hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.hacc,
+                       B <= CH ? b.ycur : nullptr, B <= CH ? b.xcur : nullptr, b.par_hint, B, b.P, b.w1bf,
+                       b.pooled, b.code, b.ctrl, b.X, b.labels, b.G, b.hconv, PP, eager2(b, B), b.P, b.V, b.w1bf,
+                       b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G, xargs(b), b.xnext, b.xtag,
+                       auxm);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
