@@ -38,6 +38,7 @@ class ConvNetTrainer : public StepExecutor {
   ConvNetTrainer(int device, py::dict bufs, int B, int PP, int grad_allreduce)
       : StepExecutor(device), B_(B), PP_(PP), grad_allreduce_(grad_allreduce) {
     if (B <= 0) throw std::invalid_argument("batch must be > 0");
+    if (B > 65535) throw std::invalid_argument("per-rank batch must be < 65536 (packed kernel argument)");
     if (PP < 1 || PP > 4) throw std::invalid_argument("positions per slice must be in [1,4]");
     auto g = [&](const char* k) -> uintptr_t { return bufs[k].cast<uintptr_t>(); };
     b_.X = nullptr; b_.labels = nullptr; b_.x_u8 = 0;

@@ -119,17 +119,20 @@ __device__ __forceinline__ float4 unpack_bf16x4(uint2 q) {
 template <bool U8>
 // (ctrl and X lead the argument list: with kernarg preloading they arrive in SGPRs, so
 // the first dependent loads -- the ctrl block, then the batch rows -- start at once)
-__global__ __launch_bounds__(512) void fwd(Ctrl* __restrict__ ctrl, const void* __restrict__ X,
-                                           float* __restrict__ P, const float* __restrict__ G,
-                                           float* __restrict__ V, float* __restrict__ W1alt,
-                                           float* __restrict__ V1alt, uint16_t* __restrict__ w1bf,
-                                           uint16_t* __restrict__ pooled, uint8_t* __restrict__ code,
-                                           long long* __restrict__ hacc, long long* __restrict__ hconv,
-                                           float* __restrict__ calt, int B, int PP, int lg, int eager,
-                                           unsigned long long* st, const long long* __restrict__ hconv_r,
-                                           const XArgs xa, const void* __restrict__ xnext,
+// (the first 16 argument dwords arrive preloaded in SGPRs: the pointers of the prologue's
+// first loads and the packed sizes their addresses need -- bpp = B | PP << 16, lge = lg |
+// eager << 8; later arguments come from the kernarg segment, a scalar load's latency behind)
+__global__ __launch_bounds__(512) void fwd(const void* __restrict__ xnext, uint16_t* __restrict__ w1bf,
+                                           float* __restrict__ P, float* __restrict__ V,
+                                           float* __restrict__ calt, const long long* __restrict__ hconv_r,
+                                           const float* __restrict__ G, int bpp, int lge, Ctrl* __restrict__ ctrl,
+                                           const void* __restrict__ X, float* __restrict__ W1alt,
+                                           float* __restrict__ V1alt, uint16_t* __restrict__ pooled,
+                                           uint8_t* __restrict__ code, long long* __restrict__ hacc,
+                                           long long* __restrict__ hconv, unsigned long long* st, const XArgs xa,
                                            const long long* __restrict__ xtag, const int* __restrict__ labels,
                                            void* __restrict__ xcur, int* __restrict__ ycur, int phint) {
+  const int B = bpp & 0xffff, PP = bpp >> 16, lg = lge & 0xff, eager = lge >> 8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int s = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const bool sh = xa.world > 1;  // sharded multi-rank step: gradients from the exchange staging
@@ -542,14 +545,15 @@ template <bool U8, bool ONE>  // ONE: B <= 64, a single chunk (no loop-carried p
 // W2 / b2, the bf16 W1 slice, the pooled tile and codes; later arguments come from the
 // kernarg segment, a scalar load's latency behind)
 __global__ __launch_bounds__(512) void bwd(long long* __restrict__ hacc, const int* __restrict__ ycur,
-                                           const void* __restrict__ xcur, int phint, int B, const float* P,
+                                           const void* __restrict__ xcur, int phint, int bpp, const float* P,
                                            const uint16_t* w1bf, const uint16_t* __restrict__ pooled,
                                            const uint8_t* __restrict__ code, Ctrl* __restrict__ ctrl,
                                            const void* __restrict__ X, const int* __restrict__ labels,
                                            float* __restrict__ G, long long* __restrict__ hconv,
-                                           int PP, int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
+                                           int eager, float* Pw, float* Vw, uint16_t* w1bf_out,
                                            unsigned long long* st, const float* __restrict__ Gr, const XArgs xa,
                                            void* __restrict__ xnext, long long* __restrict__ xtag, int auxm) {
+  const int B = bpp & 0xffff, PP = bpp >> 16;  // (packed: both preloaded)
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const bool sh = xa.world > 1;  // sharded multi-rank step (see the exchange at the end)
   constexpr int cprobe = DAMD_PROBE_HCONV;  // 0 in every product build (see the top of the file)
@@ -1280,11 +1284,10 @@ static void launch2_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) 
   const int NS = convnet_num_slices(PP);
   const int lg = convnet_f1_lg(B);
   const dim3 g1(NS, (B + (1 << lg) - 1) >> lg);
-  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st, b.ctrl, b.X, b.P,
-                     b.Gr ? b.Gr : b.G, b.V,
-                     b.W1alt, b.V1alt, b.w1bf, b.pooled, b.code, b.hacc, b.hconv, b.calt, B, PP, lg,
-                     eager2(b, B), b.stamps,
-                     b.hconv_r ? b.hconv_r : b.hconv, xargs(b), B <= CH ? b.xnext : nullptr, b.xtag, b.labels,
+  hipLaunchKernelGGL((convnet2::fwd<U8>), g1, dim3(512), convnet2_fwd_lds(PP, lg), st,
+                     B <= CH ? b.xnext : nullptr, b.w1bf, b.P, b.V, b.calt, b.hconv_r ? b.hconv_r : b.hconv,
+                     b.Gr ? b.Gr : b.G, B | (PP << 16), lg | (eager2(b, B) << 8), b.ctrl, b.X, b.W1alt, b.V1alt,
+                     b.pooled, b.code, b.hacc, b.hconv, b.stamps, xargs(b), b.xtag, b.labels,
                      B <= CH ? b.xcur : nullptr, b.ycur, b.par_hint);
 }
 
@@ -1303,27 +1306,27 @@ static void launch2_bwd(const ConvNetBuffers& b, int B, int PPf, hipStream_t st)
   const int auxm = chunk_aux | (ltpe << 16);
   if (B <= CH)
     hipLaunchKernelGGL((convnet2::bwd<U8, true>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.hacc,
-                       B <= CH ? b.ycur : nullptr, B <= CH ? b.xcur : nullptr, b.par_hint, B, b.P, b.w1bf,
-                       b.pooled, b.code, b.ctrl, b.X, b.labels, b.G, b.hconv, PP, eager2(b, B), b.P, b.V, b.w1bf,
+                       B <= CH ? b.ycur : nullptr, B <= CH ? b.xcur : nullptr, b.par_hint, B | (PP << 16), b.P,
+                       b.w1bf, b.pooled, b.code, b.ctrl, b.X, b.labels, b.G, b.hconv, eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G, xargs(b), b.xnext, b.xtag,
                        auxm);
   else
     hipLaunchKernelGGL((convnet2::bwd<U8, false>), dim3(NS), dim3(512), convnet2_bwd_lds(PP), st, b.hacc,
-                       B <= CH ? b.ycur : nullptr, B <= CH ? b.xcur : nullptr, b.par_hint, B, b.P, b.w1bf,
-                       b.pooled, b.code, b.ctrl, b.X, b.labels, b.G, b.hconv, PP, eager2(b, B), b.P, b.V, b.w1bf,
+                       B <= CH ? b.ycur : nullptr, B <= CH ? b.xcur : nullptr, b.par_hint, B | (PP << 16), b.P,
+                       b.w1bf, b.pooled, b.code, b.ctrl, b.X, b.labels, b.G, b.hconv, eager2(b, B), b.P, b.V, b.w1bf,
                        b.stamps ? b.stamps + 2 * 256 * 16 : nullptr, b.Gr ? b.Gr : b.G, xargs(b), b.xnext, b.xtag,
                        auxm);
 }
 
 hipError_t convnet2_launch_fwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
-  if (!b.hacc || !b.hconv || !b.calt) return hipErrorInvalidValue;
+  if (!b.hacc || !b.hconv || !b.calt || B > 0xffff) return hipErrorInvalidValue;
   if (b.x_u8) launch2_fwd<true>(b, B, PP, st);
   else launch2_fwd<false>(b, B, PP, st);
   return hipGetLastError();
 }
 
 hipError_t convnet2_launch_bwd(const ConvNetBuffers& b, int B, int PP, hipStream_t st) {
-  if (!b.hacc || !b.hconv || !b.calt) return hipErrorInvalidValue;
+  if (!b.hacc || !b.hconv || !b.calt || B > 0xffff) return hipErrorInvalidValue;
   if (convnet2_bwd_lds(ppb_of(b, PP)) > 160 * 1024) return hipErrorInvalidValue;
   if (b.xa && b.xa->ppb != ppb_of(b, PP)) return hipErrorInvalidValue;
   if (b.x_u8) launch2_bwd<true>(b, B, PP, st);
