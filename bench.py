@@ -234,11 +234,20 @@ def main():
 
     diag_extra = int(os.environ.get("DAMD_BENCH_EXTRA", "0")) > 0
 
+    def ctl_ops():  # control-plane collectives (barrier / object all-gather) issued so far
+        return int(getattr(comm, "control_ops", 0))
+
     def timed(eng, k, final):
-        """Seconds for k full steps (the last deferred SGD update included), bracketed by a
-        barrier + device synchronize on both sides, max over ranks."""
+        """(seconds for k full steps, barrier seconds, control collectives in the window).
+
+        The window: a barrier + device synchronize BEFORE t0 (every rank starts together),
+        the k steps (the last deferred SGD update included), then each rank's device
+        synchronize ends ITS window (t1).  The barrier after t1 is outside the window (its
+        cost is reported separately as ``barrier_us``): a host TCP round trip among N ranks
+        is not training work.  Value = max over ranks of t1 - t0."""
         barrier()
         device_sync()
+        c0 = ctl_ops()
         t0 = time.perf_counter()
         if final:
             eng.run_and_flush(k)  # K steps + the last deferred SGD update, one graph
@@ -254,52 +263,25 @@ def main():
         # (C++-created) step streams included: a second, engine-level host wait would only
         # add a round trip to the timed window
         device_sync()
+        t1 = time.perf_counter()
+        inwin = ctl_ops() - c0  # must stay 0: no host collective inside a timed window
         barrier()
-        dt = time.perf_counter() - t0
-        return max(comm.allgather_object(dt)) if n > 1 else dt
+        tb = time.perf_counter() - t1
+        if n > 1:
+            rows = comm.allgather_object((t1 - t0, tb, inwin))
+            return max(r[0] for r in rows), max(r[1] for r in rows), sum(r[2] for r in rows)
+        return t1 - t0, tb, inwin
 
     fail_at = runtime.fault_injection_step()  # DAMD_FAIL_AT=rank:step (launcher / gang tests)
     if fail_at is not None and fail_at <= args.warmup:
         raise RuntimeError(f"injected failure on rank {rt.rank} at step {fail_at} (DAMD_FAIL_AT)")
 
-    # N > 1, fused engine, transport not pinned: every candidate gradient exchange (each
-    # self-tested at engine start, engine/xchg_selftest.py) runs warmup + K untimed-for-the-
-    # metric steps; the fastest carries the measured run.  This is also where BASELINE
-    # config 3's "RCCL ring all-reduce" gets its own number on the same ranks.
-    transports = {}
-    failed_selftest = []  # candidate transports whose start-up self-test failed (skipped)
-    model, engine = None, None
-    keep = []  # every candidate engine stays alive until the end: no destructor (device syncs,
-    # IPC unmaps, frees) may run inside a timed window
-    tune = (n > 1 and args.model == "mnist" and args.engine in ("auto", "fused") and "DAMD_ALLREDUCE" not in os.environ
-            and os.environ.get("DAMD_BENCH_TUNE", "1") != "0" and args.steps > 0)
-    if tune:
-        best = None
-        from distributed_amd.engine.fused_convnet import ExchangeSelfTestError
-
-        for cand in ("sharded", "xgmi", "rccl"):
-            try:
-                m_c, e_c = make_engine(cand)
-            except ExchangeSelfTestError as e:
-                # every rank raises (the self-test outcome is voted), so every rank skips
-                # this candidate; the headline run goes on with the transports that passed
-                print(f"[bench] transport {cand} skipped: {e}", file=sys.stderr, flush=True)
-                failed_selftest.append(cand)
-                continue
-            keep.append((m_c, e_c))
-            kind = getattr(e_c, "allreduce_kind", cand)
-            if e_c.name != "fused_convnet" or kind in transports:
-                continue  # fell back onto a transport already measured
-            e_c.prepare(max(args.steps, args.warmup))
-            run(e_c, args.warmup)
-            e_c.sync()
-            dt_c = timed(e_c, args.steps, False)
-            transports[kind] = round(dt_c * 1e3 / args.steps, 5)
-            if best is None or dt_c < best[0]:
-                best = (dt_c, m_c, e_c)
-        model, engine = best[1], best[2]
-    else:
-        model, engine = make_engine()
+    # N > 1, fused engine, transport not pinned: the engine itself self-tests every candidate
+    # gradient exchange and times each (sharded, peer, RCCL) with this bench's own window
+    # protocol -- K steps + flush as one graph -- keeping the fastest
+    # (engine/xchg_selftest.time_transport); fit() gets the same choice.  A candidate whose
+    # self-test fails is skipped on every rank (collective vote).
+    model, engine = make_engine()
     # build the replayed HIP graph(s) first: capture is setup, not part of a timed step
     engine.prepare(max(args.steps, args.warmup))
     # fused engine: the K timed steps and the final flush as one graph (setup, untimed)
@@ -313,7 +295,7 @@ def main():
     gc.collect()
     run(engine, args.warmup)
     engine.sync()
-    dt = timed(engine, args.steps, final)
+    dt, bar_s, ctl_in_window = timed(engine, args.steps, final)
     # diagnostics only (stderr, never the reported value): DAMD_BENCH_EXTRA=n repeats the
     # warmup + timed window n more times, to separate a first-window cost from the steady one
     for _ in range(int(os.environ.get("DAMD_BENCH_EXTRA", "0"))):
@@ -321,7 +303,7 @@ def main():
             engine.prepare_final(args.steps)  # (the variant for the current step phase)
         run(engine, args.warmup)
         engine.sync()
-        print(f"[bench] extra window: {timed(engine, args.steps, final) * 1e3 / args.steps:.5f} ms/step",
+        print(f"[bench] extra window: {timed(engine, args.steps, final)[0] * 1e3 / args.steps:.5f} ms/step",
               file=sys.stderr, flush=True)
     phases = engine.phase_times(args.phases) if args.phases > 0 else None
     m = engine.metrics()
@@ -372,6 +354,10 @@ def main():
             "rccl_ranks": _rccl_ranks(comm),
         }
         if n > 1:
+            # the barrier AFTER the window (outside it) and the control-plane collectives
+            # inside the window (0 by construction; tests/test_bench_cpu.py asserts it)
+            out["barrier_us"] = round(bar_s * 1e6, 1)
+            out["control_collectives_in_window"] = ctl_in_window
             ev = getattr(engine, "exchange_verified", None)
             # the device exchange passed its start-up self-test (bitwise vs the host rank-order
             # reduction) AND the replicas are bitwise mirrored after the window; None: the
@@ -382,8 +368,10 @@ def main():
             if os.environ.get("DAMD_BENCH_FALLBACK_FROM"):
                 fb = [os.environ["DAMD_BENCH_FALLBACK_FROM"]] + fb
             out["fallback_from"] = fb
+            transports = {k: round(v * 1e-3, 5) for k, v in (getattr(engine, "transport_us", None) or {}).items()}
             if transports:
                 out["transport_ms_per_step"] = transports
+            failed_selftest = [k for k in fb if not k.startswith("gang-exit")]
             if failed_selftest:
                 out["transports_failed_selftest"] = failed_selftest
             out["rccl_ms_per_step"] = transports.get("rccl", round(dt * 1e3 / args.steps, 5)

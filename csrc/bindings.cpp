@@ -231,8 +231,11 @@ class ConvNetTrainer : public StepExecutor {
   int B_, PP_, grad_allreduce_;
 };
 
+const char* damd_src_hash();  // build/obj/src_hash.cpp, generated by distributed_amd/_build.py
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_amd native runtime (HIP/gfx950 kernels, RCCL, hipGraph executor)";
+  m.def("src_hash", []() { return std::string(damd_src_hash()); });
   m.attr("CONVNET_NPARAM") = kConvNetNParam;
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
   m.attr("CONVNET_NCONV") = kConvNetNConv;

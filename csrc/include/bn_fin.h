@@ -11,28 +11,33 @@
 namespace damd {
 
 // Forward statistics: the replicas acc[r][2][C] (one word per value) summed as integers
-// (exact, any order), then decoded.
+// (exact, any order), then decoded; the sticky flag plane after the replicas
+// (damd_common.h bnacc_flag) turns a channel's statistics into NaN.
 __device__ inline void acc_sums(const long long* acc, int reps, int C, int c, double& s, double& q) {
   long long ws = 0, wq = 0;
-  for (int r = 0; r < max(reps, 1); ++r) {
+  reps = max(reps, 1);
+  for (int r = 0; r < reps; ++r) {
     ws += acc[(size_t)r * 2 * C + c];
     wq += acc[(size_t)r * 2 * C + C + c];
   }
-  s = bnacc_value1(ws);
-  q = bnacc_value1(wq);
+  const long long f = acc[(size_t)reps * 2 * C + c];
+  s = bnacc_value1(ws, f);
+  q = bnacc_value1(wq, f);
 }
 // Backward sums: acc[r][4][C] (planes: sum hi, sum lo, second hi, second lo), the same way.
 __device__ inline void acc_sums2(const long long* acc, int reps, int C, int c, double& s, double& q) {
   long long sh = 0, sl = 0, qh = 0, ql = 0;
-  for (int r = 0; r < max(reps, 1); ++r) {
+  reps = max(reps, 1);
+  for (int r = 0; r < reps; ++r) {
     const long long* a = acc + (size_t)r * 4 * C;
     sh += a[c];
     sl += a[C + c];
     qh += a[2 * C + c];
     ql += a[3 * C + c];
   }
-  s = bnacc_value2(sh, sl);
-  q = bnacc_value2(qh, ql);
+  const long long f = acc[(size_t)reps * 4 * C + c];
+  s = bnacc_value2(sh, sl, f);
+  q = bnacc_value2(qh, ql, f);
 }
 // coefficients of channel c (mean, invstd, scale, shift); pub: also published to st and
 // the moving statistics (one thread per channel of the whole grid)

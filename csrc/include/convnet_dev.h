@@ -242,13 +242,15 @@ __device__ __forceinline__ long long to_fix(float v, float scale, int* bad) {
   }
   return (long long)__builtin_rintf(q);
 }
-// fixed point -> float as high word * 2^32 + unsigned low word in one fma: f32 only (the
+// fixed point -> float as (q >> 24) * 2^24 + (q & (2^24 - 1)) in one fma: f32 only (the
 // former (float)((double)q * inv) took ~6 half-rate f64 instructions per value, and the
-// head converts 8 per thread); within ~1 ulp of the exact value (the low word's rounding
-// is at most 2^-25 of 2^32 units), deterministic.  inv is a power of two.
+// head converts 8 per thread).  Both parts are exact floats for |q| < 2^48 (the signed
+// high part is arithmetic-shifted, the low part has 24 bits), so the fma rounds ONCE: the
+// correctly rounded value, negative q included (round 5 split at 2^32 and rounded the
+// unsigned low word first: q = -5 decoded to 0).  inv is a power of two.
 __device__ __forceinline__ float from_fix(long long q, double inv) {
   const float fi = (float)inv;
-  return fmaf((float)(int)(q >> 32), fi * 4294967296.f, (float)(unsigned)q * fi);
+  return fmaf((float)(q >> 24), fi * 16777216.f, (float)(int)(q & 0xFFFFFF) * fi);
 }
 
 __device__ __forceinline__ void atomic_add_i64(long long* p, long long v) {

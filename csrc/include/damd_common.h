@@ -49,39 +49,46 @@ __device__ __forceinline__ void damd_publish_drain() { asm volatile("s_waitcnt v
 //    words, hi = floor(v 2^24), lo = floor((v 2^24 - hi) 2^40) in [0, 2^40): resolution
 //    2^-64, exact for |v| >= 2^-40; < 2^23 addends per lo word.  Layout per replica:
 //    [sum hi][sum lo][second hi][second lo], C words each.
-// A non-finite or out-of-range partial adds a poison (+-2^58 to the hi word): the decoded
-// sum is NaN (a diverged run shows NaN statistics rather than wrapped ones).
-constexpr long long kBnAccPoison = 1LL << 58;
-__device__ __forceinline__ long long bnacc_hi_or_poison(float v, double& d) {
-  d = (double)v * 16777216.0;  // 2^24: exact
-  return fabsf(v) < 1073741824.f ? 0 : (v < 0.f ? -kBnAccPoison : kBnAccPoison);  // 2^30 (false for NaN)
+// A non-finite or out-of-range partial (|v| >= 2^30) is NOT added: it sets a sticky flag
+// word instead (atomicOr; one flag per channel, in a plane after the replicas:
+// acc[reps][K] then flag[K]), and every consumer that sees a set flag decodes NaN.  (Round
+// 5 added a +-2^58 poison into the sum word itself: N poisoned partials wrapped to 0 for N a
+// multiple of 64, +inf and -inf cancelled, and finite sums >= 2^33 decoded as NaN.)
+// Range of a decoded sum: the int64 word, |sum| < 2^39.
+__device__ __forceinline__ bool bnacc_ok(float v) { return fabsf(v) < 1073741824.f; }  // 2^30 (false for NaN)
+__device__ __forceinline__ void bnacc_flag(long long* flag) {
+  atomicOr(reinterpret_cast<unsigned long long*>(flag), 1ull);
 }
-__device__ __forceinline__ void bnacc_add1(long long* p, float v) {
-  double d;
-  long long w = bnacc_hi_or_poison(v, d);
-  if (w == 0) w = __double2ll_rn(d);
+__device__ __forceinline__ void bnacc_add1(long long* p, long long* flag, float v) {
+  if (!bnacc_ok(v)) {
+    bnacc_flag(flag);
+    return;
+  }
+  const long long w = __double2ll_rn((double)v * 16777216.0);  // 2^24: exact scaling
   atomicAdd(reinterpret_cast<unsigned long long*>(p), (unsigned long long)w);
 }
 // (hi and lo live in separate planes -- p_hi[c], p_lo[c] -- so that a wave's 64 channels add
 // into 512 contiguous bytes per word: interleaved pairs doubled bn_bwd_reduce, 141 -> 277 us
 // per ResNet-18 step)
-__device__ __forceinline__ void bnacc_add2(long long* p_hi, long long* p_lo, float v) {
-  double d;
-  long long hi = bnacc_hi_or_poison(v, d), lo = 0;
-  if (hi == 0) {
-    const double fh = floor(d);
-    hi = (long long)fh;
-    lo = (long long)((d - fh) * 1099511627776.0);  // [0, 1) x 2^40: exact, then floor
+__device__ __forceinline__ void bnacc_add2(long long* p_hi, long long* p_lo, long long* flag, float v) {
+  if (!bnacc_ok(v)) {
+    bnacc_flag(flag);
+    return;
   }
+  const double d = (double)v * 16777216.0;
+  const double fh = floor(d);
+  const long long hi = (long long)fh;
+  const long long lo = (long long)((d - fh) * 1099511627776.0);  // [0, 1) x 2^40: exact, then floor
   atomicAdd(reinterpret_cast<unsigned long long*>(p_hi), (unsigned long long)hi);
   if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(p_lo), (unsigned long long)lo);
 }
-__device__ __forceinline__ double bnacc_value1(long long w) {
-  if (w >= (kBnAccPoison >> 1) || w <= -(kBnAccPoison >> 1)) return __builtin_nan("");
+__device__ __forceinline__ double bnacc_value1(long long w, long long flag = 0) {
+  if (flag) return __builtin_nan("");
   return (double)w * 5.9604644775390625e-08;  // 2^-24
 }
-__device__ __forceinline__ double bnacc_value2(long long hi, long long lo) {
-  return bnacc_value1(hi) + (double)lo * 5.42101086242752217e-20;  // 2^-64
+__device__ __forceinline__ double bnacc_value2(long long hi, long long lo, long long flag = 0) {
+  if (flag) return __builtin_nan("");
+  return (double)hi * 5.9604644775390625e-08 + (double)lo * 5.42101086242752217e-20;  // 2^-24, 2^-64
 }
 
 #define DAMD_PUBLISH_WG() asm volatile(";damd.publish wg")

@@ -41,7 +41,7 @@ struct GemmArgs {
   int k_per_split;     // multiple of 32
   int kstep;           // conv_gemm.hip k-step depth: 32 | 64 (0: DAMD_CONV_KB / 64)
   long long* stats_acc;  // E_STATS: non-null -> the tile's column sum / sumsq are added (bnacc_add
-                       // atomics) into stats_acc[reps][2][N] instead of stored to `stats`:
+                       // atomics) into stats_acc[reps][2][N] (+ the sticky flag plane after the replicas) instead of stored to `stats`:
   int stats_reps;      //   M-tile tm into replica tm % reps (0 / 1: one), see layer_ops.h BNFin
   const uint16_t* bnx; // E_BNRED: the BN input x [M][ldc] bf16 and its st [4][N] (mean,
   const float* bnst;   //   invstd, scale, shift)

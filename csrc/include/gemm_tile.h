@@ -206,15 +206,18 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       const int n = n0 + t;
       if (n < a.N) {
         if (a.stats_acc) {
+          const size_t reps = a.stats_reps > 1 ? a.stats_reps : 1;
           const size_t rep = a.stats_reps > 1 ? tm % a.stats_reps : 0;
           if constexpr (EPI & E_BNRED) {  // BN-backward sums: two words per value
             long long* acc = a.stats_acc + rep * 4 * a.N;  // hi / lo planes
-            bnacc_add2(acc + n, acc + a.N + n, s);
-            bnacc_add2(acc + 2 * a.N + n, acc + 3 * a.N + n, q);
+            long long* flag = a.stats_acc + reps * 4 * a.N + n;  // sticky plane after the replicas
+            bnacc_add2(acc + n, acc + a.N + n, flag, s);
+            bnacc_add2(acc + 2 * a.N + n, acc + 3 * a.N + n, flag, q);
           } else {  // forward statistics: one word per value
             long long* acc = a.stats_acc + rep * 2 * a.N;
-            bnacc_add1(acc + n, s);
-            bnacc_add1(acc + a.N + n, q);
+            long long* flag = a.stats_acc + reps * 2 * a.N + n;
+            bnacc_add1(acc + n, flag, s);
+            bnacc_add1(acc + a.N + n, flag, q);
           }
         } else {
           float* st = a.stats + ((size_t)tm * gridDim.z + blockIdx.z) * 2 * a.N;

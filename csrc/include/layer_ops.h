@@ -22,7 +22,7 @@ struct Ctrl;  // kernels_api.h / damd_common.h
 // block, into LDS); its block 0 also writes st / co, the moving statistics and dgamma /
 // dbeta.  The accumulators are zeroed once per step (gather_batch's `zero` range).
 struct BNFin {
-  const long long* acc;  // [reps][2][C] sum, sum of squares (bnacc_add1); null: the kernel reads st
+  const long long* acc;  // [reps][2][C] sum, sum of squares (bnacc_add1) + flag plane [2C]; null: the kernel reads st
   const float* gamma;  // may be null (1)
   const float* beta;   // may be null (0)
   float* st;           // [4][C] out (block 0): mean, invstd, scale, shift
@@ -32,7 +32,7 @@ struct BNFin {
   int reps;            // replicas of acc (0 / 1: one)
 };
 struct BNBwdFin {
-  const long long* acc;  // [reps][4][C] sum dz / sum dz * xhat, hi / lo planes (bnacc_add2); null: co
+  const long long* acc;  // [reps][4][C] sum dz / sum dz * xhat, hi / lo planes (bnacc_add2) + flag plane [4C]; null: co
   float* dgamma;       // += (block 0), may be null
   float* dbeta;
   float* co;           // [3][C] out (block 0)

@@ -170,10 +170,12 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
   float* sft = reinterpret_cast<float*>(smem + sft_off);
   constexpr int FR = 8;  // replicas held in registers (more: summed in pre())
   long long fs[FR], fq[FR];  // fixed-point words (damd_common.h bnacc_add1)
+  long long ff = 0;          // the channel's sticky non-finite flag (plane after the replicas)
   float fg = 1.f, fb = 0.f;
   if (bnin && t < SC) {
     if (a.bnin.gamma) fg = a.bnin.gamma[t];
     if (a.bnin.beta) fb = a.bnin.beta[t];
+    ff = a.bnin.acc[(size_t)max(a.bnin.reps, 1) * 2 * SC + t];
 #pragma unroll
     for (int r = 0; r < FR; ++r) {
       const int rr = min(r, max(a.bnin.reps, 1) - 1);
@@ -274,8 +276,8 @@ __global__ __launch_bounds__(NT, 2) void conv3_kernel(GemmArgs a, int R, int tpi
                 ws += fs[r];
                 wq += fq[r];
               }
-            s = bnacc_value1(ws);
-            q = bnacc_value1(wq);
+            s = bnacc_value1(ws, ff);
+            q = bnacc_value1(wq, ff);
             bn_fin_sums_gb(a.bnin, SC, c, s, q, fg, fb, pub, m, inv, sc, sh);
           } else {
             acc_sums(a.bnin.acc, a.bnin.reps, SC, c, s, q);

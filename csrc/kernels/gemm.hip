@@ -602,8 +602,9 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
     }
     if (stats_acc) {
       long long* acc = stats_acc + (size_t)(blockIdx.x % reps) * 2 * N;  // forward statistics
-      bnacc_add1(acc + c0 + c, a);
-      bnacc_add1(acc + N + c0 + c, b);
+      long long* flag = stats_acc + (size_t)reps * 2 * N + c0 + c;       // sticky plane
+      bnacc_add1(acc + c0 + c, flag, a);
+      bnacc_add1(acc + N + c0 + c, flag, b);
     } else {
       stats[(size_t)blockIdx.x * 2 * N + c0 + c] = a;
       stats[(size_t)blockIdx.x * 2 * N + N + c0 + c] = b;

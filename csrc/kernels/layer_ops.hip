@@ -143,8 +143,9 @@ __device__ __forceinline__ const float* bn_bwd_fin_prologue(const BNBwdFin& f, i
 __device__ __forceinline__ void put_partial(float* part, long long* acc, int reps, int C, int ch, float a, float b) {
   if (acc) {
     long long* r = acc + (size_t)(blockIdx.x % reps) * 4 * C;  // (backward sums: hi / lo planes)
-    bnacc_add2(r + ch, r + C + ch, a);
-    bnacc_add2(r + 2 * C + ch, r + 3 * C + ch, b);
+    long long* flag = acc + (size_t)max(reps, 1) * 4 * C + ch;   // sticky plane
+    bnacc_add2(r + ch, r + C + ch, flag, a);
+    bnacc_add2(r + 2 * C + ch, r + 3 * C + ch, flag, b);
   } else {
     part[(size_t)blockIdx.x * 2 * C + ch] = a;
     part[(size_t)blockIdx.x * 2 * C + C + ch] = b;

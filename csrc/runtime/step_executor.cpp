@@ -96,9 +96,23 @@ std::pair<int, int> StepExecutor::step_graph_nodes(int k) {
 }
 
 void StepExecutor::capture(int k) {
-  const Key key{k, phase_value()};
-  if (k <= 0 || graphs_.count(key)) return;
-  graphs_[key] = capture_steps(k, false);
+  if (k <= 0) return;
+  const int p = phase_value();
+  if (!graphs_.count(Key{k, p})) graphs_[Key{k, p}] = capture_steps(k, false);
+  // a k that moves the phase (e.g. an odd step count of the fused trainer): the variant for
+  // the phase a replay ends in is captured NOW too, not lazily inside run() -- which a timed
+  // loop would otherwise pay for (capture + instantiate + upload) on its second replay
+  const int q = phase_after(p, k, false);
+  if (q != p && !graphs_.count(Key{k, q})) {
+    set_phase(q);
+    try {
+      graphs_[Key{k, q}] = capture_steps(k, false);
+    } catch (...) {
+      set_phase(p);
+      throw;
+    }
+    set_phase(p);
+  }
 }
 
 void StepExecutor::capture_final(int k) {

@@ -5,6 +5,14 @@ from ..utils import env
 from ..utils import logging as dlog
 
 
+class ExchangeFault(RuntimeError):
+    """A bounded in-kernel exchange wait expired mid-run on at least one rank (collective
+    vote at the epoch's host sync, so EVERY rank raises it).  ``Model.fit`` answers with
+    :meth:`~.fused_convnet.FusedConvNetEngine.rebuild_after_fault`: the epoch restarts from its start-of-epoch
+    snapshot on the next transport, instead of the whole gang restarting."""
+
+
+
 class Engine:
     """Executes training steps for one (model, strategy, batch) configuration."""
 

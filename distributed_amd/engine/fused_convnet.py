@@ -21,7 +21,7 @@ import torch
 
 from ..utils import env
 from ..utils import logging as dlog
-from .base import Engine
+from .base import Engine, ExchangeFault  # noqa: F401  (ExchangeFault: re-exported)
 from .data import DataFeed
 
 
@@ -37,6 +37,14 @@ HID, NCLS, FEAT, NCONV = 64, 10, 5408, 320
 (C_LR, C_MOM, C_NEST, C_NS, C_ROW0, C_GB, C_CUR, C_IT, C_CA, C_CB, C_AL, C_AC, C_AN, C_WRAP, C_CUR2, C_CUR3, C_WPAR,
  C_FLUSHT, C_PEND, C_PAR2, C_BAD, C_XCNT, C_XCNT2, C_TICKET, C_PEND2, C_XGEN) = range(26)
 SHAPES = [(3, 3, 1, 32), (32,), (5408, 64), (64,), (64, 10), (10,)]
+
+
+def _xchg_fault_at(rank: int, world: int):
+    spec = env.get_str("DAMD_XCHG_FAULT_AT", "")
+    if not spec or world < 2:
+        return None
+    r, _, st = spec.partition(":")
+    return int(st) if int(r) == rank else None
 
 
 def _f2i(f: float) -> int:
@@ -85,7 +93,7 @@ class FusedConvNetEngine(Engine):
                 return False, f"metric {m.name}"
         return True, ""
 
-    def __init__(self, model, strategy, per_replica_batch, global_batch):
+    def __init__(self, model, strategy, per_replica_batch, global_batch, exclude=()):
         super().__init__(model, strategy, per_replica_batch, global_batch)
         from ..native import require_C
 
@@ -176,6 +184,8 @@ class FusedConvNetEngine(Engine):
         # at world 1: the multi-GPU graph path exercised on a single GPU
         force = env.get_bool("DAMD_FORCE_ALLREDUCE", False)
         native = strategy.communicator.native if (self.world > 1 or force) else None
+        if "rccl" in (exclude or ()):
+            native = None  # RCCL faulted mid-run on this gang: host all-reduce from here on
         # per-step gradient exchange at world > 1 (DAMD_ALLREDUCE):
         #   auto / sharded -- inside the two step kernels (convnet.h XArgs): each rank owns a
         #       quarter-slice unit of dW1 per 1/world of the units, bwd pushes partials to the
@@ -187,12 +197,17 @@ class FusedConvNetEngine(Engine):
         # Both peer modes need every rank to map every peer (one node); else RCCL.
         self.peer = None
         self.sharded = False
+        # transports never to use again on this engine: the ones a mid-run exchange fault
+        # was detected on (rebuild_after_fault)
+        self.exclude = set(exclude or ())
+        self.transport_us: dict = {}  # measured us / step per candidate exchange (auto mode)
         # start-up self-test outcome of the device exchange (None: no device exchange was
         # self-tested -- world 1, RCCL or the host all-reduce) and the transports that failed it
         self.exchange_verified = None
         self.exchange_fallback_from: list = []
         self.hred = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)  # sharded: conv sums for flush
         mode = env.get_str("DAMD_ALLREDUCE", "auto").lower()
+        self._mode = mode
         if mode not in ("auto", "sharded", "xgmi", "rccl", "off"):
             raise ValueError("DAMD_ALLREDUCE must be auto, sharded, xgmi, rccl or off")
         # DAMD_GRAD_DTYPE=bf16: the exchanged dW1 travels as bf16 (fp32 accumulation by the
@@ -200,7 +215,7 @@ class FusedConvNetEngine(Engine):
         self.grad_dtype = env.get_str("DAMD_GRAD_DTYPE", "fp32").lower()
         if self.grad_dtype not in ("fp32", "bf16"):
             raise ValueError("DAMD_GRAD_DTYPE must be fp32 or bf16")
-        if self.world > 1 and mode not in ("rccl", "off"):
+        if self.world > 1 and mode not in ("rccl", "off") and not {"xgmi-sharded", "xgmi-peer"} <= self.exclude:
             from ..parallel.communicator import make_peer_allreduce
 
             # in-kernel wait deadline: the collective watchdog's (its default included), so a
@@ -232,25 +247,49 @@ class FusedConvNetEngine(Engine):
                 cu_split = ((share.index(self.rank), len(share))
                             if len(share) > 2 and env.get_bool("DAMD_SHARED_CU_SPLIT", True) else None)
                 # start-up self-test of each candidate transport against the host rank-order
-                # reduction, bitwise, on every rank (engine/xchg_selftest.py); the first that
-                # passes carries the run: sharded -> xgmi -> RCCL
-                cands = (["xgmi-sharded"] if want_sharded else []) + ([] if mode == "sharded" else ["xgmi-peer"])
-                chosen = None
-                if env.get_bool("DAMD_XCHG_SELFTEST", True):
-                    from . import xchg_selftest
+                # reduction, bitwise, on every rank (engine/xchg_selftest.py); then, with the
+                # transport not pinned, every candidate that passed (and RCCL) is TIMED the way
+                # bench.py times its window, and the fastest carries the run (reference
+                # README.md:398, communication = AUTO).  Without tuning: the first that passes,
+                # sharded -> xgmi -> RCCL.
+                cands = [k for k in ((["xgmi-sharded"] if want_sharded else [])
+                                     + ([] if mode == "sharded" else ["xgmi-peer"])) if k not in self.exclude]
+                tune = (mode == "auto" and env.get_bool("DAMD_XCHG_TUNE", True))
+                from . import xchg_selftest
 
+                passed = []
+                selftested = env.get_bool("DAMD_XCHG_SELFTEST", True)
+                if selftested:
                     for kind in cands:
                         if xchg_selftest.verify(kind, C, strategy.communicator, self.peer, dev, B, self.PPB, self.PP,
                                                 self.P, gbf16=self.grad_dtype == "bf16" and kind == "xgmi-sharded",
                                                 cu_split=cu_split):
-                            chosen = kind
-                            self.exchange_verified = True
-                            break
-                        self.exchange_fallback_from.append(kind)
-                    self.peer.set_timeout(wd if wd > 0 else 60.0)
+                            passed.append(kind)
+                            if not tune:
+                                break
+                        else:
+                            self.exchange_fallback_from.append(kind)
                 else:
-                    chosen = cands[0]
-                if chosen is None:
+                    passed = list(cands) if tune else cands[:1]
+                chosen = passed[0] if passed else None
+                timed = passed + (["rccl"] if (native is not None and "rccl" not in self.exclude) else [])
+                if tune and len(timed) > 1:
+                    for kind in timed:
+                        t = xchg_selftest.time_transport(kind, C, strategy.communicator, self.peer, native, dev, B,
+                                                         self.PPB, self.PP, self.P,
+                                                         gbf16=self.grad_dtype == "bf16" and kind == "xgmi-sharded",
+                                                         cu_split=cu_split)
+                        if t is not None:
+                            self.transport_us[kind] = round(t * 1e6, 2)
+                    if self.transport_us:
+                        chosen = min(self.transport_us, key=self.transport_us.get)
+                # in-kernel wait deadline of the run (DAMD_XCHG_TIMEOUT_S: shorter, for tests)
+                self.peer.set_timeout(env.get_float("DAMD_XCHG_TIMEOUT_S", wd if wd > 0 else 60.0))
+                if selftested and chosen is not None and chosen != "rccl":
+                    self.exchange_verified = True
+                if chosen == "rccl":
+                    self.peer = None  # RCCL measured fastest: set_comm below
+                elif chosen is None:
                     if mode in ("xgmi", "sharded"):
                         raise ExchangeSelfTestError(f"DAMD_ALLREDUCE={mode}: the exchange failed its start-up self-test")
                     dlog.warning("fused ConvNet engine: no xGMI exchange passed its self-test; using %s",
@@ -286,6 +325,9 @@ class FusedConvNetEngine(Engine):
                       {"xgmi-sharded": "the step kernels (sharded xGMI exchange)",
                        "xgmi-peer": "xGMI peer-to-peer all-reduce kernel", "rccl": "RCCL",
                        "host-gloo": "host (gloo)"}[self.allreduce_kind])
+            if self.transport_us:
+                dlog.info("gradient exchange: %s (%s)", self.allreduce_kind,
+                          ", ".join(f"{k} {v:.1f} us" for k, v in self.transport_us.items()))
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.graph_steps = max(1, env.get_int("DAMD_GRAPH_STEPS", 20))
         self.watchdog_s = env.get_float("DAMD_WATCHDOG_S", 0.0)
@@ -293,16 +335,25 @@ class FusedConvNetEngine(Engine):
         self.feed = None
         self._pending = False
         self.steps_done = 0
+        self._fault_done = bool(exclude)  # the fault injection fires once per gang
         dlog.debug("fused ConvNet engine: B=%d, slices=%d, graph=%s", B, NS, self.use_graph)
 
     # --- host <-> ctrl ---------------------------------------------------------------
-    def _ctrl_host(self):
+    def _ctrl_host(self, soft=False):
         self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
-        self._check_peer()
+        self._check_peer(soft)
         return self.ctrl.cpu().tolist()
 
-    def _check_peer(self):
+    def _check_peer(self, soft=False):
         if self.peer is not None and self.peer.status():
+            if soft:
+                # mid-epoch read with fault recovery on: the epoch-end vote decides (every
+                # rank together) -- raising here on one rank would strand the others
+                if not getattr(self, "_fault_logged", False):
+                    dlog.warning("gradient exchange %s: a bounded wait expired on rank %d; the epoch will be "
+                                 "re-run on another transport", self.allreduce_kind, self.rank)
+                    self._fault_logged = True
+                return
             raise RuntimeError("xGMI peer all-reduce: a wait for a peer timed out (peer missing or wedged)")
 
     def _ctrl_write(self, updates: dict):
@@ -387,6 +438,20 @@ class FusedConvNetEngine(Engine):
                           C_LR: _f2i(opt.learning_rate), C_MOM: _f2i(opt.momentum), C_NEST: int(opt.nesterov)})
 
     def run(self, n_steps):
+        fa = _xchg_fault_at(self.rank, self.world)
+        if fa is not None and self.steps_done <= fa < self.steps_done + n_steps and not self._fault_done:
+            # tests only (DAMD_XCHG_FAULT_AT=rank:step): this rank stalls before launching
+            # global step `step`, so the other ranks' bounded exchange waits expire
+            import time
+
+            self._fault_done = True
+            k = fa - self.steps_done
+            if k:
+                self.run(k)
+            self.trainer.sync(0.0)
+            time.sleep(env.get_float("DAMD_XCHG_FAULT_DELAY_S", 3.0))
+            self.run(n_steps - k)
+            return
         if self.host_collective:
             for _ in range(n_steps):
                 self.trainer.step(1)
@@ -464,12 +529,13 @@ class FusedConvNetEngine(Engine):
             self._pending = False
 
     def metrics(self):
-        c = self._ctrl_host()
+        soft = self.recovers_faults
+        c = self._ctrl_host(soft)
         # the last step's reduced metric tail (in the peer `out` staging when folded)
         tail = list(self.trainer.metric_tail()) if self._pending else [0.0, 0.0, 0.0]
         # metric_tail's gather waits (bounded) for every rank's last message: a wait that
         # expired there leaves a stale tail -- never report it
-        self._check_peer()
+        self._check_peer(soft)
         loss = _i2f(c[C_AL]) + tail[0]
         corr = _i2f(c[C_AC]) + tail[1]
         cnt = _i2f(c[C_AN]) + tail[2]
@@ -483,7 +549,61 @@ class FusedConvNetEngine(Engine):
 
     def end_epoch(self):
         self._flush()
+        if self.recovers_faults:
+            self._vote_exchange_health()
         return self.metrics()
+
+    # --- mid-run exchange faults -------------------------------------------------------
+    @property
+    def recovers_faults(self) -> bool:
+        """A device exchange whose waits are bounded (sharded / peer): a wait that expires is
+        recovered from at the epoch's end (DAMD_XCHG_RECOVER=0: raise, gang restart)."""
+        return (self.world > 1 and self.peer is not None and self._mode == "auto"
+                and env.get_bool("DAMD_XCHG_RECOVER", True))
+
+    def recovery_snapshot(self):
+        """Host copy of the state an epoch restarts from after an exchange fault (parameters,
+        momentum, iteration count), taken at the epoch's start; None without a device
+        exchange to recover."""
+        if not self.recovers_faults:
+            return None
+        self._flush()
+        self.trainer.sync(self.watchdog_s) or self._watchdog_fired()
+        return {"P": self.P[:NPARAM].cpu().clone(), "V": self.V[:NPARAM].cpu().clone(),
+                "it": int(self.ctrl.cpu()[C_IT]), "kind": self.allreduce_kind}
+
+    def _vote_exchange_health(self):
+        done = bool(self.trainer.sync(self.watchdog_s if self.watchdog_s > 0 else 120.0))
+        st = int(self.peer.status()) if self.peer is not None else 0
+        votes = self.strategy.communicator.allgather_object((done, st))
+        bad = [r for r, (d, q) in enumerate(votes) if not d or q]
+        if bad:
+            raise ExchangeFault(f"gradient exchange {self.allreduce_kind}: bounded waits expired on rank(s) {bad}")
+
+    def rebuild_after_fault(self, snap):
+        """A fresh engine on the next transport (the faulted one excluded), whose state is
+        ``snap`` (recovery_snapshot of the epoch's start).  Collective: every rank calls it
+        after the same ExchangeFault."""
+        failed = snap["kind"]
+        self.trainer.sync(5.0)
+        if self.peer is not None:
+            self.peer.clear_status()
+        torch.cuda.synchronize(self.device)
+        self.P[:NPARAM].copy_(snap["P"].to(self.device))  # the model's variables are views of P
+        opt = self.model.optimizer
+        opt._iter_source = None
+        opt.iterations = snap["it"]
+        if opt.momentum:
+            opt.ensure_slots(NPARAM, self.device)
+            opt.slots["momentum"].copy_(snap["V"].to(self.device))
+        torch.cuda.synchronize(self.device)
+        self.peer = None  # this engine is done: no host read may see its status again
+        dlog.warning("gradient exchange %s faulted mid-run: re-running the epoch from its start on the next "
+                     "transport", failed)
+        new = FusedConvNetEngine(self.model, self.strategy, self.per_replica, self.global_batch,
+                                 exclude=self.exclude | {failed})
+        new.exchange_fallback_from = list(self.exchange_fallback_from) + [f"{failed} (mid-run)"]
+        return new
 
     def finish(self):
         self._flush()

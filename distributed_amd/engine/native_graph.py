@@ -589,15 +589,17 @@ class NativeGraphEngine(Engine):
             return
         R = max(1, env.get_int("DAMD_BN_REPS", 8))
         # int64 fixed point (ops/hip.py bn_acc_encode): forward [R][2C] one word per value,
-        # backward [R][4C] two words per value
-        tot = sum(6 * R * nd.out.shape[-1] for nd in bns)
+        # backward [R][4C] two words per value, each followed by its sticky flag plane
+        # (damd_common.h bnacc_flag)
+        tot = sum(6 * (R + 1) * nd.out.shape[-1] for nd in bns)
         self.bn_acc = torch.zeros(tot, dtype=torch.int64, device=self.device)
         o = 0
         for nd in bns:
             C = nd.out.shape[-1]
-            nd.attrs["acc_f"] = self.bn_acc[o:o + 2 * C * R].view(R, 2 * C)
-            nd.attrs["acc_b"] = self.bn_acc[o + 2 * C * R:o + 6 * C * R].view(R, 4 * C)
-            o += 6 * C * R
+            nf, nb = 2 * C * (R + 1), 4 * C * (R + 1)
+            nd.attrs["acc_f"] = self.bn_acc[o:o + nf].view(R + 1, 2 * C)
+            nd.attrs["acc_b"] = self.bn_acc[o + nf:o + nf + nb].view(R + 1, 4 * C)
+            o += nf + nb
             if nd.attrs.get("stats_from_conv"):
                 self._producer(nd.inputs[0]).attrs["stats_buf"] = nd.attrs["acc_f"]
             l = nd.layer

@@ -48,7 +48,7 @@ def _f2i(f: float) -> int:
 class _Scratch:
     """One scratch trainer + buffers (what FusedConvNetEngine allocates), starting at P0."""
 
-    def __init__(self, C, dev, B, GB, rank, P0, X, Y, ppb, PP):
+    def __init__(self, C, dev, B, GB, rank, P0, X, Y, ppb, PP, wrap=0):
         f32 = dict(dtype=torch.float32, device=dev)
         BP = (B + 63) // 64 * 64
         self.P = P0.clone()
@@ -66,7 +66,7 @@ class _Scratch:
         self.hred = torch.zeros(2 * NCONV, dtype=torch.int64, device=dev)
         c = torch.zeros(32, dtype=torch.int32)
         c[C_LR], c[C_MOM], c[C_NEST] = _f2i(0.1), _f2i(0.9), 0
-        c[C_NS], c[C_ROW0], c[C_GB], c[C_WRAP] = X.shape[0], rank * B, GB, 0
+        c[C_NS], c[C_ROW0], c[C_GB], c[C_WRAP] = X.shape[0], rank * B, GB, int(wrap)
         self.ctrl.copy_(c.to(dev))
         bufs = dict(params=self.P.data_ptr(), grads=self.G.data_ptr(), velocity=self.V.data_ptr(),
                     ctrl=self.ctrl.data_ptr(), pooled=self.pooled.data_ptr(), code=self.code.data_ptr(),
@@ -116,25 +116,52 @@ def _host_reference(C, comm, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16):
     return s.result()
 
 
-def _under_test(kind, C, comm, peer, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16, cu_split):
-    s = _Scratch(C, dev, B, GB, rank, P0, X, Y, ppb, PP)
+def _setup(kind, C, comm, peer, native, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16, cu_split, wrap=0):
+    """A scratch trainer wired to transport ``kind``.  Local only: the caller votes on
+    the outcome BEFORE any collective that assumes every rank got this far."""
+    s = _Scratch(C, dev, B, GB, rank, P0, X, Y, ppb, PP, wrap)
     if cu_split is not None:
         s.t.restrict_cus(*cu_split)
     if kind == "xgmi-sharded":
         s.t.set_sharded(peer, s.hred.data_ptr(), int(gbf16))
         s.t.set_exchange_timeout(TIMEOUT_S)
-        comm.barrier()  # every rank's flags are cleared before any rank's first step
     elif kind == "xgmi-peer":
         peer.set_timeout(TIMEOUT_S)
         s.t.set_peer(peer, fold=True)
+    elif kind == "rccl":
+        if native is None:
+            raise ValueError("rccl: no native RCCL communicator")
+        s.t.set_comm(native)
     else:
         raise ValueError(kind)
+    return s
+
+
+def _voted_setup(kind, comm, *args):
+    """(scratch, why) on every rank; scratch None on EVERY rank if any rank's set-up failed
+    (restrict_cus / set_sharded / set_peer raising on one rank must not leave that rank
+    in a different collective than the others)."""
+    s, why = None, ""
+    try:
+        s = _setup(kind, *args)
+    except Exception as e:  # every rank must reach the vote below
+        why = f"set-up raised {e!r}"
+    votes = comm.allgather_object(why)
+    bad = [(r, w) for r, w in enumerate(votes) if w]
+    if bad:
+        return None, "; ".join(f"rank {r}: {w}" for r, w in bad)
+    if kind == "xgmi-sharded":
+        comm.barrier()  # every rank's flags are cleared before any rank's first step
+    return s, ""
+
+
+def _run_under_test(s, peer):
     s.t.step(STEPS)
     done = s.t.sync(4 * TIMEOUT_S + 30.0)
     s.t.flush()
     done = s.t.sync(4 * TIMEOUT_S + 30.0) and done
-    torch.cuda.synchronize(dev)
-    st = peer.status()
+    torch.cuda.synchronize()
+    st = peer.status() if peer is not None else 0
     return s.result(), bool(done), int(st)
 
 
@@ -157,15 +184,20 @@ def verify(kind: str, C, comm, peer, dev, B: int, ppb: int, PP: int, P0: torch.T
     n = GB * (STEPS + 1)
     X = torch.from_numpy(rng.integers(0, 256, size=(n, 784), dtype=np.uint8)).to(dev)
     Y = torch.from_numpy(rng.integers(0, 10, size=n).astype(np.int32)).to(dev)
-    ok, why = True, ""
+    ok, why, got = True, "", None
+    s, why = _voted_setup(kind, comm, kind, C, comm, peer, None, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16, cu_split)
+    if s is None:  # identical on every rank: skip the run AND the host reference
+        dlog.warning("gradient exchange %s: self-test set-up failed (%s)", kind, why)
+        return False
     try:
-        got, done, st = _under_test(kind, C, comm, peer, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16, cu_split)
+        got, done, st = _run_under_test(s, peer)
         if _inject_target(kind, rank):
             got[0][0] = torch.nextafter(got[0][0], torch.tensor(float("inf")))
         if not done or st != 0:
             ok, why = False, f"exchange waits expired (status {st:#x})" if st else "step did not complete"
     except Exception as e:  # every rank must reach the vote below
         ok, why, got = False, f"raised {e!r}", None
+    del s
     try:
         ref = _host_reference(C, comm, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16 and kind == "xgmi-sharded")
     except Exception as e:
@@ -191,3 +223,54 @@ def verify(kind: str, C, comm, peer, dev, B: int, ppb: int, PP: int, P0: torch.T
         dlog.info("gradient exchange %s: start-up self-test passed (%d steps bitwise equal to the host "
                   "rank-order reduction on %d ranks)", kind, STEPS, W)
     return all_ok
+
+
+def time_transport(kind: str, C, comm, peer, native, dev, B: int, ppb: int, PP: int, P0: torch.Tensor,
+                   gbf16: bool = False, cu_split: Optional[Tuple[int, int]] = None,
+                   steps: int = 20) -> Optional[float]:
+    """Seconds per step of transport ``kind`` ('xgmi-sharded' | 'xgmi-peer' | 'rccl'), max over
+    ranks, or None on EVERY rank if it could not be timed (collective).
+
+    Measured the way bench.py times its headline window: ``steps`` training steps + the
+    flush of the last deferred update captured as ONE graph (capture_final), one untimed
+    replay, then a barrier, one timed replay and a device synchronize.  Scratch buffers on
+    synthetic rows, so the model's own state is untouched; the kernels are the ones a real
+    step runs (reference README.md:398, ``CollectiveCommunication.AUTO``: the runtime, not
+    the user, picks the collective implementation)."""
+    import time
+
+    W, rank = comm.world_size, comm.rank
+    GB = B * W
+    wrap = 4
+    rng = np.random.default_rng(777)
+    X = torch.from_numpy(rng.integers(0, 256, size=(GB * wrap, 784), dtype=np.uint8)).to(dev)
+    Y = torch.from_numpy(rng.integers(0, 10, size=GB * wrap).astype(np.int32)).to(dev)
+    s, why = _voted_setup(kind, comm, kind, C, comm, peer, native, dev, B, GB, rank, P0, X, Y, ppb, PP, gbf16,
+                          cu_split, wrap)
+    if s is None:
+        dlog.warning("gradient exchange %s: not timed (%s)", kind, why)
+        return None
+    dt, ok = 0.0, True
+    try:
+        s.t.capture_final(int(steps))
+        s.t.run_final(int(steps))  # untimed: first replay
+        ok = bool(s.t.sync(4 * TIMEOUT_S + 30.0))
+    except Exception as e:  # every rank must reach the collectives below
+        dlog.warning("gradient exchange %s: timing run raised %r", kind, e)
+        ok = False
+    comm.barrier()
+    if ok:
+        t0 = time.perf_counter()
+        s.t.run_final(int(steps))
+        ok = bool(s.t.sync(4 * TIMEOUT_S + 30.0))
+        dt = time.perf_counter() - t0
+    st = peer.status() if (peer is not None and kind != "rccl") else 0
+    votes = comm.allgather_object((ok and st == 0, dt))
+    if peer is not None:
+        peer.clear_status()
+    torch.cuda.synchronize(dev)
+    del s
+    if not all(v[0] for v in votes):
+        dlog.warning("gradient exchange %s: timing run failed on some rank", kind)
+        return None
+    return max(v[1] for v in votes) / steps

@@ -299,6 +299,12 @@ class JSONMetricsLogger(Callback):
                "seconds": dt, "ms_per_step": 1e3 * dt / steps if steps else None,
                "images_per_sec": steps * bs / dt if dt > 0 else None,
                "engine": getattr(getattr(self.model, "_engine", None), "name", None)}
+        eng = getattr(self.model, "_engine", None)
+        if getattr(eng, "world", 1) > 1:
+            # which gradient exchange carried the epoch, and what each candidate measured
+            rec["gradient_exchange"] = getattr(eng, "allreduce_kind", None)
+            if getattr(eng, "transport_us", None):
+                rec["exchange_us_per_step"] = dict(eng.transport_us)
         line = json.dumps(rec)
         if self.path:
             with open(self.path, "a") as f:

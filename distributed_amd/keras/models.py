@@ -23,6 +23,7 @@ import time
 import numpy as np
 import torch
 
+from ..engine.base import ExchangeFault as _ExchangeFault
 from ..parallel import runtime as _runtime
 from ..parallel.strategy import MultiWorkerMirroredStrategy, get_strategy
 from ..utils import debug as _debug
@@ -256,8 +257,15 @@ class Model(L.Layer):
             watchdog.arm("first step (includes graph capture / communicator set-up)")
         hang_at = _hang_injection()
         try:
-            for epoch in range(initial_epoch, epochs):
+            epoch = initial_epoch
+            recoveries = 0
+            while epoch < epochs:
                 cl.on_epoch_begin(epoch)
+                # fused engine with a device exchange: the epoch's start state on the host, so
+                # a bounded exchange wait that expires mid-epoch re-runs the epoch on the next
+                # transport instead of ending the gang (ExchangeFault below)
+                snap = engine.recovery_snapshot() if hasattr(engine, "recovery_snapshot") else None
+                step0 = global_step
                 engine.start_epoch(epoch, shuffle)
                 done, last_ui = 0, time.time()
                 chunk = 1 if per_hook else max(1, min(steps, 200))
@@ -291,7 +299,19 @@ class Model(L.Layer):
                         logs["size"] = batch_size
                         cl.on_train_batch_end(done - 1, logs)
                         last_ui = time.time()
-                logs = self._public(engine.end_epoch())  # host sync: the epoch's device work is done
+                try:
+                    logs = self._public(engine.end_epoch())  # host sync: the epoch's device work is done
+                except _ExchangeFault as e:
+                    # every rank raised it (collective vote): restart this epoch from its
+                    # snapshot on the next transport
+                    if snap is None or recoveries >= 3:
+                        raise
+                    recoveries += 1
+                    dlog.warning("epoch %d: %s; re-running it", epoch + 1, e)
+                    engine = self._engine = engine.rebuild_after_fault(snap)
+                    engine.bind(x, y)
+                    global_step = step0
+                    continue
                 self.sync_on_read_variables()  # BN moving statistics: replica mean (all ranks)
                 if watchdog is not None:
                     watchdog.beat(f"epoch {epoch + 1} end")
@@ -303,6 +323,7 @@ class Model(L.Layer):
                 cl.on_epoch_end(epoch, {k: v for k, v in logs.items()})
                 if mirror_every and (epoch + 1) % mirror_every == 0:
                     _debug.check_mirrored(self, st, tag=f"epoch {epoch + 1}")
+                epoch += 1
                 if self.stop_training:
                     break
         except BaseException:

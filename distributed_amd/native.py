@@ -22,11 +22,47 @@ def _try_import(name):
     return importlib.import_module(f"distributed_amd.{name}")
 
 
+class StaleExtensionError(ImportError):
+    """The in-tree ``_C`` was built from other sources than the tree's ``csrc/``."""
+
+
+def check_fresh(so=None, csrc=None) -> None:
+    """Raise :class:`StaleExtensionError` if the built ``_C`` (``so``) does not carry the hash
+    of the sources in ``csrc`` (default: this tree).  No-op when the sources are absent (an
+    installed package) or ``DAMD_ALLOW_STALE=1``."""
+    import os
+    from pathlib import Path
+
+    from . import _build
+
+    if os.environ.get("DAMD_ALLOW_STALE", "0") == "1":
+        return
+    csrc = Path(csrc or os.environ.get("DAMD_CSRC_ROOT") or _build.CSRC)
+    so = Path(so or (_build.PKG / f"_C{_build.EXT}"))
+    if not (csrc / "bindings.cpp").exists() or not so.exists():
+        return
+    have, want = _build.embedded_hash(so), _build.source_hash(csrc)
+    if have != want:
+        raise StaleExtensionError(
+            f"{so.name} was built from other sources than {csrc} (embedded hash {have and have[:12]}, "
+            f"sources {want[:12]}): rebuild with `python -m distributed_amd._build` "
+            "(DAMD_ALLOW_STALE=1 runs it anyway)")
+
+
 def load_C(build_if_missing: bool = True):
     global _C, _err
     with _lock:
         if _C is not None:
             return _C
+        try:
+            check_fresh()  # before the import: a loaded extension cannot be replaced
+        except StaleExtensionError:
+            if not build_if_missing:
+                raise
+            from . import _build
+
+            _build._build_C()
+            check_fresh()
         try:
             _C = _try_import("_C")
         except ImportError as e:  # not built yet

@@ -249,9 +249,19 @@ def _wgrad_gemm(A, B, dw, workspace, *, amode, M, N, K, lda=0, ldb=0, geo=(), ac
 
 def acc_reps(acc):
     """Replica count of a BatchNorm statistics accumulator (int64 fixed point, layer_ops.h
-    BNFin): [reps, 2C] forward / [reps, 4C] backward (2-D) or a single replica (1-D).
-    Producer block b adds into replica b % reps."""
-    return int(acc.shape[0]) if acc is not None and acc.dim() == 2 else 1
+    BNFin): [reps + 1, 2C] forward / [reps + 1, 4C] backward (2-D: the last row is the sticky
+    non-finite flag plane, damd_common.h bnacc_flag) or one replica + its flag plane (1-D,
+    [2 x K]).  Producer block b adds into replica b % reps."""
+    if acc is None or acc.dim() != 2:
+        return 1
+    if acc.shape[0] < 2:
+        raise ValueError("a BatchNorm accumulator needs >= 1 replica row + the flag row")
+    return int(acc.shape[0]) - 1
+
+
+def acc_zeros(reps: int, K: int, device) -> torch.Tensor:
+    """A cleared accumulator of ``reps`` replicas of K words + the flag plane."""
+    return torch.zeros(reps + 1, K, dtype=torch.int64, device=device)
 
 
 # Fixed-point BatchNorm accumulators (csrc/include/damd_common.h bnacc_add1 / bnacc_add2):
@@ -277,17 +287,25 @@ def bn_acc_encode(values: torch.Tensor, words: int = 1) -> torch.Tensor:
 
 
 def bn_acc_decode(acc: torch.Tensor, words: int = 1) -> torch.Tensor:
-    """Replica-summed values of an accumulator ([reps, K * words] or [K * words]) as fp64."""
+    """Replica-summed values of an accumulator ([reps + 1, K] or [2K]: replicas then the flag
+    plane) as fp64; NaN where a channel's flag is set."""
     a = acc.cpu()
     if a.dim() == 1:
-        a = a.unsqueeze(0)
-    a = a.sum(0)
+        a = a.view(2, -1)
+    flag = a[-1]
+    a = a[:-1].sum(0)
     if words == 1:
-        return a.double() * ACC_UNIT
-    C = a.numel() // 4
-    s = a[:C].double() * ACC_UNIT + a[C:2 * C].double() * 2.0 ** -64
-    q = a[2 * C:3 * C].double() * ACC_UNIT + a[3 * C:].double() * 2.0 ** -64
-    return torch.cat([s, q])
+        C = a.numel() // 2
+        out = a.double() * ACC_UNIT
+        bad = torch.cat([flag[:C] != 0] * 2)
+    else:
+        C = a.numel() // 4
+        s = a[:C].double() * ACC_UNIT + a[C:2 * C].double() * 2.0 ** -64
+        q = a[2 * C:3 * C].double() * ACC_UNIT + a[3 * C:].double() * 2.0 ** -64
+        out = torch.cat([s, q])
+        bad = torch.cat([flag[:C] != 0] * 2)
+    out[bad] = float("nan")
+    return out
 
 
 def _stats_ptrs(stats):
@@ -470,8 +488,9 @@ def _check_stats(stats, plan, cout, who):
     if stats is None:
         return
     if stats.dtype == torch.int64:
-        if stats.numel() != 2 * cout * acc_reps(stats) or stats.shape[-1] != 2 * cout:
-            raise ValueError(f"{who}: a statistics accumulator is int64 [reps][2 x {cout}], got {tuple(stats.shape)}")
+        if stats.numel() != 2 * cout * (acc_reps(stats) + 1) or stats.shape[-1] != 2 * cout:
+            raise ValueError(f"{who}: a statistics accumulator is int64 [reps + 1][2 x {cout}], "
+                             f"got {tuple(stats.shape)}")
     elif stats.shape[0] != plan["stats_T"]:
         raise ValueError(f"{who}: stats needs {plan['stats_T']} partial rows, got {stats.shape[0]}")
 

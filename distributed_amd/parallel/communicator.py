@@ -31,6 +31,9 @@ class Communicator:
     name = "base"
     world_size = 1
     rank = 0
+    # control-plane collectives issued (barrier / object all-gather / object broadcast):
+    # bench.py checks that none runs inside a timed window
+    control_ops = 0
 
     def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         raise NotImplementedError
@@ -142,14 +145,17 @@ class TorchCommunicator(Communicator):
         return torch.stack(out)
 
     def barrier(self):
+        self.control_ops += 1
         dist.barrier()
 
     def allgather_object(self, obj):
+        self.control_ops += 1
         out = [None] * self.world_size
         dist.all_gather_object(out, obj)
         return out
 
     def broadcast_object(self, obj, root=0):
+        self.control_ops += 1
         box = [obj]
         dist.broadcast_object_list(box, src=root)
         return box[0]

@@ -57,7 +57,7 @@ for (hw, c) in [(56, 64), (28, 128), (14, 256), (7, 512)]:
     tb, tbb = timeit(base), timeit(bwd_base)
     print(f"{hw}x{hw}x{c} (M {M}, T {T}): partials+finalize+apply fwd {tb:6.2f} us  bwd {tbb:6.2f} us")
     for r in REPS:
-        acc = torch.zeros(r, 4 * c, dtype=torch.int64, device=dev)  # (backward layout: 2 words / value)
+        acc = torch.zeros(r + 1, 4 * c, dtype=torch.int64, device=dev)  # (backward layout: 2 words / value; + flag plane)
         fin = H.BNFin(acc, gamma, beta, st, rm, rv, M, 1e-3, 0.99)
         red = lambda: C_.bn_bwd_reduce_acc(x.data_ptr(), 0, 0, x.data_ptr(), ident.data_ptr(), 0, acc.data_ptr(),
                                            T, M, c, s, r)

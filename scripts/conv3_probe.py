@@ -64,7 +64,7 @@ for h, cin, cout in SHAPES:
     print(f"fwd  {h}x{h} {cin}->{cout}: {t:7.2f} us  {flop / t / 1e6:6.1f} TFLOP/s  plan {plan['amode']} tile {plan['tile']}")
     phases(f, 4096)
     # the same conv on a BatchNorm's input (GemmArgs::bnin: finalize + BN/ReLU on load + y store)
-    acc = torch.zeros(8, 2 * cin, dtype=torch.int64, device=dev)
+    acc = torch.zeros(8 + 1, 2 * cin, dtype=torch.int64, device=dev)  # 8 replicas + the flag plane
     acc[0, cin:] = (B * h * h) << 24  # sum of squares = count (fixed point, 2^-24 units)
     bst = torch.zeros(4, cin, device=dev)
     fin = H.BNFin(acc, None, None, bst, None, None, B * h * h, 1e-3, 0.99)

@@ -1,0 +1,90 @@
+#!/bin/bash
+# Round-6 GPU checks, stage by stage (STAGES="tests rehearse bench ..." selects).  Every GPU
+# step has its own time limit; a fault, abort or timeout stops the script.
+set -u
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+step() {  # step <name> <limit_s> <cmd...>   (stdout/err -> gpurun_out/<name>.log)
+  local name=$1 lim=$2; shift 2
+  echo "=== $name (limit ${lim}s): $*"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 6 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then echo "STOP: $name rc=$rc"; exit $rc; fi
+  return 0
+}
+for s in ${STAGES:-xtests bench}; do
+  case $s in
+    xtests)  # the exchange: in-process sharded ranks, bitwise cross-transport, self-test fallback
+      step xtests 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread \
+        tests/test_sharded_inproc_gpu.py tests/test_peer_allreduce_gpu.py ;;
+    bn)  # BatchNorm fixed-point statistics
+      step bntests 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+        tests/test_hip_ops_gpu.py tests/test_conv_gemm_gpu.py -k "bn or bnin" ;;
+    tests)
+      step gputests 1100 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests ;;
+    bench)
+      step bench_n1 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      step bench_n1b 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      step bench_n1_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200 ;;
+    rehearse)  # the driver's multi-GPU launch, N ranks sharing cuda:0 (gloo control plane)
+      for N in ${RANKS:-2}; do
+        DAMD_COMM=gloo step share_n$N 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $N \
+          --master-addr 127.0.0.1 --master-port $((29500 + N)) bench.py --gpus $N --steps 200 --warmup 20
+      done ;;
+    fused)
+      step fused 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_fused_convnet_gpu.py ;;
+    bextra)  # the bench's window repeated (stderr): first-window vs steady cost at K = 20
+      DAMD_BENCH_EXTRA=3 step bench_extra 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      DAMD_GRAPH_STEPS=5 DAMD_BENCH_EXTRA=3 step bench_extra_g5 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      DAMD_BENCH_EXTRA=3 step bench_extra_b 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      DAMD_GRAPH_STEPS=5 DAMD_BENCH_EXTRA=3 step bench_extra_g5b 200 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    ab)  # same-box A/B: build/ab/A (scripts/ab_build.sh) against the working tree, alternating
+      for i in 1 2 3; do
+        step ab_A_long$i 200 bash -c "cd build/ab/A && python bench.py --gpus 1 --steps 2000 --warmup 200"
+        step ab_B_long$i 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+        step ab_A_short$i 200 bash -c "cd build/ab/A && python bench.py --gpus 1 --steps 20 --warmup 5"
+        step ab_B_short$i 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      done ;;
+    ppsweep)  # slice sizes: fwd positions per block (DAMD_PP) x bwd (DAMD_PP_BWD), long runs
+      for pp in 2 3 4; do for pb in 1 2 3; do
+        DAMD_PP=$pp DAMD_PP_BWD=$pb step pp_${pp}_${pb} 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      done; done ;;
+    ovh)  # fixed cost of a timed window (launch, flush, sync): fit over K
+      step overhead 300 python scripts/overhead_probe.py ;;
+    stamps)
+      step stamps 200 python scripts/stamps.py 64 ;;
+    gprobe)
+      step gprobe 300 python scripts/probe_graph_branches.py 4 8 ;;
+    dpprof)  # ResNet-18 N = 2 sharing the GPU: bucket all-reduce overlap (peer transport)
+      step dpprof 500 bash scripts/prof_resnet_dp.sh
+      python scripts/dp_overlap.py gpurun_out/prof_rn_dp/rn_kernel_trace.csv gpurun_out/dp_overlap.txt || true ;;
+    ngpeer)
+      step ngpeer 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_peer_allreduce_gpu.py -k native_graph ;;
+    c3)  # direct conv kernels on the ResNet-18 shapes
+      step c3base 300 python scripts/conv3_probe.py 64 ;;
+    mab)  # MNIST step A/B on one box: prefetch + parity hints on / off, alternating
+      for i in 1 2; do
+        step mab_on$i 200 python bench.py --gpus 1 --steps 20 --warmup 5
+        DAMD_XPREFETCH=0 DAMD_PAR_HINT=0 step mab_off$i 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      done
+      step mab_on_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      DAMD_XPREFETCH=0 DAMD_PAR_HINT=0 step mab_off_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      DAMD_XPREFETCH=0 DAMD_PAR_HINT=0 step stamps_off 200 python scripts/stamps.py 64
+      step stamps_on 200 python scripts/stamps.py 64 ;;
+    shdiag)  # the sharded exchange at N = 2 sharing the GPU: pinned, with / without the self-test
+      DAMD_COMM=gloo DAMD_ALLREDUCE=sharded step sh_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20
+      DAMD_COMM=gloo DAMD_ALLREDUCE=sharded DAMD_XCHG_SELFTEST=0 step sh_noself 300 python bench.py --gpus 2 --steps 200 --warmup 20
+      DAMD_COMM=gloo DAMD_ALLREDUCE=xgmi step xg_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20 ;;
+    resnet)
+      step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5
+      step resnet_long 300 python bench.py --model resnet18 --steps 100 --warmup 10 ;;
+    bnab)  # bn_bwd_reduce grid size A/B (fixed-point accumulator atomics vs memory parallelism)
+      for t in 1024 512 256; do
+        DAMD_BN_BWD_BLOCKS=$t step rn_bnt$t 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done ;;
+    rnprof)
+      step rnprof 400 bash scripts/prof_resnet.sh ;;
+  esac
+done
+echo stages-done

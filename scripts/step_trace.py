@@ -9,6 +9,10 @@ with open(out, 'w') as f:
     f.write("start_us  dur_us  workgroups  kernel\n")
     for r in rows[i:j]:
         s, e = int(r['Start_Timestamp']), int(r['End_Timestamp']); busy += e - s
-        wg = int(r['Grid_Size_X']) * int(r['Grid_Size_Y']) // max(1, int(r['Workgroup_Size_X']) * int(r['Workgroup_Size_Y']))
+        # rocprofv3 reports the grid in work-items per dimension: workgroups = product over
+        # X, Y AND Z (split-K launches put their slabs in Z)
+        gx, gy, gz = (int(r.get(f'Grid_Size_{d}') or 1) for d in 'XYZ')
+        bx, by, bz = (int(r.get(f'Workgroup_Size_{d}') or 1) for d in 'XYZ')
+        wg = (gx // max(1, bx)) * (gy // max(1, by)) * (gz // max(1, bz))
         f.write(f"{(s-t0)/1000:8.1f} {(e-s)/1000:7.1f} {wg:10d}  {r['Kernel_Name'][:90]}\n")
     f.write(f"busy {busy/1000:.1f} us, span {(int(rows[j]['Start_Timestamp'])-t0)/1000:.1f} us\n")

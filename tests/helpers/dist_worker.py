@@ -64,6 +64,7 @@ def main():
                    "exchange": getattr(eng, "allreduce_kind", None),
                    "exchange_verified": getattr(eng, "exchange_verified", None),
                    "fallback_from": list(getattr(eng, "exchange_fallback_from", []) or []),
+                   "transport_us": dict(getattr(eng, "transport_us", {}) or {}),
                    "iterations": int(model.optimizer.iterations)}, f)
     if rank == 0:
         np.savez(os.path.join(out, "init0.npz"), *init)

@@ -66,3 +66,38 @@ def test_bench_refuses_timing_probes():
     assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
     assert not lines
     assert "refusing" in r.stderr
+
+
+@pytest.mark.dist
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_dp8_window_has_no_host_collective():
+    """BASELINE configs 3 / 5 are 8 ranks at global batch 512 (README.md:413: global batch =
+    64 x workers).  bench.py --gpus 8 spawns 8 gloo ranks, prints ONE line for the job, and no
+    control-plane collective (barrier / object all-gather) runs between t0 and the
+    end-of-window device synchronize: the trailing barrier is outside the window and
+    reported on its own as barrier_us."""
+    r, lines = _run(["--gpus", "8", "--engine", "generic", "--steps", "3", "--warmup", "1"],
+                    {"OMP_NUM_THREADS": "1"}, timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 8
+    assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 512
+    assert out["control_collectives_in_window"] == 0
+    assert out["barrier_us"] >= 0
+    assert out["replicas_mirrored"] is True
+    # value is the whole-job rate: global batch x steps / window
+    assert abs(out["value"] - 512 * 1e3 / out["ms_per_step"]) / out["value"] < 1e-3
+
+
+def test_bench_timed_window_has_no_collective_between_t0_and_sync():
+    """Static check of bench.py's window: between t0 and t1 (the end-of-window device
+    synchronize) the only calls are the steps and the synchronize -- the barrier and the
+    all-gather of the per-rank times come after t1."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    body = src[src.index("    def timed(eng, k, final):"):src.index("    fail_at = runtime.fault_injection_step()")]
+    win = body[body.index("t0 = time.perf_counter()"):body.index("t1 = time.perf_counter()")]
+    for call in ("barrier()", "allgather_object", "broadcast_object", "all_reduce"):
+        assert call not in win, call
+    after = body[body.index("t1 = time.perf_counter()"):]
+    assert "barrier()" in after and "allgather_object" in after

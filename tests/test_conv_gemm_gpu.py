@@ -483,7 +483,7 @@ def test_direct_conv3_bn_input(H, monkeypatch, n, h, cin, cout, reps):
     sums = torch.cat([x64.sum(0), (x64 * x64).sum(0)])
     # split the sums over the replicas (the consumers add the replicas' integer words)
     acc = torch.stack([H.bn_acc_encode(sums * (0.5 ** (r + 1) if r < reps - 1 else 0.5 ** (reps - 1)))
-                       for r in range(reps)]).to(dev)
+                       for r in range(reps)] + [torch.zeros(2 * cin, dtype=torch.int64)]).to(dev)  # + flag plane
     M = n * h * h
     res = []
     for fold in (True, False):
@@ -492,7 +492,7 @@ def test_direct_conv3_bn_input(H, monkeypatch, n, h, cin, cout, reps):
         fin = H.BNFin(acc, gamma, beta, st, rm, rv, M, 1e-3, 0.99)
         y = torch.full(shape, float("nan"), device=dev, dtype=torch.bfloat16)
         out = torch.empty(n, h, h, cout, device=dev, dtype=torch.bfloat16)
-        ostat = torch.zeros(2 * cout, dtype=torch.int64, device=dev)
+        ostat = torch.zeros(2 * 2 * cout, dtype=torch.int64, device=dev)  # one replica + flag plane
         if fold:
             H.conv_fwd(xb, wb, out, (1, 1), "same", stats=ostat, bnin=(fin, y))
         else:

@@ -59,6 +59,33 @@ def test_two_workers_mirror_and_match_single_worker(tmp_path):
     np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-5)
 
 
+@pytest.mark.timeout(600)
+def test_eight_workers_mirror_and_match_single_worker(tmp_path):
+    """BASELINE configs 3 / 5 run 8 ranks: 8 workers x 8 rows per step == 1 worker x 64 rows
+    from the same initial weights; replicas bitwise mirrored, History identical on all 8
+    (README.md:229-231), rank-order sums over 8 ranks, ports base..base+7."""
+    d8 = tmp_path / "w8"
+    d8.mkdir()
+    res = launch.launch_script([WORKER], nproc=8, env=_env(d8, DAMD_TEST_PER_REPLICA=8, DAMD_CHECK_MIRRORS=1,
+                                                           DAMD_BUCKET_MB=0.05, OMP_NUM_THREADS=1), timeout=400)
+    assert res.ok, res.returncodes
+    outs = [_load(d8, r) for r in range(8)]
+    w0, j0 = outs[0]
+    assert j0["world"] == 8 and j0["iterations"] == 6
+    for w, j in outs[1:]:
+        assert all(np.array_equal(a, b) for a, b in zip(w0, w))
+        assert j["history"] == j0["history"]
+    d1 = tmp_path / "w1"
+    d1.mkdir()
+    res = launch.launch_script([WORKER], nproc=1, env=_env(d1, DAMD_TEST_PER_REPLICA=64,
+                                                           DAMD_TEST_INIT_FROM=d8 / "init0.npz"), timeout=240)
+    assert res.ok, res.returncodes
+    ws, js = _load(d1, 0)
+    for a, b in zip(w0, ws):
+        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(j0["history"]["loss"], js["history"]["loss"], rtol=1e-5)
+
+
 @pytest.mark.timeout(300)
 def test_short_last_batch_with_many_buckets(tmp_path):
     """70 rows at global batch 64: the second step has 6 rows, all on rank 0, so rank 1
@@ -148,6 +175,9 @@ def test_barrier_apply_order_and_error_strings():
 
 def test_barrier_apply_gang_restart():
     assert launch.barrier_apply(_crash_first_attempt, 2, max_restarts=1) == [1, 1]
+    # at the deployment size (BASELINE config 5: 8 local ranks): one task's crash restarts
+    # all 8, and every task of the second attempt reports it
+    assert launch.barrier_apply(_crash_first_attempt, 8, max_restarts=1) == [1] * 8
     with pytest.raises(RuntimeError):
         launch.barrier_apply(_crash_first_attempt, 2, max_restarts=0)
 
@@ -202,6 +232,51 @@ def _spark_closure(df, barrier):
         return str(max(result.metrics["accuracy"]))
     except Exception as e:  # error = function(e) e$message
         return str(e)
+
+
+def _spark_closure_derived_world(df, barrier):
+    """The README closure with the world size taken from the barrier (never
+    hard-code num_workers), a smaller slice of rows, and the partition index returned."""
+    import os as _os
+
+    _os.environ["DAMD_DEVICE"] = "cpu"
+    _os.environ["OMP_NUM_THREADS"] = "1"
+    from distributed_amd import r_api as k
+    import distributed_amd as tf
+
+    k.sys_setenv(TF_CONFIG=k.barrier_tf_config(barrier, base_port=int(_os.environ["SPARK_PORT_BASE"])))
+    strategy = tf.distribute.experimental.MultiWorkerMirroredStrategy()
+    num_workers = len(barrier["address"])
+    mnist = k.dataset_mnist()
+    x_train = k.array_reshape(mnist["train"]["x"][:1024], k.c(1024, 28, 28, 1)) / 255
+    y_train = mnist["train"]["y"][:1024]
+    with strategy.scope():
+        model = k.keras_model_sequential()
+        k.layer_conv_2d(model, filters=32, kernel_size=3, activation="relu", input_shape=k.c(28, 28, 1))
+        k.layer_max_pooling_2d(model)
+        k.layer_flatten(model)
+        k.layer_dense(model, units=64, activation="relu")
+        k.layer_dense(model, units=10)
+        k.compile(model, loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+                  optimizer=tf.keras.optimizers.SGD(learning_rate=0.001), metrics="accuracy")
+    result = k.fit(model, x_train, y_train, batch_size=64 * num_workers, epochs=2, steps_per_epoch=2, verbose=0)
+    return f"{barrier['partition']}/{strategy.num_replicas_in_sync}/{max(result.metrics['accuracy'])!r}"
+
+
+@pytest.mark.timeout(600)
+def test_spark_apply_eight_partitions_in_order(monkeypatch):
+    """BASELINE config 5: spark_apply(barrier=TRUE) over sdf_len(8) -> 8 rows, in partition
+    order, every rank training at world 8 and reporting the identical global accuracy."""
+    monkeypatch.setenv("SPARK_PORT_BASE", str(launch.free_port_base(9)))
+    sdf = launch.sdf_len(8, repartition=8)
+    rows = launch.collect(launch.spark_apply(sdf, _spark_closure_derived_world, barrier=True,
+                                             columns={"address": "character"}, timeout=500))
+    assert len(rows) == 8
+    vals = [r["address"] for r in rows]
+    parts = [v.split("/") for v in vals]
+    assert [int(p[0]) for p in parts] == list(range(8)), vals
+    assert all(p[1] == "8" for p in parts), vals
+    assert len({p[2] for p in parts}) == 1, vals
 
 
 @pytest.mark.timeout(300)

@@ -333,18 +333,19 @@ def test_bn_statistics_accumulators_are_order_independent(H):
     s = torch.cuda.current_stream().cuda_stream
     outs = []
     for reps, rev in ((8, False), (8, True), (1, False)):
-        acc = torch.zeros(reps, 4 * C, dtype=torch.int64, device=dev)
+        acc = H.acc_zeros(reps, 4 * C, dev)
         C_.bn_reduce_reverse(rev)
         try:
             C_.bn_bwd_reduce_acc(dy.data_ptr(), 0, 0, x.data_ptr(), st.data_ptr(), 0, acc.data_ptr(), T, M, C, s, reps)
             torch.cuda.synchronize()
         finally:
             C_.bn_reduce_reverse(False)
-        words = acc.cpu().sum(0)
+        assert not acc[-1].any(), "finite partials set the non-finite flag"
+        words = acc.cpu()[:-1].sum(0)
         outs.append(words)
     assert torch.equal(outs[0], outs[1]), "reversed block order changed the backward sums"
     assert torch.equal(outs[0], outs[2]), "the replica count changed the backward sums"
-    got = H.bn_acc_decode(outs[0].unsqueeze(0), words=2)
+    got = H.bn_acc_decode(torch.stack([outs[0], torch.zeros_like(outs[0])]), words=2)
     d, xh = dy.double(), (x.double() - st[0].double()) * st[1].double()
     want = torch.cat([d.sum(0), (d * xh).sum(0)]).cpu()
     assert torch.allclose(got, want, rtol=1e-5, atol=1e-12), (got - want).abs().max()
@@ -355,13 +356,63 @@ def test_bn_statistics_accumulators_are_order_independent(H):
     wb = rb(rnd(3, 3, cin, cout, scale=0.05, seed=44)).bfloat16()
     sums = []
     for reps in (1, 8):
-        acc = torch.zeros(reps, 2 * cout, dtype=torch.int64, device=dev)
+        acc = H.acc_zeros(reps, 2 * cout, dev)
         out = torch.empty(n, h, h, cout, device=dev, dtype=torch.bfloat16)
-        H.conv_fwd(xb, wb, out, (1, 1), "same", stats=acc if reps > 1 else acc[0])
+        # (reps 1: the 1-D form, one replica then its flag plane)
+        H.conv_fwd(xb, wb, out, (1, 1), "same", stats=acc if reps > 1 else acc.view(-1))
         torch.cuda.synchronize()
-        sums.append(acc.cpu().sum(0))
+        sums.append(acc.cpu()[:-1].sum(0))
     assert torch.equal(sums[0], sums[1]), "the replica count changed the forward statistics"
     o = out.double().reshape(-1, cout)
     want = torch.cat([o.sum(0), (o * o).sum(0)]).cpu()
-    got = H.bn_acc_decode(sums[0].unsqueeze(0), words=1)
+    got = H.bn_acc_decode(torch.stack([sums[0], torch.zeros_like(sums[0])]), words=1)
     assert torch.allclose(got, want, rtol=1e-5, atol=1e-3), (got - want).abs().max()
+
+
+def test_bn_accumulators_large_sums_and_sticky_nonfinite_flag(H):
+    """(a) a FINITE sum above 2^33 (sum of squares of a conv output with mean
+    square ~5e5 over 65,536 positions ~ 3e10) decodes finite and right -- round 5's in-word
+    poison read every |word| >= 2^57 (sums >= 2^33) as NaN; (b) non-finite partials set a
+    sticky per-channel flag: channel 3 NaN in EVERY block (a block count that is a multiple
+    of 64 wrapped the additive poison to 0) and channel 5 with +inf in one block and -inf
+    in another (they cancelled) both decode NaN; the other channels stay exact."""
+    from distributed_amd.native import require_C
+
+    C_ = require_C()
+    n, h, cin, cout = 64, 32, 64, 64
+    xb = rb(rnd(n, h, h, cin, seed=51) * 60).bfloat16()
+    wb = rb(rnd(3, 3, cin, cout, scale=0.5, seed=52)).bfloat16()
+    acc = H.acc_zeros(8, 2 * cout, dev)
+    out = torch.empty(n, h, h, cout, device=dev, dtype=torch.bfloat16)
+    H.conv_fwd(xb, wb, out, (1, 1), "same", stats=acc)
+    torch.cuda.synchronize()
+    o = out.double().reshape(-1, cout)
+    want = torch.cat([o.sum(0), (o * o).sum(0)]).cpu()
+    assert want[cout:].min() > 2.0 ** 33, want[cout:].min()
+    got = H.bn_acc_decode(acc, words=1)
+    assert torch.isfinite(got).all()
+    assert torch.allclose(got, want, rtol=1e-5, atol=1e-3), (got - want).abs().max()
+
+    M, C = 64 * 1024, 64
+    T = C_.bn_bwd_blocks(M, C)
+    dy = rb(rnd(M, C, scale=1e-3, seed=53))
+    dy[:, 3] = float("nan")
+    dy[7, 5] = float("inf")
+    dy[M - 9, 5] = float("-inf")
+    dy = dy.bfloat16()
+    x = rb(rnd(M, C, seed=54)).bfloat16()
+    st = torch.stack([x.float().mean(0), torch.rsqrt(x.float().var(0) + 1e-3),
+                      torch.ones(C, device=dev), torch.zeros(C, device=dev)]).contiguous()
+    acc = H.acc_zeros(8, 4 * C, dev)
+    s = torch.cuda.current_stream().cuda_stream
+    C_.bn_bwd_reduce_acc(dy.data_ptr(), 0, 0, x.data_ptr(), st.data_ptr(), 0, acc.data_ptr(), T, M, C, s, 8)
+    torch.cuda.synchronize()
+    got = H.bn_acc_decode(acc, words=2)
+    bad = torch.zeros(2 * C, dtype=torch.bool)
+    for c in (3, 5):
+        bad[c] = bad[C + c] = True
+    assert torch.isnan(got[bad]).all(), got[bad]
+    assert torch.isfinite(got[~bad]).all()
+    d, xh = dy.double(), (x.double() - st[0].double()) * st[1].double()
+    want = torch.cat([d.sum(0), (d * xh).sum(0)]).cpu()
+    assert torch.allclose(got[~bad], want[~bad], rtol=1e-5, atol=1e-12)

@@ -256,3 +256,36 @@ def test_strategy_reduce_single_replica():
     assert s.reduce("sum", v).tolist() == v
     assert s.reduce(tf.distribute.ReduceOp.MEAN, v, axis=0).tolist() == [2.0, 3.5]
     assert s.reduce("min", v, axis=1).tolist() == [1.0, 3.0]
+
+
+def test_baseline_config1_two_conv_cnn_through_r_verbs():
+    """BASELINE.json config 1: "MNIST 2-conv CNN single-worker on CPU via R
+    keras_model_sequential" -- the R pipe chain (README.md:58-75) through r_api's verbs,
+    one worker, CPU, with the second Conv2D(64, 3, relu) of models.mnist_cnn(two_conv=True).
+    After 3 epochs x 5 steps at lr 1e-3 (README.md:75) the loss is still ~ln 10 (random-init
+    logits are ~uniform; 15 SGD steps at 1e-3 barely move it)."""
+    from distributed_amd import r_api as k
+
+    tf.set_seed(3)
+    mnist = k.dataset_mnist()
+    x_train = k.array_reshape(mnist["train"]["x"][:2048], k.c(2048, 28, 28, 1)) / 255
+    y_train = mnist["train"]["y"][:2048]
+    model = k.pipe(k.keras_model_sequential(),
+                   lambda m: k.layer_conv_2d(m, filters=32, kernel_size=3, activation="relu",
+                                             input_shape=k.c(28, 28, 1)),
+                   lambda m: k.layer_max_pooling_2d(m),
+                   lambda m: k.layer_conv_2d(m, filters=64, kernel_size=3, activation="relu"),
+                   lambda m: k.layer_flatten(m),
+                   lambda m: k.layer_dense(m, units=64, activation="relu"),
+                   lambda m: k.layer_dense(m, units=10))
+    k.compile(model, loss=tf.keras.losses.SparseCategoricalCrossentropy(from_logits=True),
+              optimizer=tf.keras.optimizers.SGD(learning_rate=0.001), metrics="accuracy")
+    assert [l.name for l in model.layers] == ["conv2d", "max_pooling2d", "conv2d_1", "flatten", "dense", "dense_1"]
+    ref = tf.models.mnist_cnn(two_conv=True)
+    assert model.count_params() == ref.count_params() == 515146
+    result = k.fit(model, x_train, y_train, batch_size=64, epochs=3, steps_per_epoch=5, verbose=0)
+    assert model._engine.name == "generic"  # CPU: the PyTorch reference engine
+    assert len(result.metrics["loss"]) == 3 and len(result.metrics["accuracy"]) == 3
+    assert abs(result.metrics["loss"][-1] - math.log(10)) < 0.05, result.metrics["loss"]
+    assert all(0.0 <= a <= 1.0 for a in result.metrics["accuracy"])
+    assert int(model.optimizer.iterations) == 15
