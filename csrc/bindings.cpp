@@ -8,6 +8,7 @@
 
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "comm.h"
@@ -236,6 +237,40 @@ const char* damd_src_hash();  // build/obj/src_hash.cpp, generated by distribute
 PYBIND11_MODULE(_C, m) {
   m.doc() = "distributed_amd native runtime (HIP/gfx950 kernels, RCCL, hipGraph executor)";
   m.def("src_hash", []() { return std::string(damd_src_hash()); });
+  // structure of a captured (not yet destroyed) hipGraph: one (node type, kernel name or
+  // "", [indices of the nodes it depends on]) per node -- what the tests use to check that
+  // each gradient bucket's collective depends only on the backward work that wrote it
+  m.def("graph_nodes", [](uintptr_t gp) {
+    hipGraph_t g = reinterpret_cast<hipGraph_t>(gp);
+    size_t n = 0;
+    HIP_CHECK(hipGraphGetNodes(g, nullptr, &n));
+    std::vector<hipGraphNode_t> nodes(n);
+    if (n) HIP_CHECK(hipGraphGetNodes(g, nodes.data(), &n));
+    std::unordered_map<hipGraphNode_t, int> idx;
+    for (size_t i = 0; i < n; ++i) idx[nodes[i]] = (int)i;
+    py::list out;
+    for (size_t i = 0; i < n; ++i) {
+      hipGraphNodeType t;
+      HIP_CHECK(hipGraphNodeGetType(nodes[i], &t));
+      std::string name;
+      if (t == hipGraphNodeTypeKernel) {
+        hipKernelNodeParams kp{};
+        if (hipGraphKernelNodeGetParams(nodes[i], &kp) == hipSuccess && kp.func) {
+          const char* nm = hipKernelNameRefByPtr(kp.func, nullptr);
+          if (nm) name = nm;
+        }
+        (void)hipGetLastError();
+      }
+      size_t nd = 0;
+      HIP_CHECK(hipGraphNodeGetDependencies(nodes[i], nullptr, &nd));
+      std::vector<hipGraphNode_t> deps(nd);
+      if (nd) HIP_CHECK(hipGraphNodeGetDependencies(nodes[i], deps.data(), &nd));
+      std::vector<int> di;
+      for (auto d : deps) di.push_back(idx.count(d) ? idx[d] : -1);
+      out.append(py::make_tuple((int)t, name, di));
+    }
+    return out;
+  });
   m.attr("CONVNET_NPARAM") = kConvNetNParam;
   m.attr("CONVNET_NGRAD") = kConvNetNGrad;
   m.attr("CONVNET_NCONV") = kConvNetNConv;

@@ -68,6 +68,9 @@ hipError_t wgrad3_stamps_read(unsigned long long* host, int blocks);  // [blocks
 // block for an H x W image (0: not supported); stats partials = Nimg * ceil(H / rows)
 hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream_t s);
 int conv3_rows(int H, int W, int bn);
+// conv3r.hip: the persistent weight-stationary variant for 64 -> 64 channels (layer 1)
+int conv3r_ok(const GemmArgs& a, int dgrad);
+hipError_t conv3r_launch(const GemmArgs& a, int dgrad, int epi, hipStream_t s);
 hipError_t conv3_stamps_enable(int on);                              // diagnostics
 hipError_t conv3_stamps_read(unsigned long long* host, int blocks);  // [blocks][4]
 int wgrad64_rows_per_step(int Wo, int kstep);

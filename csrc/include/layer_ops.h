@@ -151,7 +151,7 @@ struct OptArgs {
   int flag;
 };
 hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, uint16_t* Pb, long n, Ctrl* ctrl,
-                    const float* tail, const OptArgs& o, hipStream_t s);
+                    const float* tail, const OptArgs& o, hipStream_t s, int book = 1);
 
 // Data / layout glue -------------------------------------------------------------------------
 // the step's rows of the (epoch-permuted) dataset: row = (cursor*global_batch + row0 + i)

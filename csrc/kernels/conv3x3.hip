@@ -472,6 +472,9 @@ hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream
     return hipErrorInvalidValue;
   if (dgrad && (a.kc != a.Cin || a.bnin.acc)) return hipErrorInvalidValue;
   if (epi & (E_SLAB | E_ATOMIC)) return hipErrorInvalidValue;
+  // 64 -> 64 channels: the persistent weight-stationary strip kernel (conv3r.hip), the same
+  // tiles / numerics
+  if (bn == 64 && conv3r_ok(a, dgrad)) return conv3r_launch(a, dgrad, epi, s);
   // (a weight-stationary persistent variant for 64 -> 64 channels -- 72 KiB of weights +
   // two halos = the CU's 160 KiB -- measured slower on ResNet layer 1, forward 42 vs 33 us,
   // backprop-input 37 vs 29 us: one 4-wave block per CU cannot hide the LDS / MFMA

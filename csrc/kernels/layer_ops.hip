@@ -1578,7 +1578,7 @@ __global__ __launch_bounds__(NT) void unpad_add_k(const float* src, int R, int C
 __global__ __launch_bounds__(NT) void opt_step_k(float* __restrict__ P, const float* __restrict__ G,
                                                  float* __restrict__ S0, float* __restrict__ S1,
                                                  float* __restrict__ S2, uint16_t* __restrict__ Pb, long n,
-                                                 Ctrl* ctrl, const float* tail, OptArgs o) {
+                                                 Ctrl* ctrl, const float* tail, OptArgs o, int book) {
   const float lr = ctrl->lr;
   const int t = ctrl->cur3;
   float lr_t = lr;
@@ -1623,7 +1623,10 @@ __global__ __launch_bounds__(NT) void opt_step_k(float* __restrict__ P, const fl
     P[i] = w;
     Pb[i] = f2bf(w);
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  // the step's bookkeeping, once per step: by the launch covering the metric tail's bucket
+  // when the update is split per gradient bucket (native_graph bucket_opt), else by the
+  // single launch.  (The per-bucket launches only READ ctrl's lr / cur3.)
+  if (book && blockIdx.x == 0 && threadIdx.x == 0) {
     ctrl->acc_loss += tail[0];
     ctrl->acc_correct += tail[1];
     ctrl->acc_count += tail[2];
@@ -1635,9 +1638,10 @@ __global__ __launch_bounds__(NT) void opt_step_k(float* __restrict__ P, const fl
 }
 
 hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, uint16_t* Pb, long n, Ctrl* ctrl,
-                    const float* tail, const OptArgs& o, hipStream_t s) {
-  if (o.kind < 0 || o.kind > 2) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(opt_step_k, dim3(grid_for(n, NT, 4096)), dim3(NT), 0, s, P, G, S0, S1, S2, Pb, n, ctrl, tail, o);
+                    const float* tail, const OptArgs& o, hipStream_t s, int book) {
+  if (o.kind < 0 || o.kind > 2 || n < 0) return hipErrorInvalidValue;
+  const int grid = n > 0 ? grid_for(n, NT, 4096) : 1;
+  hipLaunchKernelGGL(opt_step_k, dim3(grid), dim3(NT), 0, s, P, G, S0, S1, S2, Pb, n, ctrl, tail, o, book);
   return hipGetLastError();
 }
 

@@ -313,12 +313,14 @@ void register_kernel_ops(py::module_& m) {
           "sgd_step");
   });
   m.def("opt_step", [](U P, U G, U S0, U S1, U S2, U Pb, long n, U ctrl, U tail, int kind, float b1, float b2,
-                       float eps, float rho, float mom, int flag, U s) {
+                       float eps, float rho, float mom, int flag, U s, int book) {
     damd::OptArgs o{kind, b1, b2, eps, rho, mom, flag};
     check(damd::opt_step(P_<float>(P), P_<const float>(G), P_<float>(S0), P_<float>(S1), P_<float>(S2), P_<u16>(Pb), n,
-                         P_<damd::Ctrl>(ctrl), P_<const float>(tail), o, P_<ihipStream_t>(s)),
+                         P_<damd::Ctrl>(ctrl), P_<const float>(tail), o, P_<ihipStream_t>(s), book),
           "opt_step");
-  });
+  }, py::arg("P"), py::arg("G"), py::arg("S0"), py::arg("S1"), py::arg("S2"), py::arg("Pb"), py::arg("n"),
+     py::arg("ctrl"), py::arg("tail"), py::arg("kind"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("rho"),
+     py::arg("mom"), py::arg("flag"), py::arg("s"), py::arg("book") = 1);
   m.def("gather_batch", [](U x, int x_u8, float scale, U labels, U ctrl, int per, int HW, int Cin, int Cp, U xb, U yb,
                            U s, U zero, long zero_bytes, U zero2, long zero2_bytes) {
     check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<damd::Ctrl>(ctrl),

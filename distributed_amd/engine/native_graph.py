@@ -301,6 +301,22 @@ class NativeGraphEngine(Engine):
         if self.peer is not None and self.grad_bf16:
             dlog.warning("DAMD_GRAD_DTYPE=bf16 applies to the RCCL buckets; the peer transport reduces fp32")
             self.grad_bf16 = False
+        # RCCL buckets: one communicator PER BUCKET (a unique id each, exchanged over the gloo
+        # control plane), each on its own stream.  Collectives on ONE communicator must run
+        # in issue order, so a shared communicator forces the captured graph into a chain --
+        # each all-reduce node waiting on the previous one AND on its backward -- which the
+        # graph executor serialised with the backward (profiles/r05_graph_branches: no
+        # overlap for the last buckets).  With a communicator per bucket every all-reduce
+        # node depends only on the backward work that wrote its bucket.  DAMD_BUCKET_COMMS=0:
+        # the single shared communicator and one comm stream (the round-5 chain).
+        self.bucket_comms = []
+        if (self.native_comm is not None and self.peer is None and len(self._buckets) > 1
+                and env.get_bool("DAMD_BUCKET_COMMS", True)):
+            comm = strategy.communicator
+            uids = [C.rccl_unique_id() for _ in self._buckets] if self.rank == 0 else None
+            if self.world > 1:
+                uids = comm.broadcast_object(uids, 0)
+            self.bucket_comms = [C.RcclComm(self.world, self.rank, u, dev.index or 0) for u in uids]
         self.host_collective = self.world > 1 and self.native_comm is None and self.peer is None
         self.allreduce_kind = ("none" if self.native_comm is None and self.peer is None else
                                "xgmi-peer-bucketed" if self.peer is not None else
@@ -310,11 +326,23 @@ class NativeGraphEngine(Engine):
         self.use_graph = env.get_bool("DAMD_GRAPH", True) and not self.host_collective
         self.g16 = (torch.zeros(self.nparam, dtype=torch.bfloat16, device=dev)
                     if self.grad_bf16 and self.native_comm is not None else None)
-        # created up front: no stream creation while a graph is being captured.  RCCL: one
-        # comm stream (collectives on one communicator stay in order); peer: one per bucket
+        # created up front: no stream creation while a graph is being captured.  One stream
+        # per bucket (peer staging or RCCL communicator per bucket); a single comm stream
+        # when all buckets share one RCCL communicator (its collectives stay in order)
+        per_bucket = self.peer is not None or bool(self.bucket_comms)
         self._comm_stream = (torch.cuda.Stream(dev) if (self.native_comm is not None or self.peer is not None)
                              else None)
-        self._comm_streams = ([torch.cuda.Stream(dev) for _ in self._buckets] if self.peer is not None else [])
+        self._comm_streams = [torch.cuda.Stream(dev) for _ in self._buckets] if per_bucket else []
+        # the SGD / Adam / RMSprop update of a bucket's variables runs right behind the
+        # bucket's all-reduce on its own stream (it overlaps the rest of backward, and only
+        # the update of the LAST bucket trails the step).  World 1: the buckets' updates run
+        # on side streams as soon as backward has written them (DAMD_BUCKET_OPT=0: one
+        # optimizer launch after the join).  The bucket holding the metric tail also does
+        # the step's bookkeeping (metric fold, cursor, iterations).
+        self.bucket_opt = (env.get_bool("DAMD_BUCKET_OPT", True) and not self.host_collective
+                           and len(self._buckets) > 1)
+        if self.bucket_opt and not self._comm_streams:
+            self._comm_streams = [torch.cuda.Stream(dev) for _ in self._buckets]
         for k, b in enumerate(self._buckets):
             b["k"] = k
         opt._iter_source = self._iterations
@@ -732,21 +760,26 @@ class NativeGraphEngine(Engine):
         """SUM all-reduce of G[lo:hi] on stream ``st`` by the configured transport."""
         lo, hi = b["lo"], b["hi"]
         gp = self.G.data_ptr()
+        comm = self.bucket_comms[b["k"]] if self.bucket_comms else self.native_comm
         if self.peer is not None:
             self.peers[b["k"]].allreduce(gp + 4 * lo, hi - lo, st)
         elif self.g16 is not None:
             n = min(hi, self.nparam) - lo  # the parameter part travels as bf16 ...
             g16 = self.g16.data_ptr() + 2 * lo
             self.C.cast_f32_bf16(gp + 4 * lo, g16, n, st)
-            self.native_comm.allreduce(g16, g16, n, 1, 0, st)
+            comm.allreduce(g16, g16, n, 1, 0, st)
             self.C.cast_bf16_f32(g16, gp + 4 * lo, n, st)
             if hi > self.nparam:  # ... the metric tail (counts, sums) as fp32
-                self.native_comm.allreduce(gp + 4 * self.nparam, gp + 4 * self.nparam, hi - self.nparam, 0, 0, st)
+                comm.allreduce(gp + 4 * self.nparam, gp + 4 * self.nparam, hi - self.nparam, 0, 0, st)
         else:
-            self.native_comm.allreduce(gp + 4 * lo, gp + 4 * lo, hi - lo, 0, 0, st)
+            comm.allreduce(gp + 4 * lo, gp + 4 * lo, hi - lo, 0, 0, st)
+
+    def _bucket_stream(self, b):
+        return self._comm_streams[b["k"]] if self._comm_streams else self._comm_stream
 
     def _bucket_progress(self, nd, final=False):
-        if self.native_comm is None and self.peer is None:
+        reduce = self.native_comm is not None or self.peer is not None
+        if not reduce and not self.bucket_opt:
             return
         done = set(self._writes.get(id(nd), ())) if nd is not None else set()
         main = torch.cuda.current_stream(self.device)
@@ -756,13 +789,33 @@ class NativeGraphEngine(Engine):
             b["left"] -= done
             if b["left"] and not final:
                 continue
-            cs = self._comm_streams[b["k"]] if self.peer is not None else self._comm_stream
+            cs = self._bucket_stream(b)
             cs.wait_stream(main)
-            self._reduce_bucket(b, cs.cuda_stream)
+            if reduce:
+                self._reduce_bucket(b, cs.cuda_stream)
+            if self.bucket_opt:
+                with torch.cuda.stream(cs):
+                    self._optimizer_step(b)
             b["sent"] = True
         if final:
-            for cs in (self._comm_streams if self.peer is not None else [self._comm_stream]):
+            for cs in (self._comm_streams or [self._comm_stream]):
                 main.wait_stream(cs)
+
+    def graph_nodes(self):
+        """Structure of one captured step (tests): [(node type, kernel name, [dependency
+        indices])] of a fresh capture whose hipGraph is kept (C.graph_nodes)."""
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        gc.collect()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                self._step_body()
+        torch.cuda.synchronize(self.device)
+        nodes = self.C.graph_nodes(g.raw_cuda_graph())
+        del g
+        return nodes
 
     def _all_tensors(self):
         out = [self.x0]
@@ -904,11 +957,13 @@ class NativeGraphEngine(Engine):
         self._mark("backward")
         self._bucket_progress(None, final=True)
         self._mark("allreduce")  # the part of the all-reduce not hidden behind backward
-        if not self.host_collective:
+        if not self.host_collective and not self.bucket_opt:
             self._optimizer_step()
         self._mark("optimizer")
 
-    def _optimizer_step(self):
+    def _optimizer_step(self, b=None):
+        """The optimizer update of every parameter (b None), or of bucket b's range only --
+        the bucket whose range holds the metric tail also does the step's bookkeeping."""
         opt = self.model.optimizer
         ptr = [self.S[nm].data_ptr() if nm else self._slot_dummy.data_ptr() for nm in self.slot_kernel_names]
         if self.opt_kind == 1:
@@ -917,8 +972,15 @@ class NativeGraphEngine(Engine):
             args = (0.0, 0.0, float(opt.epsilon), float(opt.rho), float(opt.momentum), int(opt.centered))
         else:
             args = (0.0, 0.0, 0.0, 0.0, float(opt.momentum), int(opt.nesterov))
-        self.C.opt_step(self.P.data_ptr(), self.G.data_ptr(), ptr[0], ptr[1], ptr[2], self.Pb.data_ptr(), self.nparam,
-                        self.ctrl.data_ptr(), self.G[self.nparam:].data_ptr(), self.opt_kind, *args, H.stream_handle())
+        lo, hi, book = 0, self.nparam, 1
+        if b is not None:
+            lo, hi = b["lo"], min(b["hi"], self.nparam)
+            book = int(b["hi"] > self.nparam)
+        # (a slot pointer of an unused slot is the dummy: offset, never dereferenced)
+        o4 = 4 * lo
+        self.C.opt_step(self.P.data_ptr() + o4, self.G.data_ptr() + o4, ptr[0] + o4, ptr[1] + o4, ptr[2] + o4,
+                        self.Pb.data_ptr() + 2 * lo, max(hi - lo, 0), self.ctrl.data_ptr(),
+                        self.G[self.nparam:].data_ptr(), self.opt_kind, *args, H.stream_handle(), book=book)
 
     # forward ops
     def _w(self, nd, var):

@@ -76,6 +76,10 @@ for s in ${STAGES:-xtests bench}; do
       DAMD_COMM=gloo DAMD_ALLREDUCE=sharded step sh_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20
       DAMD_COMM=gloo DAMD_ALLREDUCE=sharded DAMD_XCHG_SELFTEST=0 step sh_noself 300 python bench.py --gpus 2 --steps 200 --warmup 20
       DAMD_COMM=gloo DAMD_ALLREDUCE=xgmi step xg_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20 ;;
+    c3r)  # the persistent 64 -> 64 direct conv (conv3r.hip) and every direct-conv test
+      step c3r 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_conv_gemm_gpu.py -k "conv3" ;;
+    ngraph)  # bucket graph structure + native-graph tests
+      step ngraph 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_native_graph_gpu.py ;;
     resnet)
       step resnet 300 python bench.py --model resnet18 --steps 20 --warmup 5
       step resnet_long 300 python bench.py --model resnet18 --steps 100 --warmup 10 ;;

@@ -507,3 +507,65 @@ def test_direct_conv3_bn_input(H, monkeypatch, n, h, cin, cout, reps):
     var = (x64 * x64).mean(0) - mean * mean
     ref_y = torch.relu((xb.float().reshape(-1, cin) - mean.float()) * torch.rsqrt(var.float() + 1e-3) * gamma + beta)
     close(y, ref_y, 1e-2, 4e-3)
+
+
+@pytest.mark.parametrize("n", [2, 20, 64])
+def test_direct_conv3r_bitwise_equals_general_kernel(H, monkeypatch, n):
+    """The persistent weight-stationary 64 -> 64 kernel (csrc/kernels/conv3r.hip: one strip
+    of 4-row tiles per CU, a ring of halo rows, a loader wave) == the general direct kernel
+    (conv3x3.hip, DAMD_CONV3R=0), BITWISE -- same tiles, fragment layouts and MFMA order:
+    forward with bias + ReLU, with fixed-point BN statistics, on a BatchNorm input (y, the
+    conv output, the statistics, the published st / moving statistics); backprop-input
+    plain, accumulating, and with the BN-backward epilogue.  n = 2: one tile per strip;
+    20: strips of one or two tiles; 64: the ResNet-18 batch, strips of 3-4 tiles (the ring
+    reuses slots)."""
+    h, c = 56, 64
+    shape = (n, h, h, c)
+    xb = rb(rnd(*shape, scale=2.0, seed=61) + 0.3).bfloat16()
+    wb = rb(rnd(3, 3, c, c, scale=0.05, seed=62)).bfloat16()
+    dyb = rb(rnd(*shape, seed=63)).bfloat16()
+    bias = rnd(c, scale=0.1, seed=64)
+    gamma, beta = rnd(c, seed=65).abs() + 0.5, rnd(c, seed=66) * 0.2
+    x64 = xb.double().reshape(-1, c)
+    sums = torch.cat([x64.sum(0), (x64 * x64).sum(0)])
+    accin = torch.stack([H.bn_acc_encode(sums * 0.5), H.bn_acc_encode(sums * 0.5),
+                         torch.zeros(2 * c, dtype=torch.int64)]).to(dev)
+    st_bw = torch.stack([rnd(c, seed=67) * 0.1, rnd(c, seed=68).abs() + 0.5,
+                         rnd(c, seed=69).abs() + 0.5, rnd(c, seed=70)]).float().contiguous()
+    base = rb(rnd(*shape, seed=71)).bfloat16()
+
+    def run():
+        out = {}
+        o = torch.empty(shape, device=dev, dtype=torch.bfloat16)
+        H.conv_fwd(xb, wb, o, (1, 1), "same", bias=bias, relu=True)
+        out["fwd_bias_relu"] = o
+        o2, acc = torch.empty_like(o), H.acc_zeros(8, 2 * c, dev)
+        H.conv_fwd(xb, wb, o2, (1, 1), "same", stats=acc)
+        out["fwd_stats"], out["fwd_stats_acc"] = o2, acc
+        st, rm, rv = torch.zeros(4, c, device=dev), torch.zeros(c, device=dev), torch.ones(c, device=dev)
+        fin = H.BNFin(accin, gamma, beta, st, rm, rv, n * h * h, 1e-3, 0.99)
+        y = torch.full(shape, float("nan"), device=dev, dtype=torch.bfloat16)
+        o3, acc3 = torch.empty_like(o), H.acc_zeros(8, 2 * c, dev)
+        H.conv_fwd(xb, wb, o3, (1, 1), "same", stats=acc3, bnin=(fin, y))
+        out.update(bnin_y=y, bnin_out=o3, bnin_acc=acc3, bnin_st=st, bnin_rm=rm, bnin_rv=rv)
+        dx = torch.empty_like(o)
+        H.conv_dgrad(dyb, wb, dx, (1, 1), "same")
+        out["dgrad"] = dx
+        dx2 = base.clone()
+        H.conv_dgrad(dyb, wb, dx2, (1, 1), "same", accumulate=True)
+        out["dgrad_acc"] = dx2
+        dx3, part = torch.empty_like(o), H.acc_zeros(8, 4 * c, dev)
+        assert H.conv_dgrad(dyb, wb, dx3, (1, 1), "same", bnred=(xb, st_bw, part))
+        out["dgrad_bnred"], out["dgrad_bnred_acc"] = dx3, part
+        torch.cuda.synchronize()
+        return out
+
+    monkeypatch.setenv("DAMD_CONV3R", "1")
+    new = run()
+    monkeypatch.setenv("DAMD_CONV3R", "0")
+    old = run()
+    for k in new:
+        assert torch.equal(new[k], old[k]), k
+    # and against the fp32 reference (guards a shared bug)
+    y = ref.conv2d(xb.float(), wb.float(), None, (1, 1), "same")
+    close(new["fwd_stats"], y, 1e-2, 4e-3)
