@@ -313,10 +313,10 @@ class NativeGraphEngine(Engine):
         if (self.native_comm is not None and self.peer is None and len(self._buckets) > 1
                 and env.get_bool("DAMD_BUCKET_COMMS", True)):
             comm = strategy.communicator
-            uids = [C.rccl_unique_id() for _ in self._buckets] if self.rank == 0 else None
+            uids = [self.C.rccl_unique_id() for _ in self._buckets] if self.rank == 0 else None
             if self.world > 1:
                 uids = comm.broadcast_object(uids, 0)
-            self.bucket_comms = [C.RcclComm(self.world, self.rank, u, dev.index or 0) for u in uids]
+            self.bucket_comms = [self.C.RcclComm(self.world, self.rank, u, dev.index or 0) for u in uids]
         self.host_collective = self.world > 1 and self.native_comm is None and self.peer is None
         self.allreduce_kind = ("none" if self.native_comm is None and self.peer is None else
                                "xgmi-peer-bucketed" if self.peer is not None else
@@ -335,11 +335,14 @@ class NativeGraphEngine(Engine):
         self._comm_streams = [torch.cuda.Stream(dev) for _ in self._buckets] if per_bucket else []
         # the SGD / Adam / RMSprop update of a bucket's variables runs right behind the
         # bucket's all-reduce on its own stream (it overlaps the rest of backward, and only
-        # the update of the LAST bucket trails the step).  World 1: the buckets' updates run
-        # on side streams as soon as backward has written them (DAMD_BUCKET_OPT=0: one
-        # optimizer launch after the join).  The bucket holding the metric tail also does
-        # the step's bookkeeping (metric fold, cursor, iterations).
-        self.bucket_opt = (env.get_bool("DAMD_BUCKET_OPT", True) and not self.host_collective
+        # the update of the LAST bucket trails the step; DAMD_BUCKET_OPT=0: one optimizer
+        # launch after the join).  The bucket holding the metric tail also does the step's
+        # bookkeeping (metric fold, cursor, iterations).
+        # (world 1, no all-reduce: off by default -- the 4096-block update launches on side
+        # streams took CUs from the backward kernels, measured +170 us per ResNet-18 step;
+        # the persistent direct convs need every CU)
+        reduce = self.native_comm is not None or self.peer is not None
+        self.bucket_opt = (env.get_bool("DAMD_BUCKET_OPT", reduce) and not self.host_collective
                            and len(self._buckets) > 1)
         if self.bucket_opt and not self._comm_streams:
             self._comm_streams = [torch.cuda.Stream(dev) for _ in self._buckets]

@@ -488,7 +488,9 @@ def _check_stats(stats, plan, cout, who):
     if stats is None:
         return
     if stats.dtype == torch.int64:
-        if stats.numel() != 2 * cout * (acc_reps(stats) + 1) or stats.shape[-1] != 2 * cout:
+        ok = (stats.numel() == 4 * cout if stats.dim() == 1 else
+              (stats.dim() == 2 and stats.shape[0] >= 2 and stats.shape[-1] == 2 * cout))
+        if not ok:
             raise ValueError(f"{who}: a statistics accumulator is int64 [reps + 1][2 x {cout}], "
                              f"got {tuple(stats.shape)}")
     elif stats.shape[0] != plan["stats_T"]:

@@ -36,6 +36,9 @@ def phases(fn, nblk):
     st = np.array(C.conv3_stamps_read(min(nblk, 4096)), dtype=np.float64).reshape(-1, 4)
     C.conv3_stamps_enable(0)
     st = st[st[:, 0] > 0]
+    if len(st) == 0:  # a kernel without stamps (conv3r.hip)
+        print("    (no phase stamps: persistent conv3r kernel)")
+        return
     t0 = st[:, 0].min()
     rel = (st - t0) / 100.0  # 100 MHz -> us
     land, taps, epi = rel[:, 1] - rel[:, 0], rel[:, 2] - rel[:, 1], rel[:, 3] - rel[:, 2]  # (persistent: first
