@@ -276,12 +276,7 @@ __device__ __forceinline__ float row16_max(float v) {
   v = fmaxf(v, dppf<DPP_HMIRROR>(v));
   return fmaxf(v, dppf<DPP_MIRROR>(v));
 }
-__device__ __forceinline__ float row16_sum(float v) {
-  v += dppf<DPP_QSWAP1>(v);
-  v += dppf<DPP_QSWAP2>(v);
-  v += dppf<DPP_HMIRROR>(v);
-  return v + dppf<DPP_MIRROR>(v);
-}
+// (row16_sum: damd_common.h, the same DPP sequence, shared with the GEMM epilogues)
 __device__ __forceinline__ int row16_min(int v) {
   v = min(v, dppi<DPP_QSWAP1>(v));
   v = min(v, dppi<DPP_QSWAP2>(v));

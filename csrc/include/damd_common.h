@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace damd {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -89,6 +91,20 @@ __device__ __forceinline__ double bnacc_value1(long long w, long long flag = 0) 
 __device__ __forceinline__ double bnacc_value2(long long hi, long long lo, long long flag = 0) {
   if (flag) return __builtin_nan("");
   return (double)hi * 5.9604644775390625e-08 + (double)lo * 5.42101086242752217e-20;  // 2^-24, 2^-64
+}
+
+// Sum over the 16 lanes of a DPP row (lanes 16 r .. 16 r + 15), on DPP moves: quad swaps,
+// then the half-row and row mirrors; every lane of the row ends with the same bits (each
+// step adds two equal partial sums, in either order).  VALU only: the __shfl_xor butterfly
+// it replaces in the GEMM epilogues' statistics was four ds_bpermute LDS round trips.
+__device__ __forceinline__ float row16_sum(float v) {
+  auto dpp = [](float x, auto ctrl) __attribute__((always_inline)) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xf, 0xf, false));
+  };
+  v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm [1, 0, 3, 2]
+  v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm [2, 3, 0, 1]
+  v += dpp(v, std::integral_constant<int, 0x141>{});  // row_half_mirror
+  return v + dpp(v, std::integral_constant<int, 0x140>{});  // row_mirror
 }
 
 #define DAMD_PUBLISH_WG() asm volatile(";damd.publish wg")

@@ -171,17 +171,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
     }
   }
   if constexpr ((EPI & (E_STATS | E_BNRED)) != 0) {
-    // reduce over the 16 rows held by lanes l&15 (xor 1,2,4,8), then over the wave grid's
+    // reduce over the 16 rows held by lanes l&15 (DPP row sum), then over the wave grid's
     // M direction through LDS; one partial per column per M-tile: stats[tm][z][2][N]
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-#pragma unroll
-        for (int s = 1; s < 16; s <<= 1) {
-          csum[j][e] += __shfl_xor(csum[j][e], s);
-          csq[j][e] += __shfl_xor(csq[j][e], s);
-        }
+        csum[j][e] = row16_sum(csum[j][e]);
+        csq[j][e] = row16_sum(csq[j][e]);
       }
     if ((lane & 15) == 0) {
 #pragma unroll

@@ -13,9 +13,12 @@
 // a whole one) and one 64-channel N-tile, the whole strip's accumulators in registers (each
 // compute wave up to G = 4 groups of 16 pixels x 64 channels):
 //   * the strip's (R + 2) x (W + 2) input halo of one 64-channel chunk is resident in LDS,
-//     double-buffered: a HALO LOADER wave fetches chunk c + 1 while chunk c is consumed;
-//   * a WEIGHT LOADER wave streams the [64 k][64 n] weight stage of every (chunk, tap)
-//     through a ring of D stages, D - 1 in flight, waiting on its own vmcnt;
+//     double-buffered: chunk c + 1 is fetched (by the compute waves, once per chunk) while
+//     chunk c is consumed;
+//   * four WEIGHT LOADER waves stream the [64 k][64 n] weight stage of every (chunk, tap)
+//     through a ring of D stages, D - 1 in flight, each waiting on its own vmcnt (an
+//     LDS-DMA stream lands in issue order at ~25 GB/s per wave: a single loader wave
+//     starved the stages, layer-3 backprop-input 50.7 vs 27.6 us for the general kernel);
 //   * the four compute waves only read fragments and issue MFMAs: one barrier per stage,
 //     both 32-deep k-steps' fragments read before the MFMAs.
 // So the weights of a block are streamed once for R x W pixels (2-4x the tile of the
@@ -37,7 +40,7 @@
 namespace damd {
 namespace {
 
-constexpr int SNT = 384;       // 4 compute + weight loader + halo loader
+constexpr int SNT = 512;       // 4 compute waves (+ the halo DMA) + 4 weight-loader waves
 constexpr int WST_B = 64 * 64 * 2;  // one weight stage
 __device__ __attribute__((aligned(64))) uint4 g_zero16_s[4];
 
@@ -45,12 +48,13 @@ using tile::glds16;
 
 __device__ __forceinline__ void sbar() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// wait until at most `ahead` weight stages (8 DMA pieces each) of this wave are outstanding
+// wait until at most `ahead` weight stages (2 DMA pieces per loader wave each) of this
+// wave are outstanding
 template <int A>
 __device__ __forceinline__ void wait_stages(int ahead) {
   if constexpr (A > 0) {
     if (ahead >= A) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A * 8) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A * 2) : "memory");
       return;
     }
     wait_stages<A - 1>(ahead);
@@ -103,12 +107,16 @@ __global__ __launch_bounds__(SNT, 1) void conv3s_kernel(GemmArgs a, SGeo sg) {
     const void* p = ok ? (const void*)(src + ((long)ih * W + iw) * SC + c * 64 + 8 * cs) : zero;
     glds16(p, smem + (c & 1) * sg.hbytes + j * 1024);
   };
-  // weight stage s = (chunk s / 9, tap s % 9) into ring slot s % D, 8 pieces of 1 KiB
-  auto weight_stage = [&](int s) __attribute__((always_inline)) {
+  // loader wave l's share of weight stage s = (chunk s / 9, tap s % 9): 1 KiB pieces 2l and
+  // 2l + 1 of the stage's 8, into ring slot s % D (one LDS-DMA stream lands in issue order
+  // at ~25 GB/s per wave: four loader waves, four streams)
+  const int ldr = wave - 4;
+  auto weight_part = [&](int s) __attribute__((always_inline)) {
     const int c = s / 9, tap = s - c * 9;
     char* dst = ring + (s % D) * WST_B;
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
+    for (int u = 0; u < 2; ++u) {
+      const int p = 2 * ldr + u;
       const uint16_t* ptr;
       if constexpr (DGRAD) {  // [n = ci][k = co]: W[tap][n0 + n][c * 64 + k], k-contiguous
         const int n = 8 * p + (lane >> 3);
@@ -125,10 +133,10 @@ __global__ __launch_bounds__(SNT, 1) void conv3s_kernel(GemmArgs a, SGeo sg) {
   const int nhp = sg.hbytes / 1024;  // halo pieces per chunk (1 KiB granules, padded)
 
   // ---- prologue ---------------------------------------------------------------------
-  if (wave == 5) {
-    for (int j = 0; j < nhp; ++j) halo_piece(0, j);
-  } else if (wave == 4) {
-    for (int s = 0; s < min(D - 1, NS); ++s) weight_stage(s);
+  if (wave < 4) {
+    for (int j = wave; j < nhp; j += 4) halo_piece(0, j);
+  } else {
+    for (int s = 0; s < min(D - 1, NS); ++s) weight_part(s);
   }
   if (bnin && t < SC) {  // BatchNorm input: scale / shift of every input channel
     double s, q;
@@ -138,8 +146,8 @@ __global__ __launch_bounds__(SNT, 1) void conv3s_kernel(GemmArgs a, SGeo sg) {
     sft[t] = sc;
     sft[SC + t] = sh;
   }
-  if (wave == 5) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk 0's halo landed
-  if (wave == 4) wait_stages<D - 2>(min(D - 1, NS) - 1);            // stage 0 landed
+  if (wave < 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk 0's halo landed
+  else wait_stages<D - 2>(min(D - 1, NS) - 1);                     // stage 0 landed
 
   // compute waves: per group, the halo pixel of its lanes' output pixel at tap offset 0
   int hbase[G];
@@ -158,22 +166,18 @@ __global__ __launch_bounds__(SNT, 1) void conv3s_kernel(GemmArgs a, SGeo sg) {
   for (int s = 0; s < NS; ++s) {
     const int c = s / 9, tap = s - c * 9;
     sbar();  // stage s (and at a chunk start its halo) landed; stage s - 1 fully consumed
-    if (wave == 4) {
+    if (wave >= 4) {
       const int sn = s + D - 1;
-      if (sn < NS) weight_stage(sn);
+      if (sn < NS) weight_part(sn);
       // stage s + 1 landed before the next barrier: leave the later ones in flight
       if (s + 1 < NS) wait_stages<D - 2>(min(sn, NS - 1) - (s + 1));
       if (bnin && tap == 0) sbar();
       continue;
     }
-    if (wave == 5) {
-      // chunk c + 1's halo into the other buffer (chunk c - 1, its last user, is done)
-      if (tap == 0 && c + 1 < nch)
-        for (int j = 0; j < nhp; ++j) halo_piece(c + 1, j);
-      if (tap == 8) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // before the next chunk
-      if (bnin && tap == 0) sbar();
-      continue;
-    }
+    // compute waves: chunk c + 1's halo into the other buffer (chunk c - 1, its last user,
+    // is done), landed before the next chunk's first barrier
+    if (tap == 0 && c + 1 < nch)
+      for (int j = wave; j < nhp; j += 4) halo_piece(c + 1, j);
     char* hcur = smem + (c & 1) * sg.hbytes;
     if (bnin && tap == 0) {
       // y = bf16(relu(x * scale + shift)) in place over the chunk's in-image halo pixels
@@ -249,6 +253,8 @@ __global__ __launch_bounds__(SNT, 1) void conv3s_kernel(GemmArgs a, SGeo sg) {
       if (i < ng)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[1][j], af[i], acc[i][j]);
+    // the next chunk's halo (issued at this chunk's first stage) landed before its barrier
+    if (tap == 8 && c + 1 < nch) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 
   // ---- epilogue over the wave's G groups (rows m0s + wave * 16 G + 16 i + lane & 15) ----
@@ -330,11 +336,10 @@ __global__ __launch_bounds__(SNT, 1) void conv3s_kernel(GemmArgs a, SGeo sg) {
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-#pragma unroll
-          for (int sft_ = 1; sft_ < 16; sft_ <<= 1) {
-            csum[j][e] += __shfl_xor(csum[j][e], sft_);
-            csq[j][e] += __shfl_xor(csq[j][e], sft_);
-          }
+        {
+          csum[j][e] = row16_sum(csum[j][e]);
+          csq[j][e] = row16_sum(csq[j][e]);
+        }
       if ((lane & 15) == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -441,8 +446,10 @@ bool strip_plan(const GemmArgs& a, int cus, SGeo& sg, int& G, int& D) {
 }  // namespace
 
 int conv3s_ok(const GemmArgs& a, int dgrad, int epi) {
+  // opt-in while it loses to the general kernel (round 6: a single weight-loader wave's
+  // LDS-DMA stream could not keep the stages fed -- layer-3 backprop-input 50.7 vs 27.6 us)
   const char* ev = getenv("DAMD_CONV3S");
-  if (ev && ev[0] == '0') return 0;
+  if (!(ev && ev[0] == '1')) return 0;
   if (a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || a.Cin % 64 || a.N % 64 || a.Cin < 128) return 0;
   if (a.H < 1 || a.M % (a.H * a.W)) return 0;
   if (dgrad && (a.kc != a.Cin || a.bnin.acc)) return 0;
