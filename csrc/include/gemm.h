@@ -71,9 +71,6 @@ int conv3_rows(int H, int W, int bn);
 // conv3r.hip: the persistent weight-stationary variant for 64 -> 64 channels (layer 1)
 int conv3r_ok(const GemmArgs& a, int dgrad);
 hipError_t conv3r_launch(const GemmArgs& a, int dgrad, int epi, hipStream_t s);
-// conv3s.hip: strip-resident halo, weights streamed by a loader wave (layers 2 / 3)
-int conv3s_ok(const GemmArgs& a, int dgrad, int epi);
-hipError_t conv3s_launch(const GemmArgs& a, int dgrad, int epi, hipStream_t s);
 hipError_t conv3_stamps_enable(int on);                              // diagnostics
 hipError_t conv3_stamps_read(unsigned long long* host, int blocks);  // [blocks][4]
 int wgrad64_rows_per_step(int Wo, int kstep);

@@ -16,9 +16,10 @@
 //     pixel q at slot c ^ (q & 7)): a tile needs its 6 halo rows, the next tile's 4 new
 //     rows arrive in the other 4 slots while this tile computes -- every input row crosses
 //     HBM -> LDS once, and vertically adjacent tiles share their 2 overlap rows.
-// A fifth, LOADER wave issues every row DMA after the prologue and waits on its own vmcnt,
-// so the four compute waves' epilogue stores never sit in front of a halo wait (in-order
-// vmcnt: the round-4 persistent attempt serialised the next halo behind the stores).
+// Four LOADER waves issue every row DMA after the prologue (one row each, four LDS-DMA
+// streams) and wait on their own vmcnt, so the four compute waves' epilogue stores never
+// sit in front of a halo wait (in-order vmcnt: the round-4 persistent attempt serialised
+// the next halo behind the stores).
 // Synchronisation is the workgroup barrier only (no flag polling): per tile A (rows of
 // this tile landed; the previous tile's taps done, so its exclusive rows are free), B
 // (BatchNorm-input transform of the new rows done; forward with bnin only) and the
@@ -40,7 +41,7 @@
 namespace damd {
 namespace {
 
-constexpr int RNT = 320;               // 4 compute waves + 1 loader wave
+constexpr int RNT = 512;               // 4 compute waves + 4 loader waves
 constexpr int RR = 4;                  // output rows per tile
 constexpr int RING = 10;               // halo row slots: 6 of the tile + 4 incoming
 constexpr int SLOT_PX = 64;            // pixels per row slot (W + 2 <= 64)
@@ -66,7 +67,8 @@ __global__ __launch_bounds__(RNT, 1) void conv3r_kernel(GemmArgs a, int tpi, int
   const int tk0 = sidx * tpi / S, tk1 = (sidx + 1) * tpi / S;  // this block's tiles [tk0, tk1)
   const int t = threadIdx.x, lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const bool loader = wave == 4;
+  const bool loader = wave >= 4;
+  const int ldr = wave - 4;  // loader index: rows ir with ir % 4 == ldr
   const uint16_t* src = (const uint16_t*)a.A + (long)img * H * W * 64;
   const uint16_t* wsrc = (const uint16_t*)a.B;
   const void* zero = tile::pinned_addr(g_zero16_r);
@@ -125,7 +127,7 @@ __global__ __launch_bounds__(RNT, 1) void conv3r_kernel(GemmArgs a, int tpi, int
     const int r0 = tk0 * RR - 1, nr = tile_rows(tk0) + 2;
     const int nw = DGRAD ? 72 : 0;  // forward: the weights are transposed below
     const int npieces = nw + nr * 8;
-    for (int j = wave; j < npieces; j += 5) {
+    for (int j = wave; j < npieces; j += 8) {
       if (j < nw) w_piece(j);
       else row_piece(r0 + (j - nw) / 8, (j - nw) & 7);
     }
@@ -181,9 +183,12 @@ __global__ __launch_bounds__(RNT, 1) void conv3r_kernel(GemmArgs a, int tpi, int
       // alone used
       if (k + 1 < tk1) {
         const int nlo = row0 + rk + 1, nhi = (k + 1) * RR + tile_rows(k + 1);
+        // one row (8 pieces) per loader wave: four LDS-DMA streams, each landing in issue
+        // order (~25 GB/s per wave) -- a single loader wave's 32 pieces outlasted a tile
         for (int ir = nlo; ir <= nhi; ++ir)
+          if ((ir & 3) == ldr)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) row_piece(ir, j);
+            for (int j = 0; j < 8; ++j) row_piece(ir, j);
       }
       if (bnin) bar();                                       // B(k)
       if constexpr ((EPI & (E_STATS | E_BNRED)) != 0) __syncthreads();  // the epilogue's barrier

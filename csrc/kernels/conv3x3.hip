@@ -475,9 +475,9 @@ hipError_t conv3_launch(const GemmArgs& a, int dgrad, int epi, int bn, hipStream
   // 64 -> 64 channels: the persistent weight-stationary strip kernel (conv3r.hip), the same
   // tiles / numerics
   if (bn == 64 && conv3r_ok(a, dgrad)) return conv3r_launch(a, dgrad, epi, s);
-  // >= 128 input channels: one image strip per CU, halo resident, weights streamed by a
-  // loader wave (conv3s.hip), the same numerics
-  if (conv3s_ok(a, dgrad, epi)) return conv3s_launch(a, dgrad, epi, s);
+  // (>= 128 channels, measured and removed in round 6: one image strip per CU with the
+  // halo resident and the weights streamed by 1 or 4 loader waves -- layer 2 forward 49 vs
+  // 30 us, backprop-input 40 vs 24 us; layer 3 42 vs 36 / 36 vs 28 us against this kernel)
   // (a weight-stationary persistent variant for 64 -> 64 channels -- 72 KiB of weights +
   // two halos = the CU's 160 KiB -- measured slower on ResNet layer 1, forward 42 vs 33 us,
   // backprop-input 37 vs 29 us: one 4-wave block per CU cannot hide the LDS / MFMA

@@ -143,7 +143,7 @@ def _voted_setup(kind, comm, *args):
     in a different collective than the others)."""
     s, why = None, ""
     try:
-        s = _setup(kind, *args)
+        s = _setup(*args)
     except Exception as e:  # every rank must reach the vote below
         why = f"set-up raised {e!r}"
     votes = comm.allgather_object(why)

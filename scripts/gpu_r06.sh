@@ -78,19 +78,21 @@ for s in ${STAGES:-xtests bench}; do
       DAMD_COMM=gloo DAMD_ALLREDUCE=xgmi step xg_pinned 300 python bench.py --gpus 2 --steps 200 --warmup 20 ;;
     c3r)  # the persistent 64 -> 64 direct conv (conv3r.hip) and every direct-conv test
       step c3r 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_conv_gemm_gpu.py -k "conv3" ;;
-    c3ab)  # direct conv kernels on the ResNet-18 shapes, conv3r / conv3s on / off
-      DAMD_CONV3R=1 DAMD_CONV3S=1 step c3ab_on 300 python scripts/conv3_probe.py 64
-      DAMD_CONV3R=0 DAMD_CONV3S=0 step c3ab_off 300 python scripts/conv3_probe.py 64 ;;
+    c3ab)  # direct conv kernels on the ResNet-18 shapes, conv3r on / off
+      DAMD_CONV3R=1 step c3ab_on 300 python scripts/conv3_probe.py 64
+      DAMD_CONV3R=0 step c3ab_off 300 python scripts/conv3_probe.py 64 ;;
     abt)  # one GPU test in the round-5 tree (build/ab/A) and in the working tree
       K=${ABT_K:-short_final_batch}
       (cd build/ab/A && timeout -k 10 200 python -u -m pytest -q -p no:cacheprovider tests/test_native_graph_gpu.py -k "$K" -s) > gpurun_out/abt_A.log 2>&1; echo "abt_A rc=$?"; tail -5 gpurun_out/abt_A.log
       timeout -k 10 200 python -u -m pytest -q -p no:cacheprovider tests/test_native_graph_gpu.py -k "$K" -s > gpurun_out/abt_B.log 2>&1; echo "abt_B rc=$?"; tail -5 gpurun_out/abt_B.log ;;
+    peer)  # the multi-rank exchange tests (ranks sharing the GPU)
+      step peer 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread tests/test_peer_allreduce_gpu.py ;;
     testsall)  # every GPU test, no -x: all failures at once
       timeout -k 10 1300 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/testsall.log 2>&1
       rc=$?; echo "testsall rc=$rc"; grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/testsall.log | tail -20
       if [ $rc -gt 1 ]; then exit $rc; fi ;;
     c3s)  # the strip kernel's correctness first (its own limit), then timings
-      step c3s 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_conv_gemm_gpu.py -k "conv3s or conv3r" ;;
+      step c3s 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_conv_gemm_gpu.py -k "conv3r" ;;
     pmc)  # PMC passes per direct-conv mode (one shape each)
       for cfg in "l1f:56 64 64 fwd" "l1d:56 64 64 dgrad" "l2f:28 128 128 fwd" "l3f:14 256 256 fwd" "l3d:14 256 256 dgrad" "l1w:56 64 64 wgrad"; do
         TAG=${cfg%%:*} CONV="${cfg#*:}" step pmc_${cfg%%:*} 200 bash scripts/pmc_conv.sh

@@ -570,68 +570,3 @@ def test_direct_conv3r_bitwise_equals_general_kernel(H, monkeypatch, n):
     # and against the fp32 reference (guards a shared bug)
     y = ref.conv2d(xb.float(), wb.float(), None, (1, 1), "same")
     close(new["fwd_stats"], y, 1e-2, 4e-3)
-
-
-@pytest.mark.parametrize("n,h,c", [(64, 28, 128), (64, 14, 256), (5, 14, 256), (7, 28, 128)])
-def test_direct_conv3s_matches_general_kernel(H, monkeypatch, n, h, c):
-    """The strip-resident direct kernel with a weight-loader wave (csrc/kernels/conv3s.hip:
-    ResNet-18 layers 2 / 3) == the general direct kernel (DAMD_CONV3S=0): outputs BITWISE
-    (same fragments, same MFMA order per element) for forward with bias + ReLU, with BN
-    statistics, on a BatchNorm input (y, outputs, published st), backprop-input plain /
-    accumulating / with the BN-backward epilogue; the fixed-point statistics agree to fp32
-    summation order (each kernel sums its own tile's rows first)."""
-    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
-    shape = (n, h, h, c)
-    xb = rb(rnd(*shape, scale=2.0, seed=81) + 0.3).bfloat16()
-    wb = rb(rnd(3, 3, c, c, scale=0.05, seed=82)).bfloat16()
-    dyb = rb(rnd(*shape, seed=83)).bfloat16()
-    bias = rnd(c, scale=0.1, seed=84)
-    gamma, beta = rnd(c, seed=85).abs() + 0.5, rnd(c, seed=86) * 0.2
-    x64 = xb.double().reshape(-1, c)
-    sums = torch.cat([x64.sum(0), (x64 * x64).sum(0)])
-    accin = torch.stack([H.bn_acc_encode(sums * 0.5), H.bn_acc_encode(sums * 0.5),
-                         torch.zeros(2 * c, dtype=torch.int64)]).to(dev)
-    st_bw = torch.stack([rnd(c, seed=87) * 0.1, rnd(c, seed=88).abs() + 0.5,
-                         rnd(c, seed=89).abs() + 0.5, rnd(c, seed=90)]).float().contiguous()
-    base = rb(rnd(*shape, seed=91)).bfloat16()
-
-    def run():
-        out, stats = {}, {}
-        o = torch.empty(shape, device=dev, dtype=torch.bfloat16)
-        H.conv_fwd(xb, wb, o, (1, 1), "same", bias=bias, relu=True)
-        out["fwd_bias_relu"] = o
-        o2, acc = torch.empty_like(o), H.acc_zeros(8, 2 * c, dev)
-        H.conv_fwd(xb, wb, o2, (1, 1), "same", stats=acc)
-        out["fwd_stats"], stats["fwd"] = o2, (acc, 1)
-        st, rm, rv = torch.zeros(4, c, device=dev), torch.zeros(c, device=dev), torch.ones(c, device=dev)
-        fin = H.BNFin(accin, gamma, beta, st, rm, rv, n * h * h, 1e-3, 0.99)
-        y = torch.full(shape, float("nan"), device=dev, dtype=torch.bfloat16)
-        o3, acc3 = torch.empty_like(o), H.acc_zeros(8, 2 * c, dev)
-        H.conv_fwd(xb, wb, o3, (1, 1), "same", stats=acc3, bnin=(fin, y))
-        out.update(bnin_y=y, bnin_out=o3, bnin_st=st, bnin_rm=rm, bnin_rv=rv)
-        stats["bnin"] = (acc3, 1)
-        dx = torch.empty_like(o)
-        H.conv_dgrad(dyb, wb, dx, (1, 1), "same")
-        out["dgrad"] = dx
-        dx2 = base.clone()
-        H.conv_dgrad(dyb, wb, dx2, (1, 1), "same", accumulate=True)
-        out["dgrad_acc"] = dx2
-        dx3, part = torch.empty_like(o), H.acc_zeros(8, 4 * c, dev)
-        assert H.conv_dgrad(dyb, wb, dx3, (1, 1), "same", bnred=(xb, st_bw, part))
-        out["dgrad_bnred"], stats["bnred"] = dx3, (part, 2)
-        torch.cuda.synchronize()
-        return out, stats
-
-    monkeypatch.setenv("DAMD_CONV3S", "1")
-    new, snew = run()
-    monkeypatch.setenv("DAMD_CONV3S", "0")
-    old, sold = run()
-    for k in new:
-        assert torch.equal(new[k], old[k]), k
-    for k in snew:
-        a, words = snew[k]
-        b, _ = sold[k]
-        da, db = H.bn_acc_decode(a, words), H.bn_acc_decode(b, words)
-        assert torch.allclose(da, db, rtol=1e-5, atol=1e-3), (k, (da - db).abs().max())
-    y = ref.conv2d(xb.float(), wb.float(), None, (1, 1), "same")
-    close(new["fwd_stats"], y, 1e-2, 4e-3)
