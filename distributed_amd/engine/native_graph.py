@@ -346,6 +346,14 @@ class NativeGraphEngine(Engine):
                            and len(self._buckets) > 1)
         if self.bucket_opt and not self._comm_streams:
             self._comm_streams = [torch.cuda.Stream(dev) for _ in self._buckets]
+        # convolution weight gradients on a side stream (DAMD_WGRAD_STREAM): a conv's
+        # weight gradient and its backprop-input read the same dy and are independent, so
+        # the weight-gradient kernel (+ its split-K reduce) runs beside the backprop-input /
+        # BatchNorm-backward chain of the main stream (own workspace); joined before the
+        # optimizer, and every bucket all-reduce waits for it
+        self._wgrad_stream = torch.cuda.Stream(dev) if env.get_bool("DAMD_WGRAD_STREAM", False) else None
+        self.gemm_ws_w = torch.zeros_like(self.gemm_ws) if self._wgrad_stream is not None else None
+        self._wgrad_side_minc = env.get_int("DAMD_WGRAD_STREAM_MINC", 0)  # convs with fewer outputs stay inline
         for k, b in enumerate(self._buckets):
             b["k"] = k
         opt._iter_source = self._iterations
@@ -794,6 +802,8 @@ class NativeGraphEngine(Engine):
                 continue
             cs = self._bucket_stream(b)
             cs.wait_stream(main)
+            if self._wgrad_stream is not None:
+                cs.wait_stream(self._wgrad_stream)
             if reduce:
                 self._reduce_bucket(b, cs.cuda_stream)
             if self.bucket_opt:
@@ -957,6 +967,8 @@ class NativeGraphEngine(Engine):
         for nd in reversed(live):
             getattr(self, "_bwd_" + nd.kind)(nd)
             self._bucket_progress(nd)
+        if self._wgrad_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._wgrad_stream)
         self._mark("backward")
         self._bucket_progress(None, final=True)
         self._mark("allreduce")  # the part of the all-reduce not hidden behind backward
@@ -1158,20 +1170,13 @@ class NativeGraphEngine(Engine):
         if "dz" in nd.attrs:
             self._act_bwd(nd, dy, y.buf, nd.attrs["dz"])
             dy = nd.attrs["dz"]
-        if l.use_bias:
-            H.colsum(dy, self.gviews[id(l.bias)], workspace=self.gemm_ws)
-        if nd.attrs.get("stem4"):
-            kh, kw, cin, cout = l.kernel.shape
-            dwp = nd.attrs["dw_pad"]
-            H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=self.gemm_ws, accumulate=False)
-            H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
-        elif "dw_pad" in nd.attrs:
-            dwp = nd.attrs["dw_pad"]
-            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=self.gemm_ws, accumulate=False)
-            kh, kw, cin, cout = l.kernel.shape
-            H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
+        side = self._wgrad_stream
+        if side is not None and l.kernel.shape[-1] >= self._wgrad_side_minc:
+            side.wait_stream(torch.cuda.current_stream(self.device))  # dy and x are final
+            with torch.cuda.stream(side):
+                self._conv_wgrad(nd, xt, dy, self.gemm_ws_w)
         else:
-            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=self.gemm_ws)
+            self._conv_wgrad(nd, xt, dy, self.gemm_ws)
         if xt.needs_grad:
             wb = nd.attrs.get("w_pad", self._w(nd, l.kernel))
             acc = xt.written
@@ -1187,6 +1192,24 @@ class NativeGraphEngine(Engine):
                     H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
             else:
                 H.conv_dgrad(dy, wb, xt.grad, l.strides, l.padding, accumulate=acc, workspace=self.gemm_ws)
+
+    def _conv_wgrad(self, nd, xt, dy, ws):
+        """Bias and weight gradient of conv node nd (current stream, workspace ws)."""
+        l = nd.layer
+        if l.use_bias:
+            H.colsum(dy, self.gviews[id(l.bias)], workspace=ws)
+        if nd.attrs.get("stem4"):
+            kh, kw, cin, cout = l.kernel.shape
+            dwp = nd.attrs["dw_pad"]
+            H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=ws, accumulate=False)
+            H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
+        elif "dw_pad" in nd.attrs:
+            dwp = nd.attrs["dw_pad"]
+            H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=ws, accumulate=False)
+            kh, kw, cin, cout = l.kernel.shape
+            H.unpad_add(dwp, kh * kw, cin, cout, nd.attrs["cin_pad"], cout, self.gviews[id(l.kernel)])
+        else:
+            H.conv_wgrad(xt.buf, dy, self.gviews[id(l.kernel)], l.strides, l.padding, workspace=ws)
 
     def _bn_backward(self, bn, dy, ymask, relu, dz_out=None, mask_from_x=False):
         """BatchNorm backward of node ``bn`` for upstream gradient dy (masked by

@@ -108,6 +108,17 @@ for s in ${STAGES:-xtests bench}; do
       done ;;
     rnprof)
       step rnprof 400 bash scripts/prof_resnet.sh ;;
+    wsprof)  # kernel trace of the step with the weight-gradient side stream on
+      DAMD_WGRAD_STREAM=1 PROF_OUT=gpurun_out/prof_rn_ws step wsprof 400 bash scripts/prof_resnet.sh
+      PROF_OUT=gpurun_out/prof_rn_base step rnprof_base 400 bash scripts/prof_resnet.sh ;;
+    wstest)  # weight gradients on a side stream: bitwise against the single-stream step
+      step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
+    wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
+      for i in 1 2; do
+        DAMD_WGRAD_STREAM=0 step ws_off$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+        DAMD_WGRAD_STREAM=1 step ws_on$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+        DAMD_WGRAD_STREAM=1 DAMD_WGRAD_STREAM_MINC=128 step ws_on128_$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done ;;
   esac
 done
 echo stages-done

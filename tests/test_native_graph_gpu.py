@@ -482,6 +482,30 @@ def test_bn_applied_inside_direct_conv_is_bitwise(monkeypatch):
     assert hf == hu
 
 
+@pytest.mark.parametrize("allreduce", [False, True])
+def test_weight_gradients_on_side_stream_are_bitwise(monkeypatch, allreduce):
+    """DAMD_WGRAD_STREAM=1: every conv weight gradient (+ split-K reduce) on a side stream
+    beside the backprop-input / BN chain (own workspace, joined before the optimizer; with
+    DAMD_FORCE_ALLREDUCE each bucket all-reduce also waits on it) == the single-stream
+    step, bitwise over two momentum steps (graph replay)."""
+    def build():
+        return resnet18(classes=10, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(2, 1, 1, 1))
+
+    monkeypatch.setenv("DAMD_CONV3_MIN_WG", "1")
+    x, y = _data(64, (64, 64, 3), 10, seed=11)
+    tf.keras.backend.clear_session()
+    init = build().get_weights()
+    extra = {"DAMD_FORCE_ALLREDUCE": "1", "DAMD_BUCKET_MB": "0.05"} if allreduce else {}
+    ws, hs, es = _train(build, x, y, init, 32, 3, native=True, momentum=0.9,
+                        extra_env={**extra, "DAMD_WGRAD_STREAM": "1"})
+    w1, h1, e1 = _train(build, x, y, init, 32, 3, native=True, momentum=0.9,
+                        extra_env={**extra, "DAMD_WGRAD_STREAM": "0"})
+    assert es == e1 == "native_graph"
+    for a, b in zip(ws, w1):
+        np.testing.assert_array_equal(a, b)
+    assert hs == h1
+
+
 def test_resnet18_full_size_trains():
     x, y = _data(64, (224, 224, 3), 1000, seed=3)
     tf.keras.backend.clear_session()
