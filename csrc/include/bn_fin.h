@@ -13,14 +13,30 @@ namespace damd {
 // Forward statistics: the replicas acc[r][2][C] (one word per value) summed as integers
 // (exact, any order), then decoded; the sticky flag plane after the replicas
 // (damd_common.h bnacc_flag) turns a channel's statistics into NaN.
+// The replicas are read ACC_U at a time with every load issued before the first add: the
+// words were just written by memory-side atomics, so each dependent round trip costs a
+// memory latency -- a rolled loop (one wait per replica) made the finalize of every
+// consumer prologue 8 + 2 serialised round trips.  (Clamped indices: the loads past reps
+// re-read the last replica and are not added.)
+constexpr int ACC_U = 8;
 __device__ inline void acc_sums(const long long* acc, int reps, int C, int c, double& s, double& q) {
   long long ws = 0, wq = 0;
   reps = max(reps, 1);
-  for (int r = 0; r < reps; ++r) {
-    ws += acc[(size_t)r * 2 * C + c];
-    wq += acc[(size_t)r * 2 * C + C + c];
-  }
   const long long f = acc[(size_t)reps * 2 * C + c];
+  for (int r0 = 0; r0 < reps; r0 += ACC_U) {
+    long long vs[ACC_U], vq[ACC_U];
+#pragma unroll
+    for (int u = 0; u < ACC_U; ++u) {
+      const size_t r = (size_t)min(r0 + u, reps - 1);
+      vs[u] = acc[r * 2 * C + c];
+      vq[u] = acc[r * 2 * C + C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < ACC_U; ++u) {
+      ws += r0 + u < reps ? vs[u] : 0ll;
+      wq += r0 + u < reps ? vq[u] : 0ll;
+    }
+  }
   s = bnacc_value1(ws, f);
   q = bnacc_value1(wq, f);
 }
@@ -28,14 +44,24 @@ __device__ inline void acc_sums(const long long* acc, int reps, int C, int c, do
 __device__ inline void acc_sums2(const long long* acc, int reps, int C, int c, double& s, double& q) {
   long long sh = 0, sl = 0, qh = 0, ql = 0;
   reps = max(reps, 1);
-  for (int r = 0; r < reps; ++r) {
-    const long long* a = acc + (size_t)r * 4 * C;
-    sh += a[c];
-    sl += a[C + c];
-    qh += a[2 * C + c];
-    ql += a[3 * C + c];
-  }
   const long long f = acc[(size_t)reps * 4 * C + c];
+  for (int r0 = 0; r0 < reps; r0 += ACC_U) {
+    long long v[ACC_U][4];
+#pragma unroll
+    for (int u = 0; u < ACC_U; ++u) {
+      const long long* a = acc + (size_t)min(r0 + u, reps - 1) * 4 * C;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) v[u][p] = a[p * C + c];
+    }
+#pragma unroll
+    for (int u = 0; u < ACC_U; ++u) {
+      const bool in = r0 + u < reps;
+      sh += in ? v[u][0] : 0ll;
+      sl += in ? v[u][1] : 0ll;
+      qh += in ? v[u][2] : 0ll;
+      ql += in ? v[u][3] : 0ll;
+    }
+  }
   s = bnacc_value2(sh, sl, f);
   q = bnacc_value2(qh, ql, f);
 }

@@ -1719,6 +1719,22 @@ static int fin_rows_cap() {
   }();
   return cap;
 }
+// ... and at least DAMD_BN_FIN_MINKB KiB of each input tensor per block: every block reads
+// all R x 4C accumulator words, which on the deep layers (C = 512: 128 KiB per block) was
+// more than the block's share of the data
+static int fin_rows_grid(long M, int C) {
+  static long minb = -1;
+  if (minb < 0) {
+    const char* e = getenv("DAMD_BN_FIN_MINKB");
+    minb = e ? atol(e) * 1024 : 0;
+  }
+  int g = rows_grid(M, C, fin_rows_cap());
+  if (minb > 0) {
+    const long cap = ((long)M * C * 2 + minb - 1) / minb;
+    if (g > cap) g = (int)(cap < 1 ? 1 : cap);
+  }
+  return g;
+}
 
 // blocks of a consumer that finalizes in its prologue: every block pays one pass over the
 // C channels, so the grid-stride kernels run at most 8 blocks per CU
@@ -1736,7 +1752,7 @@ hipError_t bn_apply(const uint16_t* x, const float* st, const uint16_t* r, const
   // (the f2 region starts at 4C: allocate it whenever f2 finalizes)
   const size_t lds2 = b.acc ? 8 * C * sizeof(float) : lds;
   if (NT % (C / 8) == 0) {
-    hipLaunchKernelGGL(bn_apply_rows_k, dim3(rows_grid(M, C, (a.acc || b.acc) ? fin_rows_cap() : 16384)), dim3(NT),
+    hipLaunchKernelGGL(bn_apply_rows_k, dim3((a.acc || b.acc) ? fin_rows_grid(M, C) : rows_grid(M, C, 16384)), dim3(NT),
                        lds2, s, x, st, r, st2,
                        res_mode, relu, y, M, C, a, b);
     return hipGetLastError();
@@ -1759,6 +1775,16 @@ int bn_bwd_blocks(long M, int C) {
   const int rpi = NT / (C / 8);
   long rows = (M + target - 1) / target;
   if (rows < rpi) rows = rpi;
+  // at least DAMD_BN_BWD_MINKB KiB of dy per block: on the small deep layers (M = 3136 rows
+  // of 512 channels) the 512-block target gave 7 rows per block, and the 4C fixed-point
+  // atomics of every block, not the 6 MB read, set the launch time
+  static long minb = -1;
+  if (minb < 0) {
+    const char* e = getenv("DAMD_BN_BWD_MINKB");
+    minb = e ? atol(e) * 1024 : 0;
+  }
+  const long row_bytes = (long)C * 2;
+  if (minb > 0 && rows * row_bytes < minb) rows = (minb + row_bytes - 1) / row_bytes;
   return (int)((M + rows - 1) / rows);
 }
 
@@ -1790,7 +1816,7 @@ hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, co
   const BNBwdFin f = bf ? *bf : kNoBwdFin;
   if (f.acc && (!f.co || C > FIN_MAX_C)) return hipErrorInvalidValue;
   if (NT % (C / 8) == 0) {
-    hipLaunchKernelGGL(bn_bwd_apply_rows_k, dim3(rows_grid(M, C, f.acc ? fin_rows_cap() : 16384)), dim3(NT),
+    hipLaunchKernelGGL(bn_bwd_apply_rows_k, dim3(f.acc ? fin_rows_grid(M, C) : rows_grid(M, C, 16384)), dim3(NT),
                        f.acc ? 3 * C * sizeof(float) : 0, s, dy, y,
                        relu_mask, x, st, co, dx, M, C, f);
     return hipGetLastError();

@@ -111,6 +111,18 @@ for s in ${STAGES:-xtests bench}; do
     wsprof)  # kernel trace of the step with the weight-gradient side stream on
       DAMD_WGRAD_STREAM=1 PROF_OUT=gpurun_out/prof_rn_ws step wsprof 400 bash scripts/prof_resnet.sh
       PROF_OUT=gpurun_out/prof_rn_base step rnprof_base 400 bash scripts/prof_resnet.sh ;;
+    rnab)  # ResNet-18 step, build/ab/A (scripts/ab_build.sh) against the working tree, alternating
+      for i in 1 2 3; do
+        step rnab_A$i 300 bash -c "cd build/ab/A && python bench.py --model resnet18 --steps 50 --warmup 10"
+        step rnab_B$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done
+      grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/rnab_A*.log gpurun_out/rnab_B*.log ;;
+    bngrid)  # BN kernel grids: minimum KiB per block (apply with finalize / backward reduce)
+      for cfg in "0 0" "32 0" "64 0" "0 32" "0 64" "32 32" "0 0"; do
+        set -- $cfg
+        DAMD_BN_FIN_MINKB=$1 DAMD_BN_BWD_MINKB=$2 step bng_$1_$2 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/bng_*.log ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
