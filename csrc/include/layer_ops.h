@@ -66,6 +66,16 @@ hipError_t bn_bwd_finalize(const float* part, int T, int C, float count, const f
 hipError_t bn_bwd_apply(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x, const float* st,
                         const float* co, uint16_t* dx, long M, int C, hipStream_t s, const BNBwdFin* bf = nullptr);
 
+// Two BatchNorms of the same masked gradient (relu_mask 0 / 1), fixed-point accumulators
+// and in-consumer finalize only: one reduce pass and one apply pass for both (bitwise the
+// two single-BN launch pairs)
+hipError_t bn_bwd_reduce_dual(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
+                              const uint16_t* x2, const float* st, const float* st2, int T, long M, int C,
+                              hipStream_t s, long long* acc, long long* acc2, int acc_reps);
+hipError_t bn_bwd_apply_dual(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
+                             const uint16_t* x2, const float* st, const float* st2, uint16_t* dx, uint16_t* dx2,
+                             long M, int C, hipStream_t s, const BNBwdFin& bf, const BNBwdFin& bf2);
+
 // Pooling ----------------------------------------------------------------------------------
 hipError_t maxpool_fwd(const uint16_t* x, int N, int H, int W, int C, int ph, int pw, int sh, int sw, int pad_t,
                        int pad_l, int Ho, int Wo, uint16_t* y, uint8_t* arg, hipStream_t s);

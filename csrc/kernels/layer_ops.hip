@@ -409,6 +409,146 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
   }
 }
 
+// Two BatchNorms fed by the same masked gradient (a ResNet downsampling block's output
+// relu(BN2(x2) + BNd(xd))): ONE pass over dy and the mask source y for both -- per
+// channel sum dz (shared), sum dz * xhat2, sum dz * xhatd -- each BN's partials into its own
+// accumulator.  The row ranges, the per-thread order and the LDS tree are those of
+// bn_bwd_reduce_k, so each accumulator receives bitwise the partials the single-BN launch
+// would add (relu_mask 0 / 1 only; fixed-point accumulators only).
+__global__ __launch_bounds__(NT) void bn_bwd_reduce2_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
+                                                       int relu_mask, const uint16_t* __restrict__ x,
+                                                       const uint16_t* __restrict__ x2, const float* __restrict__ st,
+                                                       const float* __restrict__ st2, long M, int C,
+                                                       long rows_per_block, long long* __restrict__ acc,
+                                                       long long* __restrict__ acc2, int reps) {
+  __shared__ float red[3][NT * 8];
+  const int cg = C / 8, t = threadIdx.x;
+  const int rpi = NT / cg;
+  const int g = t % cg, rr = t / cg;
+  const int c = g * 8;
+  const long blk = blockIdx.x;
+  float s0[8], s1[8], s2[8], mean[8], inv[8], mean2[8], inv2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s0[e] = s1[e] = s2[e] = 0.f;
+  ld8f(st + c, mean);
+  ld8f(st + C + c, inv);
+  ld8f(st2 + c, mean2);
+  ld8f(st2 + C + c, inv2);
+  const long r0 = blk * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  if (rr < rpi) {
+    for (long row = r0 + rr; row < r1; row += rpi) {
+      const long off = (row * C + c) / 8;
+      float d[8], xv[8], xw[8];
+      unpack8(reinterpret_cast<const uint4*>(dy)[off], d);
+      unpack8(reinterpret_cast<const uint4*>(x)[off], xv);
+      unpack8(reinterpret_cast<const uint4*>(x2)[off], xw);
+      if (relu_mask) {
+        float yv[8];
+        unpack8(reinterpret_cast<const uint4*>(y)[off], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s0[e] += d[e];
+        s1[e] += d[e] * (xv[e] - mean[e]) * inv[e];
+        s2[e] += d[e] * (xw[e] - mean2[e]) * inv2[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    red[0][t * 8 + e] = rr < rpi ? s0[e] : 0.f;
+    red[1][t * 8 + e] = rr < rpi ? s1[e] : 0.f;
+    red[2][t * 8 + e] = rr < rpi ? s2[e] : 0.f;
+  }
+  __syncthreads();
+  for (int ch = t; ch < C; ch += NT) {
+    const int gg = ch / 8, e = ch % 8;
+    float a = 0.f, b = 0.f, b2 = 0.f;
+    for (int q = 0; q < rpi; ++q) {
+      a += red[0][(q * cg + gg) * 8 + e];
+      b += red[1][(q * cg + gg) * 8 + e];
+      b2 += red[2][(q * cg + gg) * 8 + e];
+    }
+    put_partial(nullptr, acc, reps, C, ch, a, b);
+    put_partial(nullptr, acc2, reps, C, ch, a, b2);
+  }
+}
+
+// ... and the matching apply: both BNs' coefficients finalized in the prologue, dx and dx2
+// from one read of dy / y (row mapping and arithmetic of bn_bwd_apply_rows_k)
+__global__ __launch_bounds__(NT) void bn_bwd_apply2_rows_k(const uint16_t* __restrict__ dy,
+                                                           const uint16_t* __restrict__ y, int relu_mask,
+                                                           const uint16_t* __restrict__ x,
+                                                           const uint16_t* __restrict__ x2,
+                                                           const float* __restrict__ st,
+                                                           const float* __restrict__ st2, uint16_t* __restrict__ dx,
+                                                           uint16_t* __restrict__ dx2, long M, int C, BNBwdFin bf,
+                                                           BNBwdFin bf2) {
+  extern __shared__ float sfin[];  // [3][C] (bf), then [3][C] (bf2)
+  const int cg = C / 8, t = threadIdx.x, rpi = NT / cg;
+  const int g = t % cg, rr = t / cg, c = g * 8;
+  const long stride = (long)gridDim.x * rpi;
+  const uint4* d4 = reinterpret_cast<const uint4*>(dy);
+  const uint4* x4 = reinterpret_cast<const uint4*>(x);
+  const uint4* w4 = reinterpret_cast<const uint4*>(x2);
+  const uint4* y4 = reinterpret_cast<const uint4*>(y);
+  uint4* o4 = reinterpret_cast<uint4*>(dx);
+  uint4* p4 = reinterpret_cast<uint4*>(dx2);
+  uint4 dq[BN_UNR], xq[BN_UNR], wq[BN_UNR], yq[BN_UNR];
+  auto load = [&](long row0) {
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = min(row0 + u * stride, M - 1);
+      dq[u] = d4[row * cg + g];
+      xq[u] = x4[row * cg + g];
+      wq[u] = w4[row * cg + g];
+      if (relu_mask) yq[u] = y4[row * cg + g];
+    }
+  };
+  long row0 = (long)blockIdx.x * rpi + rr;
+  load(row0);
+  const float* co = bn_bwd_fin_prologue(bf, C, st, sfin, bf.co);
+  const float* co2 = bn_bwd_fin_prologue(bf2, C, st2, sfin + 3 * C, bf2.co);
+  float mean[8], inv[8], a[8], b[8], cc[8], mean2[8], inv2[8], a2[8], b2[8], cc2[8];
+  ld8f(st + c, mean);
+  ld8f(st + C + c, inv);
+  ld8f(co + c, a);
+  ld8f(co + C + c, b);
+  ld8f(co + 2 * C + c, cc);
+  ld8f(st2 + c, mean2);
+  ld8f(st2 + C + c, inv2);
+  ld8f(co2 + c, a2);
+  ld8f(co2 + C + c, b2);
+  ld8f(co2 + 2 * C + c, cc2);
+  for (bool first = true; row0 < M; row0 += stride * BN_UNR, first = false) {
+    if (!first) load(row0);
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      const long row = row0 + u * stride;
+      if (row >= M) break;
+      float d[8], xv[8], xw[8], o[8], p[8];
+      unpack8(dq[u], d);
+      unpack8(xq[u], xv);
+      unpack8(wq[u], xw);
+      if (relu_mask) {
+        float yv[8];
+        unpack8(yq[u], yv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = a[e] * d[e] + b[e] + cc[e] * (xv[e] - mean[e]) * inv[e];
+        p[e] = a2[e] * d[e] + b2[e] + cc2[e] * (xw[e] - mean2[e]) * inv2[e];
+      }
+      o4[row * cg + g] = pack8(o);
+      p4[row * cg + g] = pack8(p);
+    }
+  }
+}
+
 __global__ __launch_bounds__(FT) void bn_bwd_finalize_k(const float* part, int T, int C, float count,
                                                         const float* st, float* dgamma, float* dbeta, float* co) {
   __shared__ double sums[16];
@@ -1798,6 +1938,28 @@ hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, c
   const long rows = (M + T - 1) / T;
   hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows,
                      acc, acc_reps, g_bn_reduce_reverse ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_reduce_dual(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
+                              const uint16_t* x2, const float* st, const float* st2, int T, long M, int C,
+                              hipStream_t s, long long* acc, long long* acc2, int acc_reps) {
+  if (C % 8 || C / 8 > NT || !acc || !acc2 || acc_reps < 1 || relu_mask < 0 || relu_mask > 1)
+    return hipErrorInvalidValue;
+  const long rows = (M + T - 1) / T;
+  hipLaunchKernelGGL(bn_bwd_reduce2_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, x2, st, st2, M, C, rows, acc,
+                     acc2, acc_reps);
+  return hipGetLastError();
+}
+
+hipError_t bn_bwd_apply_dual(const uint16_t* dy, const uint16_t* y, int relu_mask, const uint16_t* x,
+                             const uint16_t* x2, const float* st, const float* st2, uint16_t* dx, uint16_t* dx2,
+                             long M, int C, hipStream_t s, const BNBwdFin& bf, const BNBwdFin& bf2) {
+  if (C % 8 || NT % (C / 8) || !bf.acc || !bf2.acc || !bf.co || !bf2.co || C > FIN_MAX_C || relu_mask < 0 ||
+      relu_mask > 1)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_apply2_rows_k, dim3(fin_rows_grid(M, C)), dim3(NT), 6 * C * sizeof(float), s, dy, y,
+                     relu_mask, x, x2, st, st2, dx, dx2, M, C, bf, bf2);
   return hipGetLastError();
 }
 

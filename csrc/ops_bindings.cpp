@@ -184,6 +184,21 @@ void register_kernel_ops(py::module_& m) {
                              f.co, P_<u16>(dx), M, C, P_<ihipStream_t>(s), &f),
           "bn_bwd_apply_fin");
   });
+  m.def("bn_bwd_reduce_dual_acc", [](U dy, U y, int relu_mask, U x, U x2, U st, U st2, U acc, U acc2, int T, long M,
+                                     int C, U s, int reps) {
+    check(damd::bn_bwd_reduce_dual(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x),
+                                   P_<const u16>(x2), P_<const float>(st), P_<const float>(st2), T, M, C,
+                                   P_<ihipStream_t>(s), P_<long long>(acc), P_<long long>(acc2), reps),
+          "bn_bwd_reduce_dual_acc");
+  });
+  m.def("bn_bwd_apply_dual_fin", [mkbfin](U dy, U y, int relu_mask, U x, U x2, U st, U st2, U dx, U dx2, long M,
+                                          int C, std::vector<U> bp, std::vector<U> bp2, float count, U s, int reps) {
+    const damd::BNBwdFin f = mkbfin(bp, count, reps), f2 = mkbfin(bp2, count, reps);
+    check(damd::bn_bwd_apply_dual(P_<const u16>(dy), P_<const u16>(y), relu_mask, P_<const u16>(x),
+                                  P_<const u16>(x2), P_<const float>(st), P_<const float>(st2), P_<u16>(dx),
+                                  P_<u16>(dx2), M, C, P_<ihipStream_t>(s), f, f2),
+          "bn_bwd_apply_dual_fin");
+  });
   m.def("bn_relu_maxpool_fwd_fin", [mkfin](U x, std::vector<int> g, U y, U arg, std::vector<U> p, std::vector<float> v,
                                            U s) {
     if (g.size() != 12) throw std::invalid_argument("pool geometry");

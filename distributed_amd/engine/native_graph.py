@@ -1323,8 +1323,31 @@ class NativeGraphEngine(Engine):
                 fin()
         else:
             # both BN backwards mask dy by [out > 0] themselves (no separate ReLU-backward pass)
-            self._bn_backward(main, dy, out.buf, relu)
-            self._bn_backward(other, dy, out.buf, relu)
+            if not self._bn_backward_dual(main, other, dy, out.buf, relu):
+                self._bn_backward(main, dy, out.buf, relu)
+                self._bn_backward(other, dy, out.buf, relu)
+
+    def _bn_backward_dual(self, b1, b2, dy, ymask, relu):
+        """Both BatchNorms of relu(BN(x) + BN(xd)) in one reduce and one apply launch
+        (H.bn_bwd_fin_dual) when both finalize in their consumers and own their inputs'
+        gradients (DAMD_BN_DUAL=0: four launches)."""
+        if not env.get_bool("DAMD_BN_DUAL", True):
+            return False
+        xs = [b.inputs[0].root() for b in (b1, b2)]
+        if (any(b.attrs.get("fin") is None or b.attrs.get("dgrad_fused") for b in (b1, b2))
+                or xs[0] is xs[1] or any(x.written or not x.needs_grad for x in xs)
+                or xs[0].shape != xs[1].shape or xs[0].shape[-1] % 8 or 256 % (xs[0].shape[-1] // 8)):
+            return False
+        args = []
+        for b, x in zip((b1, b2), xs):
+            dx, fin = self._grad_target(x)
+            assert fin is None  # first writer (checked above)
+            l = b.layer
+            args.append({"x": x.buf, "st": b.attrs["st"], "acc": b.attrs["acc_b"], "co": b.attrs["co"], "dx": dx,
+                         "dgamma": self.gviews[id(l.gamma)] if l.gamma is not None else None,
+                         "dbeta": self.gviews[id(l.beta)] if l.beta is not None else None})
+        H.bn_bwd_fin_dual(dy, ymask if relu else None, 1 if relu else 0, args)
+        return True
 
     def _bwd_MaxPooling2D(self, nd):
         l = nd.layer

@@ -839,8 +839,34 @@ def bn_bwd_fin(dy, y, relu_mask, x, st, acc, co, dx, dgamma=None, dbeta=None, dz
     if reduce:
         _C().bn_bwd_reduce_acc(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dz_out), _ptr(acc), T, M, C,
                                s, r)
+        if dz_out is not None and relu_mask:
+            # the reduce just wrote the masked gradient: the apply reads it instead of dy and
+            # the mask source (one input tensor less, the same values)
+            dy, y, relu_mask = dz_out, None, 0
     _C().bn_bwd_apply_fin(_ptr(dy), _ptr(y), int(relu_mask), _ptr(x), _ptr(st), _ptr(dx), M, C,
                           [_ptr(acc), _ptr(dgamma), _ptr(dbeta), _ptr(co)], float(M), s, r)
+
+
+def bn_bwd_fin_dual(dy, y, relu_mask, bns):
+    """Backward of two BatchNorms fed by the same (masked) gradient dy -- the two BN inputs
+    of relu(BN(x) + BN(xd)) -- in two launches instead of four (bn_bwd_reduce_dual /
+    bn_bwd_apply_dual: one read of dy and the mask source y for both, bitwise the single-BN
+    launches).  bns: two dicts x, st, acc, co, dx, dgamma, dbeta."""
+    a, b = bns
+    C = a["x"].shape[-1]
+    M = a["x"].numel() // C
+    if b["x"].shape != a["x"].shape or acc_reps(a["acc"]) != acc_reps(b["acc"]) or relu_mask not in (0, 1):
+        raise ValueError("bn_bwd_fin_dual: the two BatchNorms must match in shape and replicas")
+    T = _C().bn_bwd_blocks(M, C)
+    s = stream_handle()
+    r = acc_reps(a["acc"])
+    _C().bn_bwd_reduce_dual_acc(_ptr(dy), _ptr(y), int(relu_mask), _ptr(a["x"]), _ptr(b["x"]), _ptr(a["st"]),
+                                _ptr(b["st"]), _ptr(a["acc"]), _ptr(b["acc"]), T, M, C, s, r)
+    _C().bn_bwd_apply_dual_fin(_ptr(dy), _ptr(y), int(relu_mask), _ptr(a["x"]), _ptr(b["x"]), _ptr(a["st"]),
+                               _ptr(b["st"]), _ptr(a["dx"]), _ptr(b["dx"]), M, C,
+                               [_ptr(a["acc"]), _ptr(a.get("dgamma")), _ptr(a.get("dbeta")), _ptr(a["co"])],
+                               [_ptr(b["acc"]), _ptr(b.get("dgamma")), _ptr(b.get("dbeta")), _ptr(b["co"])],
+                               float(M), s, r)
 
 
 def bn_relu_maxpool_fwd_fin(x, y, arg, pool, strides, padding, fin: BNFin):

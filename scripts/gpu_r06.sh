@@ -123,6 +123,9 @@ for s in ${STAGES:-xtests bench}; do
         DAMD_BN_FIN_MINKB=$1 DAMD_BN_BWD_MINKB=$2 step bng_$1_$2 300 python bench.py --model resnet18 --steps 50 --warmup 10
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/bng_*.log ;;
+    dual)  # dual-BN backward + the apply reading the masked gradient: bitwise tests
+      step dual 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_native_graph_gpu.py \
+        -k "dual or bitwise or short_final or one_step or emulated" ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating

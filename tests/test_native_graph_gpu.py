@@ -482,6 +482,38 @@ def test_bn_applied_inside_direct_conv_is_bitwise(monkeypatch):
     assert hf == hu
 
 
+def test_dual_bn_backward_is_bitwise():
+    """The two BatchNorms of every downsampling block's output relu(BN(conv) + BN(shortcut))
+    go through ONE reduce and ONE apply launch (bn_bwd_reduce_dual / bn_bwd_apply_dual) ==
+    the four single-BN launches (DAMD_BN_DUAL=0), bitwise over two momentum steps; the dual
+    path must actually be taken (3 downsampling blocks)."""
+    from distributed_amd.engine import native_graph as ng
+
+    calls = []
+    orig = ng.NativeGraphEngine._bn_backward_dual
+
+    def spy(self, *a, **k):
+        r = orig(self, *a, **k)
+        calls.append(r)
+        return r
+
+    x, y = _data(64, (32, 32, 3), 10, seed=12)
+    tf.keras.backend.clear_session()
+    init = _small_resnet().get_weights()
+    ng.NativeGraphEngine._bn_backward_dual = spy
+    try:
+        wd, hd, ed = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9)
+    finally:
+        ng.NativeGraphEngine._bn_backward_dual = orig
+    assert calls and any(calls), calls
+    ws, hs, es = _train(_small_resnet, x, y, init, 32, 2, native=True, momentum=0.9,
+                        extra_env={"DAMD_BN_DUAL": "0"})
+    assert ed == es == "native_graph"
+    for a, b in zip(wd, ws):
+        np.testing.assert_array_equal(a, b)
+    assert hd == hs
+
+
 @pytest.mark.parametrize("allreduce", [False, True])
 def test_weight_gradients_on_side_stream_are_bitwise(monkeypatch, allreduce):
     """DAMD_WGRAD_STREAM=1: every conv weight gradient (+ split-K reduce) on a side stream
