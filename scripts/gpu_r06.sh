@@ -126,6 +126,26 @@ for s in ${STAGES:-xtests bench}; do
     dual)  # dual-BN backward + the apply reading the masked gradient: bitwise tests
       step dual 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_native_graph_gpu.py \
         -k "dual or bitwise or short_final or one_step or emulated" ;;
+    stem)  # stem BN/ReLU/MaxPool kernels: numerics, then the step with the stem reduce grid swept
+      step stemt 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_hip_ops_gpu.py \
+        tests/test_native_graph_gpu.py tests/test_conv_gemm_gpu.py -k "pool or stem or maxpool" ;;
+    stemab)
+      for i in 1 2; do
+        step stab_A$i 300 bash -c "cd build/ab/A && python bench.py --model resnet18 --steps 50 --warmup 10"
+        step stab_B$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+        DAMD_POOL_BN_BLOCKS=1024 step stab_B1024_$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+        DAMD_POOL_BN_BLOCKS=2048 step stab_B2048_$i 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/stab_*.log ;;
+    profab)  # kernel traces of build/ab/A and the working tree
+      step profA 400 bash -c "cd build/ab/A && PROF_OUT=\$GRAFT_REPO_ROOT/gpurun_out/prof_A bash scripts/prof_resnet.sh"
+      PROF_OUT=gpurun_out/prof_B step profB 400 bash scripts/prof_resnet.sh ;;
+    splitsw)  # split-K planner thresholds (minimum tiles to skip split-K / target workgroups)
+      for cfg in "320 384" "100 384" "200 384" "320 256" "320 512" "320 768" "320 384"; do
+        set -- $cfg
+        DAMD_SPLIT_MIN_TILES=$1 DAMD_SPLIT_TARGET_WG=$2 step spl_$1_$2 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/spl_*.log ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
