@@ -92,6 +92,36 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) csum[j][e] = csq[j][e] = 0.f;
+  // The epilogue's global operands (the residual R, or the BN input x and its coefficients)
+  // are ALL requested before the first store: interleaved with the stores, which may alias
+  // them, every (i, j) fragment waited for its own load -- 16 dependent memory round trips
+  // per tile (the layer-1 backprop-input + BN-partials launch ran ~17 us longer than the
+  // forward).  Out-of-range fragments load a clamped in-range address and are skipped below.
+  constexpr bool kPre = (EPI & (E_ADD | E_BNRED)) != 0;
+  static_assert((EPI & E_ADD) == 0 || (EPI & E_BNRED) == 0, "one prefetched epilogue operand");
+  uint2 pre[kPre ? 4 : 1][kPre ? 4 : 1];
+  float4 bco[(EPI & E_BNRED) ? 4 : 1][4];
+  if constexpr (kPre) {
+    const uint16_t* pbase = (EPI & E_ADD) ? (const uint16_t*)a.R : a.bnx;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+      const size_t orow = row_of(m < a.M ? m : 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        pre[i][j] = *reinterpret_cast<const uint2*>(pbase + orow * a.ldc + (n < a.N ? n : 0));
+      }
+    }
+    if constexpr (EPI & E_BNRED) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4), nc = n < a.N ? n : 0;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) bco[j][p] = *reinterpret_cast<const float4*>(a.bnst + p * a.N + nc);
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm * 64 + i * 16 + (lane & 15);
@@ -110,7 +140,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
       }
       if constexpr (EPI & E_ADD) {
         if (ok) {
-          const uint2 r = *reinterpret_cast<const uint2*>((const uint16_t*)a.R + orow * a.ldc + n);
+          const uint2 r = pre[i][j];
           v[0] += __uint_as_float(r.x << 16);
           v[1] += __uint_as_float(r.x & 0xffff0000u);
           v[2] += __uint_as_float(r.y << 16);
@@ -130,13 +160,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& a, f32x4 (&acc)[4][4], 
         // BN-backward partials of the stored gradient dy: dz = dy * [bf16(relu(x sc + sh)) > 0]
         // (the mask exactly as bn_apply stored the ReLU output), sum dz, sum dz * xhat
         if (ok) {
-          const uint2 xr = *reinterpret_cast<const uint2*>(a.bnx + orow * a.ldc + n);
+          const uint2 xr = pre[i][j];
           const float xv[4] = {__uint_as_float(xr.x << 16), __uint_as_float(xr.x & 0xffff0000u),
                                __uint_as_float(xr.y << 16), __uint_as_float(xr.y & 0xffff0000u)};
-          const float4 mu = *reinterpret_cast<const float4*>(a.bnst + n);
-          const float4 iv = *reinterpret_cast<const float4*>(a.bnst + a.N + n);
-          const float4 sc = *reinterpret_cast<const float4*>(a.bnst + 2 * a.N + n);
-          const float4 sh = *reinterpret_cast<const float4*>(a.bnst + 3 * a.N + n);
+          const float4 mu = bco[j][0], iv = bco[j][1], sc = bco[j][2], sh = bco[j][3];
           const float m4[4] = {mu.x, mu.y, mu.z, mu.w}, i4[4] = {iv.x, iv.y, iv.z, iv.w};
           const float s4[4] = {sc.x, sc.y, sc.z, sc.w}, h4[4] = {sh.x, sh.y, sh.z, sh.w};
 #pragma unroll

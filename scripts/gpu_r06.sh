@@ -146,6 +146,9 @@ for s in ${STAGES:-xtests bench}; do
         DAMD_SPLIT_MIN_TILES=$1 DAMD_SPLIT_TARGET_WG=$2 step spl_$1_$2 300 python bench.py --model resnet18 --steps 50 --warmup 10
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/spl_*.log ;;
+    epi)  # epilogue operand prefetch: every conv / GEMM numerics test, then the A/B
+      step epit 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gemm_gpu.py \
+        tests/test_hip_ops_gpu.py tests/test_native_graph_gpu.py -k "not full_size and not side_stream" ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
