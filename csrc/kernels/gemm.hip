@@ -552,38 +552,69 @@ __global__ __launch_bounds__(NT) void splitk_finish_k(const float* __restrict__ 
   }
   const size_t plane = (size_t)M * N;
   if (r0 < rp) {
-    for (long m = row0 + r0; m < row1; m += rp) {
-      float v[8];
-      const float* p = slab + (size_t)m * N + n;
-      float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-      for (int sp = 1; sp < S; ++sp) {
-        const float* q = p + sp * plane;
-        a = *reinterpret_cast<const float4*>(q);
-        b = *reinterpret_cast<const float4*>(q + 4);
-        v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-      }
-      if (R) {
-        const uint4 r = *reinterpret_cast<const uint4*>(R + (size_t)m * ldc + n);
-        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+    // FR rows per pass and the first FS splits of each requested together, before the
+    // pass's stores (R may alias `out`, so the compiler kept every load behind the previous
+    // row's store: rows x splits dependent round trips per thread); splits summed in
+    // ascending order as before, so the bits are unchanged
+    constexpr int FR = 2, FS = 4;
+    for (long mb = row0 + r0; mb < row1; mb += FR * rp) {
+      float4 la[FR][FS], lb[FR][FS];
+      uint4 rq[FR];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v[2 * k] += __uint_as_float(w[k] << 16);
-          v[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      for (int f = 0; f < FR; ++f) {
+        const long m = min(mb + f * rp, row1 - 1);
+        const float* p = slab + (size_t)m * N + n;
+#pragma unroll
+        for (int u = 0; u < FS; ++u) {
+          const float* q = p + (size_t)min(u, S - 1) * plane;
+          la[f][u] = *reinterpret_cast<const float4*>(q);
+          lb[f][u] = *reinterpret_cast<const float4*>(q + 4);
         }
+        if (R) rq[f] = *reinterpret_cast<const uint4*>(R + (size_t)m * ldc + n);
       }
-      uint32_t pk[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint16_t h = f2bf(v[e] + bv[e]);
-        const float x = bf2f(h);  // statistics of the stored value
-        cs[e] += x;
-        cq[e] += x * x;
-        const uint16_t o = relu ? f2bf(fmaxf(x, 0.f)) : h;
-        if (e & 1) pk[e >> 1] |= (uint32_t)o << 16;
-        else pk[e >> 1] = o;
+      for (int f = 0; f < FR; ++f) {
+        const long m = mb + f * rp;
+        if (m >= row1) break;
+        float v[8];
+        const float* p = slab + (size_t)m * N + n;
+        float4 a = la[f][0], b = lb[f][0];
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+#pragma unroll
+        for (int u = 1; u < FS; ++u) {
+          if (u >= S) break;
+          a = la[f][u];
+          b = lb[f][u];
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+        }
+        for (int sp = FS; sp < S; ++sp) {
+          const float* q = p + sp * plane;
+          a = *reinterpret_cast<const float4*>(q);
+          b = *reinterpret_cast<const float4*>(q + 4);
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+        }
+        if (R) {
+          const uint4 r = rq[f];
+          const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[2 * k] += __uint_as_float(w[k] << 16);
+            v[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+          }
+        }
+        uint32_t pk[4];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint16_t h = f2bf(v[e] + bv[e]);
+          const float x = bf2f(h);  // statistics of the stored value
+          cs[e] += x;
+          cq[e] += x * x;
+          const uint16_t o = relu ? f2bf(fmaxf(x, 0.f)) : h;
+          if (e & 1) pk[e >> 1] |= (uint32_t)o << 16;
+          else pk[e >> 1] = o;
+        }
+        *reinterpret_cast<uint4*>(out + (size_t)m * ldc + n) = uint4{pk[0], pk[1], pk[2], pk[3]};
       }
-      *reinterpret_cast<uint4*>(out + (size_t)m * ldc + n) = uint4{pk[0], pk[1], pk[2], pk[3]};
     }
   }
   if (!stats && !stats_acc) return;
