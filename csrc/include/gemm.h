@@ -71,6 +71,11 @@ int conv3_rows(int H, int W, int bn);
 // conv3r.hip: the persistent weight-stationary variant for 64 -> 64 channels (layer 1)
 int conv3r_ok(const GemmArgs& a, int dgrad);
 hipError_t conv3r_launch(const GemmArgs& a, int dgrad, int epi, hipStream_t s);
+// conv_stem.hip: the direct packed-tap stem forward (A_CONV64 with Cin == 4; 0: not taken)
+int stem_direct_ok(const GemmArgs& a, int epi, int splits);
+hipError_t stem_direct_launch(const GemmArgs& a, int epi, hipStream_t s);
+hipError_t stem_stamps_enable(int on);                              // diagnostics
+hipError_t stem_stamps_read(unsigned long long* host, int blocks);  // [blocks][8]
 hipError_t conv3_stamps_enable(int on);                              // diagnostics
 hipError_t conv3_stamps_read(unsigned long long* host, int blocks);  // [blocks][4]
 int wgrad64_rows_per_step(int Wo, int kstep);

@@ -553,6 +553,8 @@ hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, i
   }
   if (!dg && a.ldb % 8) return hipErrorInvalidValue;
   if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
+  // the stem: input rows staged once per tile (conv_stem.hip; same tiles and bits)
+  if (stem && stem_direct_ok(a, epi, splits)) return stem_direct_launch(a, epi, s);
   if (tile == 1)
     return dg ? launch_epi<256, 64, true>(a, epi, splits, kb, s) : launch_epi<256, 64, false>(a, epi, splits, kb, s);
   return dg ? launch_epi<128, 128, true>(a, epi, splits, kb, s) : launch_epi<128, 128, false>(a, epi, splits, kb, s);

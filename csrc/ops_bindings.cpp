@@ -87,6 +87,12 @@ void register_kernel_ops(py::module_& m) {
     check(damd::conv3_stamps_read(v.data(), blocks), "conv3_stamps_read");
     return v;
   });
+  m.def("stem_stamps_enable", [](int on) { check(damd::stem_stamps_enable(on), "stem_stamps_enable"); });
+  m.def("stem_stamps_read", [](int blocks) {
+    std::vector<unsigned long long> v((size_t)blocks * 8);
+    check(damd::stem_stamps_read(v.data(), blocks), "stem_stamps_read");
+    return v;
+  });
   m.def("wgrad3_stamps_enable", [](int on) { check(damd::wgrad3_stamps_enable(on), "wgrad3_stamps_enable"); });
   m.def("wgrad3_stamps_read", [](int blocks) {
     std::vector<unsigned long long> v((size_t)blocks * 4);

@@ -149,6 +149,11 @@ for s in ${STAGES:-xtests bench}; do
     epi)  # epilogue operand prefetch: every conv / GEMM numerics test, then the A/B
       step epit 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gemm_gpu.py \
         tests/test_hip_ops_gpu.py tests/test_native_graph_gpu.py -k "not full_size and not side_stream" ;;
+    stemd)  # the direct stem forward: bitwise against the implicit GEMM, the stem tests
+      step stemd 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_conv_gemm_gpu.py \
+        -k "stem" ;;
+    stemp)
+      step stemp 200 python scripts/stem_probe.py 64 ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating

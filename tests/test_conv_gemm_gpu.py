@@ -341,6 +341,39 @@ def test_packed_tap_stem(H, n, h, cin, cout, k, padding):
     close(dw8[:, :k, :cin], gw, 1e-4, 2e-5)
 
 
+@pytest.mark.parametrize("n,relu,bias", [(2, False, False), (3, False, True)])
+def test_stem_direct_bitwise_equals_implicit_gemm(H, n, relu, bias, monkeypatch):
+    """The direct stem forward (conv_stem.hip: input rows staged once per 256-pixel tile,
+    A fragments read from them) == the implicit-GEMM packed-tap kernel (DAMD_STEM_DIRECT=0),
+    bitwise: output and the fixed-point BN statistics accumulator (same tiles, fragments,
+    MFMA order and replica assignment); the ResNet-18 stem shape (224 x 224, 7x7 / 2, 64
+    outputs) and the true KxK conv as the fp32 oracle."""
+    k, cout, h = 7, 64, 224
+    x = rb(rnd(n, h, h, 3, seed=81))
+    w = rb(rnd(k, k, 3, cout, scale=0.1, seed=82))
+    x4 = torch.zeros(n, h, h, 4, device=dev)
+    x4[..., :3] = x
+    wshape = (k, k, 4, cout)
+    w8 = torch.zeros(H.stem4_weight_shape(wshape), device=dev, dtype=torch.bfloat16)
+    w8[:, :k, :3] = w.bfloat16()
+    b = rnd(cout, seed=83) if bias else None
+    y = ref.conv2d(x, w, b, (2, 2), "same")
+    if relu:
+        y = torch.relu(y)
+    outs, accs = [], []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("DAMD_STEM_DIRECT", direct)
+        out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+        acc = H.acc_zeros(8, 2 * cout, dev)
+        H.conv_fwd_stem4(x4.bfloat16(), w8, out, k, (2, 2), "same", bias=b, relu=relu, stats=acc)
+        torch.cuda.synchronize()
+        outs.append(out)
+        accs.append(acc)
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(accs[0], accs[1])
+    close(outs[0], y, 1e-2, 4e-3)
+
+
 @pytest.mark.parametrize("splits,n", [(3, 1 << 16), (16, 3 << 14), (3, 4096), (40, 1 << 15)])
 def test_splitk_reduce_paths(H, splits, n):
     """dst += sum of the split slabs in split order: the flat kernel (<= 16 splits, large n)
