@@ -154,6 +154,18 @@ for s in ${STAGES:-xtests bench}; do
         -k "stem" ;;
     stemp)
       step stemp 200 python scripts/stem_probe.py 64 ;;
+    bnsw)  # BN knobs after the finalize rework: replicas, backward-reduce grid, apply grid cap
+      for cfg in "8 512 768" "4 512 768" "16 512 768" "8 1024 768" "8 256 768" "8 512 1536" "8 512 384" "8 512 768"; do
+        set -- $cfg
+        DAMD_BN_REPS=$1 DAMD_BN_BWD_BLOCKS=$2 DAMD_BN_FIN_GRID=$3 step bnsw_$1_$2_$3 300 python bench.py --model resnet18 --steps 50 --warmup 10
+      done
+      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/bnsw_*.log ;;
+    mnistprof)  # MNIST: bench at the driver's flags + long, phase stamps, PMC issue mix
+      step mb_n1 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      step mb_n1b 200 python bench.py --gpus 1 --steps 20 --warmup 5
+      step mb_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200
+      step mstamps 200 python scripts/stamps.py 64
+      step mpmc 400 bash scripts/pmc_mnist.sh ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
