@@ -22,7 +22,11 @@ enum GemmBMode { B_NC = 0, B_KC = 1 };
 // E_BNRED: the GEMM produces the gradient of a BN -> ReLU output (backprop-input of the
 // conv that consumes it): the tile's BN-backward partials (sum of the ReLU-masked stored
 // gradient, and of it times xhat, from bnx / bnst) go to `stats` as E_STATS would
-enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32, E_SLAB = 64, E_BNRED = 128 };
+// E_FIXUP (conv_gemm.hip, split-K): every split stores its fp32 partial to slab z, the
+// tile's LAST-arriving split (per-tile ticket) sums slabs 0..S-1 in order and runs the
+// epilogue of the other flags itself -- no separate splitk_finish launch
+enum GemmEpi { E_BIAS = 1, E_RELU = 2, E_BF16 = 4, E_ATOMIC = 8, E_STATS = 16, E_ADD = 32, E_SLAB = 64, E_BNRED = 128,
+               E_FIXUP = 256 };
 
 struct GemmArgs {
   const void* A;       // bf16
@@ -51,6 +55,10 @@ struct GemmArgs {
   // N-tile 0 also store that BN -> ReLU output to bnin_y (for the conv's weight gradient).
   BNFin bnin;
   uint16_t* bnin_y;
+  // E_FIXUP: fp32 slabs [splits][M][N] and one arrival ticket per output tile (zero between
+  // launches: the reducing split resets its tile's)
+  float* slab;
+  unsigned* tickets;
 };
 
 // tile: 0 -> 128x128 tiles, 1 -> 256x64 tiles (N <= 64 layers)

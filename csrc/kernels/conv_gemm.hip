@@ -257,6 +257,61 @@ __global__ __launch_bounds__(NT, blocks_per_cu((BM + BN) * KB * 2 * STAGES)) voi
     }
   };
   kloop<STAGES, NQ>(nk, issue, compute);
+  if constexpr ((EPI & E_FIXUP) != 0) {
+    // split-K finished in this launch (cdna_hip_programming.md, in-launch split-K reduction):
+    // slab store -> drain -> agent release -> ticket; the split drawing S - 1 acquires, sums
+    // the S slabs at its lanes' own positions in split order (the order of splitk_finish:
+    // the same output bits) and runs the final epilogue.  Nothing waits on the ticket.
+    constexpr int EF = EPI & ~E_FIXUP;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn * 64 + j * 16 + 4 * (lane >> 4);
+        if (m < a.M && n < a.N)
+          *reinterpret_cast<f32x4*>(a.slab + ((size_t)blockIdx.z * a.M + m) * a.N + n) = acc[i][j];
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* last = reinterpret_cast<int*>(smem);  // (the staging stages are free; one LDS array)
+    const int tile_id = tm * tiles_n + tn;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old = __hip_atomic_fetch_add(a.tickets + tile_id, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last[0] = old == gridDim.z - 1;
+    }
+    __syncthreads();
+    if (!last[0]) return;
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.tickets + tile_id, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int S = gridDim.z;
+    for (int sp = 0; sp < S; ++sp) {
+      f32x4 v[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = min(m0 + wm * 64 + i * 16 + (lane & 15), a.M - 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = min(n0 + wn * 64 + j * 16 + 4 * (lane >> 4), a.N - 4);
+          v[i][j] = *reinterpret_cast<const f32x4*>(a.slab + ((size_t)sp * a.M + m) * a.N + n);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = sp == 0 ? v[i][j] : acc[i][j] + v[i][j];
+    }
+    __syncthreads();  // `red` aliases the staging stages (the ticket flag included)
+    tile::epilogue<BM, BN, EF>(a, acc, m0, n0, tm, wm, wn, wave, lane, reinterpret_cast<float*>(smem));
+    return;
+  }
   if constexpr ((EPI & E_STATS) != 0) __syncthreads();  // `red` aliases the staging stages
   if (sp) {
     // class-grid row (n, i2, j2) -> input pixel (n, 2 i2 + ra, 2 j2 + rb)
@@ -473,6 +528,15 @@ hipError_t launch_epi(const GemmArgs& a, int epi, int splits, int kb, hipStream_
     case E_BF16 | E_STATS: return launch_t<BM, BN, DG, E_BF16 | E_STATS>(a, splits, kb, s);
     case E_BIAS | E_BF16 | E_STATS: return launch_t<BM, BN, DG, E_BIAS | E_BF16 | E_STATS>(a, splits, kb, s);
     case E_BF16 | E_ADD: return launch_t<BM, BN, DG, E_BF16 | E_ADD>(a, splits, kb, s);
+    case E_FIXUP | E_BF16: return launch_t<BM, BN, DG, E_FIXUP | E_BF16>(a, splits, kb, s);
+    case E_FIXUP | E_BF16 | E_STATS: return launch_t<BM, BN, DG, E_FIXUP | E_BF16 | E_STATS>(a, splits, kb, s);
+    case E_FIXUP | E_BIAS | E_BF16: return launch_t<BM, BN, DG, E_FIXUP | E_BIAS | E_BF16>(a, splits, kb, s);
+    case E_FIXUP | E_BIAS | E_BF16 | E_STATS:
+      return launch_t<BM, BN, DG, E_FIXUP | E_BIAS | E_BF16 | E_STATS>(a, splits, kb, s);
+    case E_FIXUP | E_RELU | E_BF16: return launch_t<BM, BN, DG, E_FIXUP | E_RELU | E_BF16>(a, splits, kb, s);
+    case E_FIXUP | E_BIAS | E_RELU | E_BF16:
+      return launch_t<BM, BN, DG, E_FIXUP | E_BIAS | E_RELU | E_BF16>(a, splits, kb, s);
+    case E_FIXUP | E_BF16 | E_ADD: return launch_t<BM, BN, DG, E_FIXUP | E_BF16 | E_ADD>(a, splits, kb, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -553,6 +617,11 @@ hipError_t conv_gemm_launch(const GemmArgs& a, int amode, int epi, int splits, i
   }
   if (!dg && a.ldb % 8) return hipErrorInvalidValue;
   if ((epi & E_SLAB) && (epi & ~E_SLAB)) return hipErrorInvalidValue;
+  // E_FIXUP: a real K split over plain tiles (not the sub-pixel classes), slabs + tickets, a
+  // statistics accumulator (per-tile partial rows would not match the finish's row blocks)
+  if ((epi & E_FIXUP) && (splits < 2 || (dg && a.stride != 1) || !a.slab || !a.tickets || a.N % 4 ||
+                          ((epi & E_STATS) && !a.stats_acc) || (epi & (E_SLAB | E_ATOMIC | E_BNRED))))
+    return hipErrorInvalidValue;
   // the stem: input rows staged once per tile (conv_stem.hip; same tiles and bits)
   if (stem && stem_direct_ok(a, epi, splits)) return stem_direct_launch(a, epi, s);
   if (tile == 1)

@@ -38,8 +38,11 @@ void register_kernel_ops(py::module_& m) {
       [](int amode, int bmode, int epi, int splits, int tile, uintptr_t A, uintptr_t B, uintptr_t C, uintptr_t bias,
          uintptr_t stats, uintptr_t R, int M, int N, int K, int lda, int ldb, int ldc, std::vector<int> geo, int kc,
          int k_per_split, uintptr_t stream, int kstep, uintptr_t stats_acc, uintptr_t bnx, uintptr_t bnst,
-         int stats_reps, std::vector<uintptr_t> bnin_p, std::vector<float> bnin_v, uintptr_t bnin_y) {
+         int stats_reps, std::vector<uintptr_t> bnin_p, std::vector<float> bnin_v, uintptr_t bnin_y, uintptr_t slab,
+         uintptr_t tickets) {
         damd::GemmArgs a{};
+        a.slab = P_<float>(slab);
+        a.tickets = P_<unsigned>(tickets);
         if (!bnin_p.empty()) {  // BN on the input (A_CONV3 forward): [acc, gamma, beta, st, rmean, rvar]
           if (bnin_p.size() != 6 || bnin_v.size() != 4)
             throw std::invalid_argument("bnin: 6 pointers + [count, eps, momentum, reps]");
@@ -77,7 +80,7 @@ void register_kernel_ops(py::module_& m) {
       py::arg("lda"), py::arg("ldb"), py::arg("ldc"), py::arg("geo"), py::arg("kc"), py::arg("k_per_split"),
       py::arg("stream"), py::arg("kstep") = 0, py::arg("stats_acc") = 0, py::arg("bnx") = 0, py::arg("bnst") = 0,
       py::arg("stats_reps") = 1, py::arg("bnin_p") = std::vector<uintptr_t>{},
-      py::arg("bnin_v") = std::vector<float>{}, py::arg("bnin_y") = 0);
+      py::arg("bnin_v") = std::vector<float>{}, py::arg("bnin_y") = 0, py::arg("slab") = 0, py::arg("tickets") = 0);
   m.def("gemm_stats_tile_rows", &damd::gemm_stats_tile_rows);
   m.def("conv_gemm_kstep", &damd::conv_gemm_kstep);
   m.def("conv3_rows", &damd::conv3_rows);

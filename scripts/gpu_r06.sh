@@ -166,6 +166,14 @@ for s in ${STAGES:-xtests bench}; do
       step mb_long 200 python bench.py --gpus 1 --steps 2000 --warmup 200
       step mstamps 200 python scripts/stamps.py 64
       step mpmc 400 bash scripts/pmc_mnist.sh ;;
+    smoke)
+      step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    fixup)  # in-launch split-K finish: equivalence tests, then every conv / graph test
+      step fixt 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_conv_gemm_gpu.py -k "splitk" &&
+      step fixall 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv_gemm_gpu.py \
+        tests/test_native_graph_gpu.py tests/test_native_layers_gpu.py -k "not full_size and not side_stream" ;;
+    fixp)
+      step fixp 200 python scripts/fixup_probe.py ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating

@@ -8,6 +8,7 @@ no K split both accumulate the same 32-deep MFMA chunks in the same k order, so 
 difference is a staging / swizzle / padding bug, not rounding.  Shapes are ragged (M and
 N not multiples of the tiles, odd image sizes, zero padding on every side)."""
 import pytest
+import numpy as np
 import torch
 
 from distributed_amd.ops import reference as ref
@@ -339,6 +340,49 @@ def test_packed_tap_stem(H, n, h, cin, cout, k, padding):
     dw8 = torch.zeros(H.stem4_weight_shape(wshape), device=dev)
     H.conv_wgrad_stem4(x4.bfloat16(), dy.bfloat16(), dw8, k, (2, 2), padding)
     close(dw8[:, :k, :cin], gw, 1e-4, 2e-5)
+
+
+@pytest.mark.parametrize("shape", [(8, 7, 512, 512), (4, 7, 256, 256), (2, 7, 256, 128)])
+def test_splitk_in_launch_finish_matches_finish_kernel(H, shape, monkeypatch):
+    """Split-K conv GEMMs finished inside the launch (E_FIXUP: per-tile ticket, the last split
+    sums the slabs in split order and runs the epilogue) == the slab GEMM + splitk_finish
+    launch (DAMD_SPLITK_FIXUP=0): forward output and backprop-input (also accumulating onto
+    dx) bitwise; the BN statistics accumulator within fp32 rounding of the regrouped
+    partials; both against the fp32 reference.  Three launches each, so the self-resetting
+    tickets are exercised."""
+    n, h, cin, cout = shape
+    x = rb(rnd(n, h, h, cin, seed=91))
+    w = rb(rnd(3, 3, cin, cout, scale=0.05, seed=92))
+    plan = H.conv_fwd_plan(x.shape, w.shape, (1, 1), "same")
+    assert plan["splits"] > 1 and plan["amode"] == H.A_CONV64, plan
+    y = ref.conv2d(x, w, None, (1, 1), "same")
+    outs, accs = [], []
+    for fix in ("1", "0"):
+        monkeypatch.setenv("DAMD_SPLITK_FIXUP", fix)
+        for _ in range(3):
+            out = torch.empty(y.shape, device=dev, dtype=torch.bfloat16)
+            acc = H.acc_zeros(8, 2 * cout, dev)
+            H.conv_fwd(x.bfloat16(), w.bfloat16(), out, (1, 1), "same", stats=acc)
+        torch.cuda.synchronize()
+        outs.append(out)
+        accs.append(H.bn_acc_decode(acc))
+    assert torch.equal(outs[0], outs[1])
+    close(outs[0], y, 1e-2, 4e-3)
+    np.testing.assert_allclose(accs[0].numpy(), accs[1].numpy(), rtol=1e-5, atol=1e-2)
+    dplan = H.conv_dgrad_plan(x.shape, w.shape, (1, 1), "same")
+    dy = rb(rnd(*y.shape, seed=93))
+    base = rb(rnd(*x.shape, seed=94)).bfloat16()
+    for accumulate in (False, True):
+        res = []
+        for fix in ("1", "0"):
+            monkeypatch.setenv("DAMD_SPLITK_FIXUP", fix)
+            for _ in range(3):
+                dx = base.clone()
+                H.conv_dgrad(dy.bfloat16(), w.bfloat16(), dx, (1, 1), "same", accumulate=accumulate)
+            torch.cuda.synchronize()
+            res.append(dx)
+        if dplan["splits"] > 1:
+            assert torch.equal(res[0], res[1]), accumulate
 
 
 @pytest.mark.parametrize("n,relu,bias", [(2, False, False), (3, False, True)])
