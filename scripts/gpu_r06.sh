@@ -174,6 +174,17 @@ for s in ${STAGES:-xtests bench}; do
         tests/test_native_graph_gpu.py tests/test_native_layers_gpu.py -k "not full_size and not side_stream" ;;
     fixp)
       step fixp 200 python scripts/fixup_probe.py ;;
+    rehx)  # N = 2 sharing the GPU: auto twice, peer pinned, sharded pinned
+      for v in auto1 xgmi auto2 sharded; do
+        DAMD_ALLREDUCE=${v%[12]} DAMD_COMM=gloo step rehx_$v 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 200 --warmup 20
+      done ;;
+    rehab)  # N = 2 sharing the GPU, peer pinned: build/ab/A against the working tree, alternating
+      for i in 1 2; do
+        DAMD_ALLREDUCE=xgmi DAMD_COMM=gloo step rehab_A$i 400 bash -c "cd build/ab/A && python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29621 bench.py --gpus 2 --steps 200 --warmup 20"
+        DAMD_ALLREDUCE=xgmi DAMD_COMM=gloo step rehab_B$i 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+          --master-addr 127.0.0.1 --master-port 29622 bench.py --gpus 2 --steps 200 --warmup 20
+      done ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
