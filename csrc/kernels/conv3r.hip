@@ -21,10 +21,11 @@
 // sit in front of a halo wait (in-order vmcnt: the round-4 persistent attempt serialised
 // the next halo behind the stores).
 // Synchronisation is the workgroup barrier only (no flag polling): per tile A (rows of
-// this tile landed; the previous tile's taps done, so its exclusive rows are free), B
-// (BatchNorm-input transform of the new rows done; forward with bnin only) and the
-// epilogue's statistics barrier -- every wave, loader included, passes each one the same
-// number of times (trip counts depend on blockIdx only).
+// this tile landed -- and, forward with a BN input, transformed to relu(BN(x)) by the loader
+// that fetched them, while the compute waves ran the previous tile's taps; the previous
+// tile's taps done, so its exclusive rows are free) and the epilogue's statistics barrier
+// -- every wave, loader included, passes each one the same number of times (trip counts
+// depend on blockIdx only).
 //
 // Tiles are the 4-row tiles of conv3x3.hip (tile index img * tpi + row block), so the
 // statistics partial rows (GemmArgs::stats, stats_T = n * tpi) and the epilogue are shared
@@ -147,13 +148,17 @@ __global__ __launch_bounds__(RNT, 1) void conv3r_kernel(GemmArgs a, int tpi, int
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   bar();
 
-  // BN input: y = bf16(relu(x * scale + shift)) in place over in-image pixels of rows
-  // [lo, hi] (the padding stays zero: it is y's padding), exactly bn_apply's arithmetic
-  auto transform_rows = [&](int lo, int hi) __attribute__((always_inline)) {
+  // BN input: y = bf16(relu(x * scale + shift)) in place over the in-image pixels of rows
+  // [lo, hi] (the padding stays zero: it is y's padding), exactly bn_apply's arithmetic, by
+  // threads tid0, tid0 + nth, ...; the transformed 16-byte units of rows inside this strip's
+  // output rows [ylo, yhi) also go to y (the BN -> ReLU output, for the conv's weight
+  // gradient): every y row is stored once, by the block and at the moment it is transformed
+  const int ylo = tk0 * RR, yhi = min(tk1 * RR, H);
+  auto transform_rows = [&](int lo, int hi, int tid0, int nth) __attribute__((always_inline)) {
     lo = max(lo, 0);
     hi = min(hi, H - 1);
     const int units = (hi - lo + 1) * W * 8;
-    for (int u = t; u < units; u += 256) {
+    for (int u = tid0; u < units; u += nth) {
       const int sl = u & 7, px = u >> 3;
       const int r = lo + px / W, c = px - (px / W) * W;
       const int q = c + 1;  // pixel within the slot
@@ -169,14 +174,22 @@ __global__ __launch_bounds__(RNT, 1) void conv3r_kernel(GemmArgs a, int tpi, int
             fmaxf(fmaf(__uint_as_float(w[k] & 0xffff0000u), sft[ch + 2 * k + 1], sft[64 + ch + 2 * k + 1]), 0.f);
         o[k] = (uint32_t)f2bf(lo_) | ((uint32_t)f2bf(hi_) << 16);
       }
-      *reinterpret_cast<uint4*>(p) = uint4{o[0], o[1], o[2], o[3]};
+      const uint4 y = uint4{o[0], o[1], o[2], o[3]};
+      *reinterpret_cast<uint4*>(p) = y;
+      if (a.bnin_y && r >= ylo && r < yhi)
+        *reinterpret_cast<uint4*>(a.bnin_y + ((long)(img * H + r) * W + c) * 64 + ch) = y;
     }
   };
+  // the strip's first tile: its six rows landed in the prologue; every wave transforms
+  if (bnin) {
+    transform_rows(tk0 * RR - 1, tk0 * RR + tile_rows(tk0), t, RNT);
+    bar();
+  }
 
   for (int k = tk0; k < tk1; ++k) {
     const int rk = tile_rows(k), row0 = k * RR;
-    // A(k): this tile's rows have landed (the loader waited for them before this barrier),
-    // and every compute wave has finished the previous tile's taps
+    // A(k): this tile's rows have landed and are transformed (the loaders did both before
+    // this barrier), and every compute wave has finished the previous tile's taps
     bar();
     if (loader) {
       // the next tile's new halo rows (row0 + rk + 1 .. ) into the slots the previous tile
@@ -189,27 +202,17 @@ __global__ __launch_bounds__(RNT, 1) void conv3r_kernel(GemmArgs a, int tpi, int
           if ((ir & 3) == ldr)
 #pragma unroll
             for (int j = 0; j < 8; ++j) row_piece(ir, j);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's rows landed
+        // BN input: the loader that fetched a row transforms it (and stores its y) while the
+        // compute waves run this tile's taps -- they no longer stop for a transform pass and
+        // a second barrier per tile
+        if (bnin)
+          for (int ir = nlo; ir <= nhi; ++ir)
+            if ((ir & 3) == ldr) transform_rows(ir, ir, lane, 64);
       }
-      if (bnin) bar();                                       // B(k)
       if constexpr ((EPI & (E_STATS | E_BNRED)) != 0) __syncthreads();  // the epilogue's barrier
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // landed before A(k + 1)
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // landed + transformed before A(k + 1)
       continue;
-    }
-    if (bnin) {
-      // the rows that landed for this tile (all six for the strip's first tile)
-      transform_rows(k == tk0 ? row0 - 1 : row0 + 1, row0 + rk);
-      bar();  // B(k)
-      // y (the BN -> ReLU output) of this tile's output rows, for the conv's weight gradient
-      if (a.bnin_y) {
-        const int units = rk * W * 8;
-        uint16_t* yb = a.bnin_y + (long)(img * H + row0) * W * 64;
-        for (int u = t; u < units; u += 256) {
-          const int cl = u & 7, px = u >> 3;
-          const int r = px / W, c = px - r * W, q = c + 1;
-          *reinterpret_cast<uint4*>(yb + (long)px * 64 + 8 * cl) = *reinterpret_cast<const uint4*>(
-              ring + slot_of(row0 + r) * SLOT_B + q * 128 + 16 * (cl ^ (q & 7)));
-        }
-      }
     }
     const int npx = rk * W;
     // groups of 16 output pixels this wave owns (wave-uniform; all-invalid groups skipped)
