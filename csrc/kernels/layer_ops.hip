@@ -344,9 +344,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply_rows_k(const uint16_t* __rest
   }
 }
 
-// dz = dy * [y>0]; partial sums of dz and dz*xhat per channel for a contiguous row range
+// dz = dy * [y>0]; partial sums of dz and dz*xhat per channel for a contiguous row range.
+// MODE = relu_mask (0 none, 1 mask from the stored y, 2 recomputed from x): a template
+// argument, so the loads of RU rows (dy, x, y) are issued together before the first use --
+// with the mask source behind a runtime branch and the dz stores (which may alias the next
+// rows' loads) between rows, every row cost its own two memory round trips.  Rows are
+// still accumulated in ascending order: the partials are bitwise those of the row loop.
+constexpr int RED_RU = 4;
+template <int MODE>
 __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y,
-                                                      int relu_mask, const uint16_t* __restrict__ x,
+                                                      const uint16_t* __restrict__ x,
                                                       const float* __restrict__ st, uint16_t* __restrict__ dz_out,
                                                       float* __restrict__ part, long M, int C, long rows_per_block,
                                                       long long* __restrict__ acc, int reps, int rev) {
@@ -363,31 +370,44 @@ __global__ __launch_bounds__(NT) void bn_bwd_reduce_k(const uint16_t* __restrict
   for (int e = 0; e < 8; ++e) s0[e] = s1[e] = 0.f;
   ld8f(st + c, mean);
   ld8f(st + C + c, inv);
-  if (relu_mask == 2) {
+  if (MODE == 2) {
     ld8f(st + 2 * C + c, sc);
     ld8f(st + 3 * C + c, sh);
   }
   const long r0 = blk * rows_per_block, r1 = min(M, r0 + rows_per_block);
   if (rr < rpi) {
-    for (long row = r0 + rr; row < r1; row += rpi) {
-      const long off = (row * C + c) / 8;
-      float d[8], xv[8];
-      unpack8(reinterpret_cast<const uint4*>(dy)[off], d);
-      unpack8(reinterpret_cast<const uint4*>(x)[off], xv);
-      if (relu_mask) {
-        float yv[8];
-        if (relu_mask == 2)
-          bn_relu8(xv, sc, sh, yv);
-        else
-          unpack8(reinterpret_cast<const uint4*>(y)[off], yv);
+    for (long row = r0 + rr; row < r1; row += (long)RED_RU * rpi) {
+      uint4 dq[RED_RU], xq[RED_RU], yq[RED_RU];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
-        if (dz_out) reinterpret_cast<uint4*>(dz_out)[off] = pack8(d);
+      for (int u = 0; u < RED_RU; ++u) {
+        const long off = (min(row + u * rpi, r1 - 1) * C + c) / 8;
+        dq[u] = reinterpret_cast<const uint4*>(dy)[off];
+        xq[u] = reinterpret_cast<const uint4*>(x)[off];
+        if (MODE == 1) yq[u] = reinterpret_cast<const uint4*>(y)[off];
       }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s0[e] += d[e];
-        s1[e] += d[e] * (xv[e] - mean[e]) * inv[e];
+      for (int u = 0; u < RED_RU; ++u) {
+        const long rw = row + u * rpi;
+        if (rw >= r1) break;
+        const long off = (rw * C + c) / 8;
+        float d[8], xv[8];
+        unpack8(dq[u], d);
+        unpack8(xq[u], xv);
+        if (MODE) {
+          float yv[8];
+          if (MODE == 2)
+            bn_relu8(xv, sc, sh, yv);
+          else
+            unpack8(yq[u], yv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] = yv[e] > 0.f ? d[e] : 0.f;
+          if (dz_out) reinterpret_cast<uint4*>(dz_out)[off] = pack8(d);
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s0[e] += d[e];
+          s1[e] += d[e] * (xv[e] - mean[e]) * inv[e];
+        }
       }
     }
   }
@@ -1936,8 +1956,10 @@ hipError_t bn_bwd_reduce(const uint16_t* dy, const uint16_t* y, int relu_mask, c
                          int acc_reps) {
   if (C % 8 || C / 8 > NT || (!part && !acc) || acc_reps < 1) return hipErrorInvalidValue;
   const long rows = (M + T - 1) / T;
-  hipLaunchKernelGGL(bn_bwd_reduce_k, dim3(T), dim3(NT), 0, s, dy, y, relu_mask, x, st, dz_out, part, M, C, rows,
-                     acc, acc_reps, g_bn_reduce_reverse ? 1 : 0);
+  if (relu_mask < 0 || relu_mask > 2) return hipErrorInvalidValue;
+  auto k = relu_mask == 0 ? bn_bwd_reduce_k<0> : relu_mask == 1 ? bn_bwd_reduce_k<1> : bn_bwd_reduce_k<2>;
+  hipLaunchKernelGGL(k, dim3(T), dim3(NT), 0, s, dy, y, x, st, dz_out, part, M, C, rows, acc, acc_reps,
+                     g_bn_reduce_reverse ? 1 : 0);
   return hipGetLastError();
 }
 
