@@ -185,6 +185,9 @@ for s in ${STAGES:-xtests bench}; do
         DAMD_ALLREDUCE=xgmi DAMD_COMM=gloo step rehab_B$i 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
           --master-addr 127.0.0.1 --master-port 29622 bench.py --gpus 2 --steps 200 --warmup 20
       done ;;
+    bnall)  # every BN kernel test + the native-graph BN / dual / bitwise tests
+      step bnall 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_hip_ops_gpu.py \
+        tests/test_native_graph_gpu.py tests/test_conv_gemm_gpu.py -k "bn or dual or bitwise or stem or emulated or one_step" ;;
     wstest)  # weight gradients on a side stream: bitwise against the single-stream step
       step wstest 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_native_graph_gpu.py -k side_stream ;;
     wsab)  # ResNet-18 step, weight-gradient side stream off / on / on for >= 128 outputs, alternating
