@@ -256,6 +256,14 @@ def test_small_resnet_step_matches_bf16_emulated_reference():
 
 
 def test_small_resnet_one_step_matches_fp32_reference():
+    """One native step vs a pure fp32 CPU step of the same small ResNet: a SANITY bound,
+    deliberately loose for BatchNorm gamma / beta (cos > 0.75, rel < 0.7).  The native step
+    stores activations and their gradients in bf16; x-hat amplifies that rounding by
+    |mean| / std and the BN backward's cancellation amplifies it again, so BN parameter
+    updates drift from fp32 by design (16-draw sweep worst: cos 0.846, rel 0.541).  The
+    real numerical checks are the per-op fp32 oracles (test_hip_ops_gpu.py, BN forward /
+    backward) and the pinned-seed bf16-EMULATED reference, which rounds at the same storage
+    points and is compared tightly (test_small_resnet_step_matches_bf16_emulated_reference)."""
     tf.keras.backend.clear_session()
     x, y = _data(64, (32, 32, 3), 10)
     m0 = _small_resnet()
