@@ -1451,14 +1451,28 @@ __global__ __launch_bounds__(NT) void colsum_fin_k(const float* slab, int splits
 // gradient and no loss / metric contribution.  With ctrl != nullptr the gradient scale is
 // 1 / (rows of this global batch that exist): Keras' SUM_OVER_BATCH_SIZE on the real
 // final batch; benchmark wrap mode (ctrl->wrap > 0) always has full batches.
+// One block per row; the row is read from memory once (up to 4 values per thread held in
+// registers) and reduced by wave shuffles plus one LDS exchange per quantity.  The first
+// version re-read the row for the max, the exponent sum and the output, and reduced each
+// by an 8-level LDS tree (17 barriers per row, 30 more in the last block): 9.8 us for the
+// ResNet-18 head (64 x 1000) -- the 1000-class logits of 64 rows.
+constexpr int SX_KPT = 4, SX_NW = NT / 64;
+__device__ __forceinline__ void sx_better(float& v, int& i, float ov, int oi) {
+  if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }  // max, ties -> smallest index
+}
+__device__ __forceinline__ float sx_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
 __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ logits, int ld,
                                                      const int32_t* __restrict__ labels, int K, float scale,
                                                      const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ dl,
                                                      float* tail, float* rows) {
-  __shared__ float sv[NT];
-  __shared__ int si[NT];
+  __shared__ float wmax[SX_NW], wsum[SX_NW], wtail[3][SX_NW];
+  __shared__ int widx[SX_NW];
   __shared__ int last;
-  const int b = blockIdx.x, t = threadIdx.x, B = gridDim.x;
+  const int b = blockIdx.x, t = threadIdx.x, B = gridDim.x, lane = t & 63, w = t >> 6;
   const int y = labels[b];
   float row_loss = 0.f, row_corr = 0.f;
   if (y < 0) {
@@ -1470,46 +1484,65 @@ __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ l
       scale = 1.f / (float)(ctrl->wrap > 0 ? gb : max(1, min(gb, left)));
     }
     const float* z = logits + (size_t)b * ld;
+    const bool reg = K <= SX_KPT * NT;  // the row fits the registers
+    float zr[SX_KPT];
     float mx = -INFINITY;
     int mi = 0x7fffffff;
-    for (int k = t; k < K; k += NT) {
-      const float v = z[k];
-      if (v > mx) { mx = v; mi = k; }
-    }
-    sv[t] = mx;
-    si[t] = mi;
-    __syncthreads();
-    for (int s = NT / 2; s > 0; s >>= 1) {
-      if (t < s) {
-        const float o = sv[t + s];
-        const int oi = si[t + s];
-        if (o > sv[t] || (o == sv[t] && oi < si[t])) { sv[t] = o; si[t] = oi; }
+    if (reg) {
+#pragma unroll
+      for (int i = 0; i < SX_KPT; ++i) zr[i] = t + i * NT < K ? z[t + i * NT] : -INFINITY;
+#pragma unroll
+      for (int i = 0; i < SX_KPT; ++i)
+        if (t + i * NT < K && zr[i] > mx) { mx = zr[i]; mi = t + i * NT; }
+    } else {
+      for (int k = t; k < K; k += NT) {
+        const float v = z[k];
+        if (v > mx) { mx = v; mi = k; }
       }
-      __syncthreads();
     }
-    const float zmax = sv[0];
-    const int amax = si[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sx_better(mx, mi, __shfl_xor(mx, o), __shfl_xor(mi, o));
+    if (lane == 0) { wmax[w] = mx; widx[w] = mi; }
     __syncthreads();
+    float zmax = wmax[0];
+    int amax = widx[0];
+#pragma unroll
+    for (int v = 1; v < SX_NW; ++v) sx_better(zmax, amax, wmax[v], widx[v]);
     float se = 0.f;
-    for (int k = t; k < K; k += NT) se += __expf(z[k] - zmax);
-    sv[t] = se;
-    __syncthreads();
-    for (int s = NT / 2; s > 0; s >>= 1) {
-      if (t < s) sv[t] += sv[t + s];
-      __syncthreads();
+    if (reg) {
+#pragma unroll
+      for (int i = 0; i < SX_KPT; ++i) {
+        zr[i] = t + i * NT < K ? __expf(zr[i] - zmax) : 0.f;
+        se += zr[i];
+      }
+    } else {
+      for (int k = t; k < K; k += NT) se += __expf(z[k] - zmax);
     }
-    const float sum = sv[0];
+    se = sx_wave_sum(se);
+    if (lane == 0) wsum[w] = se;
+    __syncthreads();
+    float sum = wsum[0];
+#pragma unroll
+    for (int v = 1; v < SX_NW; ++v) sum += wsum[v];
     const float inv = 1.f / sum;
-    for (int k = t; k < K; k += NT) {
-      const float p = __expf(z[k] - zmax) * inv;
-      dl[(size_t)b * ld + k] = f2bf((p - (k == y ? 1.f : 0.f)) * scale);
+    if (reg) {
+#pragma unroll
+      for (int i = 0; i < SX_KPT; ++i) {
+        const int k = t + i * NT;
+        if (k < K) dl[(size_t)b * ld + k] = f2bf((zr[i] * inv - (k == y ? 1.f : 0.f)) * scale);
+      }
+    } else {
+      for (int k = t; k < K; k += NT) {
+        const float p = __expf(z[k] - zmax) * inv;
+        dl[(size_t)b * ld + k] = f2bf((p - (k == y ? 1.f : 0.f)) * scale);
+      }
     }
     row_loss = logf(sum) + zmax - z[y];
     row_corr = amax == y ? 1.f : 0.f;
   }
   // the batch sums in a fixed order (no float atomics: replays and graph / eager runs give
   // the same bits): every row stores (loss, correct, valid), the last block to arrive adds
-  // them up by a fixed tree and re-arms the arrival counter rows[3 B]
+  // them up (fixed shuffle tree + fixed wave order) and re-arms the arrival counter rows[3 B]
   if (t == 0) {
     rows[3 * b] = row_loss;
     rows[3 * b + 1] = row_corr;
@@ -1523,14 +1556,15 @@ __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ l
     for (int q = 0; q < 3; ++q) a[q] += rows[3 * r + q];
 #pragma unroll
   for (int q = 0; q < 3; ++q) {
-    __syncthreads();
-    sv[t] = a[q];
-    __syncthreads();
-    for (int s = NT / 2; s > 0; s >>= 1) {
-      if (t < s) sv[t] += sv[t + s];
-      __syncthreads();
-    }
-    if (t == 0) tail[q] += sv[0];
+    a[q] = sx_wave_sum(a[q]);
+    if (lane == 0) wtail[q][w] = a[q];
+  }
+  __syncthreads();
+  if (t < 3) {
+    float v = wtail[t][0];
+#pragma unroll
+    for (int u = 1; u < SX_NW; ++u) v += wtail[t][u];
+    tail[t] += v;
   }
   if (t == 0) *counter = 0;
 }

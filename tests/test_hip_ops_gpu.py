@@ -304,6 +304,34 @@ def test_dense_split_k(H, M, K, N, out_bf16):
     close(dx, 2 * (dy @ w.t()), 1e-2, 8e-3)
 
 
+@pytest.mark.parametrize("B,K,ld", [(64, 1000, 1024), (7, 1024, 1024), (3, 1500, 1504), (4, 300, 300)])
+def test_softmax_xent_wide_rows(H, B, K, ld):
+    """softmax_xent_k at the ResNet-18 head's width (64 x 1000) and around its register
+    path's limit (4 x 256 values per row; 1500 takes the re-reading loop): gradient, loss,
+    accuracy and count against the fp32 reference, ties of the max resolved to the smallest
+    index as the reference's argmax does, and two runs bitwise equal."""
+    z = rnd(B, ld, seed=31)
+    z[0, 5] = z[0, 9] = z[0, :K].max() + 1.0  # a tie for the max: class 5 wins
+    lab = torch.randint(0, K, (B,), device=dev, dtype=torch.int32)
+    lab[0] = 5
+    dl = torch.zeros(B, ld, device=dev, dtype=torch.bfloat16)
+    tail = torch.zeros(3, device=dev)
+    H.softmax_xent(z, lab, K, 1.0 / B, dl, tail)
+    zz = z[:, :K].clone().requires_grad_(True)
+    loss = ref.sparse_softmax_xent(zz, lab)
+    (gz,) = torch.autograd.grad(loss.sum() / B, (zz,))
+    close(dl[:, :K], gz, 1e-2, 4e-3)
+    assert ld == K or dl[:, K:].abs().max().item() == 0
+    close(tail[0], loss.sum(), 1e-5, 1e-6)
+    assert tail[1].item() == ref.sparse_accuracy(z[:, :K], lab).sum().item()
+    assert tail[1].item() >= 1  # row 0: the tie resolved to its label
+    assert tail[2].item() == B
+    dl2 = torch.zeros_like(dl)
+    tail2 = torch.zeros(3, device=dev)
+    H.softmax_xent(z, lab, K, 1.0 / B, dl2, tail2)
+    assert torch.equal(dl, dl2) and torch.equal(tail, tail2)
+
+
 @pytest.mark.parametrize("n,hw,c,f32", [(64, 7, 512, True), (5, 7, 2048, False), (3, 2, 64, False), (2, 14, 8, True)])
 def test_gap_fwd_paths(H, n, hw, c, f32):
     """Global average pool: per-image split kernel (C/8 <= 128, HW >= 8) and the
