@@ -94,6 +94,9 @@ int gemm_stats_tile_rows(int tile);
 // dst[i] (+)= sum_{s < splits} slab[s * n + i]  (fp32, n % 4 == 0, fixed summation order);
 // accumulate = 0 overwrites dst (no zeroing pass before a first writer)
 hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipStream_t s, int accumulate = 1);
+// splitk_reduce from a padded [R][C1p][C2p] slab layout into dst [R][C1][C2] (junk dropped)
+hipError_t splitk_reduce_unpad(const float* slab, int splits, int R, int C1, int C2, int C1p, int C2p, float* dst,
+                               hipStream_t s, int accumulate);
 // bf16 split-K epilogue: out = relu?(sum_s slab[s] + bias + R) (R bf16 [M][ldc], may alias
 // out); stats (optional) = per-column sum / sumsq of the stored pre-ReLU values per block
 // of rows_per_block rows: [ceil(M / rows_per_block)][2][N]

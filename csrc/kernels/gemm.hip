@@ -500,8 +500,13 @@ hipError_t launch_tile(const GemmArgs& a, int epi, int splits, int tile, hipStre
 // in fixed order (deterministic), so even a 9k-float4 gradient with 170 splits keeps
 // ~600 blocks streaming the slabs.
 constexpr int RED_E = 16, RED_G = NT / RED_E;
+// Unpad mode (c1p > 0): the slab rows are a padded [R][c1p][c2p4] float4 layout whose
+// entries with c1 >= u_c1 or c2 >= u_c24 are junk; the rest land at [R][u_c1][u_c24] in dst
+// (the packed-tap stem's weight gradient straight into the gradient buffer: no unpad_add
+// launch after the reduce).
 __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__ slab, int splits, long n4,
-                                                     float4* __restrict__ dst, int accumulate) {
+                                                     float4* __restrict__ dst, int accumulate, int u_c1 = 0,
+                                                     int u_c24 = 0, int u_c1p = 0, int u_c2p4 = 0) {
   __shared__ float4 part[RED_G][RED_E];
   const int e = threadIdx.x % RED_E, g = threadIdx.x / RED_E;
   const long i = blockIdx.x * (long)RED_E + e;
@@ -515,7 +520,15 @@ __global__ __launch_bounds__(NT) void splitk_reduce_k(const float4* __restrict__
   }
   part[g][e] = acc;
   __syncthreads();
-  if (g == 0 && i < n4) {
+  long di = i;
+  if (u_c1p > 0) {
+    const int c2 = (int)(i % u_c2p4);
+    const long t = i / u_c2p4;
+    const int c1 = (int)(t % u_c1p);
+    di = c1 < u_c1 && c2 < u_c24 ? (t / u_c1p * u_c1 + c1) * u_c24 + c2 : -1;
+  }
+  if (g == 0 && i < n4 && di >= 0) {
+    const long i = di;
     float4 d = accumulate ? dst[i] : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < RED_G; ++q) {
@@ -711,7 +724,17 @@ hipError_t splitk_reduce(const float* slab, int splits, long n, float* dst, hipS
   }
   const long g = (n4 + RED_E - 1) / RED_E;
   hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab),
-                     splits, n4, reinterpret_cast<float4*>(dst), accumulate);
+                     splits, n4, reinterpret_cast<float4*>(dst), accumulate, 0, 0, 0, 0);
+  return hipGetLastError();
+}
+
+hipError_t splitk_reduce_unpad(const float* slab, int splits, int R, int C1, int C2, int C1p, int C2p, float* dst,
+                               hipStream_t s, int accumulate) {
+  if (splits < 1 || R < 1 || C2 % 4 || C2p % 4 || C1 > C1p || C2 > C2p || C1 < 1 || C2 < 4) return hipErrorInvalidValue;
+  const long n4 = (long)R * C1p * (C2p / 4);
+  const long g = (n4 + RED_E - 1) / RED_E;
+  hipLaunchKernelGGL(splitk_reduce_k, dim3((unsigned)g), dim3(NT), 0, s, reinterpret_cast<const float4*>(slab),
+                     splits, n4, reinterpret_cast<float4*>(dst), accumulate, C1, C2 / 4, C1p, C2p / 4);
   return hipGetLastError();
 }
 

@@ -122,6 +122,12 @@ void register_kernel_ops(py::module_& m) {
     check(damd::splitk_reduce(P_<const float>(slab), splits, n, P_<float>(dst), P_<ihipStream_t>(stream), accumulate),
           "splitk_reduce");
   }, py::arg("slab"), py::arg("splits"), py::arg("n"), py::arg("dst"), py::arg("stream"), py::arg("accumulate") = 1);
+  m.def("splitk_reduce_unpad", [](uintptr_t slab, int splits, int R, int C1, int C2, int C1p, int C2p, uintptr_t dst,
+                                  uintptr_t stream, int accumulate) {
+    check(damd::splitk_reduce_unpad(P_<const float>(slab), splits, R, C1, C2, C1p, C2p, P_<float>(dst),
+                                    P_<ihipStream_t>(stream), accumulate),
+          "splitk_reduce_unpad");
+  });
 
   using U = uintptr_t;
   using u16 = uint16_t;

@@ -1201,8 +1201,11 @@ class NativeGraphEngine(Engine):
         if nd.attrs.get("stem4"):
             kh, kw, cin, cout = l.kernel.shape
             dwp = nd.attrs["dw_pad"]
-            H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=ws, accumulate=False)
-            H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
+            # split-K: the reduce adds straight into the gradient view (0 + sum, as
+            # unpad_add(reduce) did: the same bits); one split: the atomic GEMM into dw_pad
+            if not H.conv_wgrad_stem4(xt.buf, dy, dwp, kh, l.strides, l.padding, workspace=ws, accumulate=False,
+                                      dw=self.gviews[id(l.kernel)]):
+                H.unpad_add(dwp, kh, kw, cin * cout, 8, 4 * cout, self.gviews[id(l.kernel)])
         elif "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]
             H.conv_wgrad(xt.buf, dy, dwp, l.strides, l.padding, workspace=ws, accumulate=False)

@@ -521,9 +521,13 @@ def _check_stats(stats, plan, cout, who):
 
 
 def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
-                     workspace: Optional[torch.Tensor] = None, accumulate: bool = True):
+                     workspace: Optional[torch.Tensor] = None, accumulate: bool = True,
+                     dw: Optional[torch.Tensor] = None) -> bool:
     """Packed-tap stem weight gradient: dw8 [KH][8][4][Cout] (fp32) += the gradient in the
-    stem4_weight_shape layout (entries beyond the true kernel are junk to drop)."""
+    stem4_weight_shape layout (entries beyond the true kernel are junk to drop).  With
+    ``dw`` (the true [KH][KW][Cin][Cout] fp32 gradient) and a split-K plan, the split-K
+    reduce drops the junk and ADDS straight into ``dw`` (dw8 untouched; ``accumulate``
+    applies to dw8 only); returns True then, else False (the caller unpads dw8 itself)."""
     k = kernel_size
     cout = dw8.shape[-1]
     wshape = (k, k, 4, cout)
@@ -541,11 +545,20 @@ def conv_wgrad_stem4(x, dy, dw8, kernel_size, strides=(2, 2), padding="same",
             dw8.zero_()
         gemm(x, dy, dw8, amode=A_WGRAD64, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_ATOMIC, geo=geo,
              k_per_split=plan["kps"], tile=plan["tile"], kstep=plan["kstep"])
-        return
+        return False
     workspace = _workspace(workspace, plan["ws"], x.device)
     gemm(x, dy, workspace, amode=A_WGRAD64, bmode=B_NC, M=M, N=N, K=K, ldb=cout, ldc=N, epi=E_SLAB,
          splits=splits, k_per_split=plan["kps"], tile=plan["tile"], geo=geo, kstep=plan["kstep"])
+    if dw is not None:
+        _chk(dw, torch.float32, "dw")
+        ci = dw.shape[2] if dw.dim() == 4 else 0
+        if tuple(dw.shape) != (k, k, ci, cout) or not 1 <= ci <= 4:
+            raise ValueError(f"conv_wgrad_stem4: dw shape {tuple(dw.shape)} is not [{k}][{k}][<=4][{cout}]")
+        # the reduce's rows [KH][8][4 x Cout] -> [KH][KW][Cin x Cout]
+        _C().splitk_reduce_unpad(_ptr(workspace), splits, k, k, ci * cout, 8, 4 * cout, _ptr(dw), stream_handle(), 1)
+        return True
     _C().splitk_reduce(_ptr(workspace), splits, M * N, _ptr(dw8), stream_handle(), accumulate=int(accumulate))
+    return False
 
 
 # ---- direct 3x3 / stride-1 / pad-1 convolution (csrc/kernels/conv3x3.hip) ---------------

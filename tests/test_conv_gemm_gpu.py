@@ -342,6 +342,36 @@ def test_packed_tap_stem(H, n, h, cin, cout, k, padding):
     close(dw8[:, :k, :cin], gw, 1e-4, 2e-5)
 
 
+def test_packed_tap_stem_wgrad_reduces_into_true_layout(H):
+    """The stem's split-K weight gradient reduced straight into the true [7][7][3][64]
+    gradient (splitk_reduce_unpad: the junk taps / channel dropped in the reduce) == the
+    padded reduce + unpad: bitwise onto zeros (both 0 + the same fixed-order sum), within
+    rounding onto a non-zero buffer, and against the fp32 reference."""
+    n, h, cin, cout, k = 8, 64, 3, 64, 7
+    x = rb(rnd(n, h, h, cin, seed=74))
+    x4 = torch.zeros(n, h, h, 4, device=dev)
+    x4[..., :cin] = x
+    wshape = (k, k, 4, cout)
+    plan = H.conv_wgrad_plan(x4.shape, wshape, (2, 2), "same")
+    assert plan["splits"] > 1, plan
+    w = rb(rnd(k, k, cin, cout, scale=0.1, seed=75)).requires_grad_(True)
+    y = ref.conv2d(x, w, None, (2, 2), "same")
+    dy = rb(rnd(*y.shape, seed=76))
+    gw, = torch.autograd.grad(y, (w,), dy)
+    dw8 = torch.zeros(H.stem4_weight_shape(wshape), device=dev)
+    assert not H.conv_wgrad_stem4(x4.bfloat16(), dy.bfloat16(), dw8, k, (2, 2), "same", accumulate=False)
+    dw = torch.zeros(k, k, cin, cout, device=dev)
+    junk = torch.full(H.stem4_weight_shape(wshape), 7.0, device=dev)
+    assert H.conv_wgrad_stem4(x4.bfloat16(), dy.bfloat16(), junk, k, (2, 2), "same", accumulate=False, dw=dw)
+    assert torch.equal(dw, dw8[:, :k, :cin])
+    assert torch.equal(junk, torch.full_like(junk, 7.0))  # the padded buffer is not touched
+    close(dw, gw, 1e-4, 2e-5)
+    base = rnd(k, k, cin, cout, seed=77)
+    dwb = base.clone()
+    H.conv_wgrad_stem4(x4.bfloat16(), dy.bfloat16(), dw8, k, (2, 2), "same", accumulate=False, dw=dwb)
+    close(dwb, base + gw, 1e-4, 2e-5)
+
+
 @pytest.mark.parametrize("shape", [(8, 7, 512, 512), (4, 7, 256, 256), (2, 7, 256, 128)])
 def test_splitk_in_launch_finish_matches_finish_kernel(H, shape, monkeypatch):
     """Split-K conv GEMMs finished inside the launch (E_FIXUP: per-tile ticket, the last split
