@@ -170,9 +170,17 @@ hipError_t opt_step(float* P, const float* G, float* S0, float* S1, float* S2, u
 // [per][HW][Cp] zero-padded channels; labels int32.  zero / zero2 (optional): byte ranges
 // (16-byte aligned, multiples of 16 bytes) cleared in the same launch -- the step's
 // gradient buffer and BatchNorm statistics accumulators, so no memset launch precedes it.
+// A pad_cast (below) run inside gather_batch's launch: the step's first layer's padded bf16
+// weights refreshed without a launch of their own (src == nullptr: none).
+struct PadCastJob {
+  const float* src;
+  uint16_t* dst;
+  int R, C1, C2, C1p, C2p;
+};
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
                         int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, void* zero = nullptr,
-                        long zero_bytes = 0, void* zero2 = nullptr, long zero2_bytes = 0);
+                        long zero_bytes = 0, void* zero2 = nullptr, long zero2_bytes = 0,
+                        PadCastJob pc = PadCastJob{nullptr, nullptr, 0, 0, 0, 0, 0});
 // fp32 [R][C1][C2] -> bf16 [R][C1p][C2p] (zero padding)
 hipError_t pad_cast(const float* src, int R, int C1, int C2, int C1p, int C2p, uint16_t* dst, hipStream_t s);
 // dst fp32 [R][C1][C2] += src fp32 [R][C1p][C2p] (the un-padded part)

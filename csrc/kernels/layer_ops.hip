@@ -1653,9 +1653,33 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
                                                      const int32_t* __restrict__ labels, Ctrl* __restrict__ ctrl,
                                                      int per, int HW, int Cin, int Cp, uint16_t* __restrict__ xb,
                                                      int32_t* __restrict__ yb, uint4* __restrict__ zero, long nz16,
-                                                     uint4* __restrict__ zero2, long nz16b) {
+                                                     uint4* __restrict__ zero2, long nz16b, PadCastJob pc) {
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nz16; i += (long)gridDim.x * NT) zero[i] = uint4{0u, 0u, 0u, 0u};
   for (long i = blockIdx.x * (long)NT + threadIdx.x; i < nz16b; i += (long)gridDim.x * NT) zero2[i] = uint4{0u, 0u, 0u, 0u};
+  // a layer's padded bf16 weight copy, element for element as pad_cast_k: a thread's first
+  // element is loaded here and stored when the thread's gather work is done (the load's
+  // latency hides under it; loading and storing up front cost the launch ~2 us)
+  const long pc_total = pc.src ? (long)pc.R * pc.C1p * pc.C2p : 0;
+  const long gt = blockIdx.x * (long)NT + threadIdx.x;
+  auto pc_src = [&](long i) -> const float* {
+    const int c2 = (int)(i % pc.C2p);
+    const long t = i / pc.C2p;
+    const int c1 = (int)(t % pc.C1p), r = (int)(t / pc.C1p);
+    return c1 < pc.C1 && c2 < pc.C2 ? pc.src + ((long)r * pc.C1 + c1) * pc.C2 + c2 : nullptr;
+  };
+  float pcf = 0.f;
+  if (gt < pc_total) {
+    const float* p = pc_src(gt);
+    pcf = p ? *p : 0.f;
+  }
+  auto pc_finish = [&]() {
+    if (gt >= pc_total) return;
+    pc.dst[gt] = f2bf(pcf);
+    for (long i = gt + (long)gridDim.x * NT; i < pc_total; i += (long)gridDim.x * NT) {
+      const float* p = pc_src(i);
+      pc.dst[i] = p ? f2bf(*p) : (uint16_t)0;
+    }
+  };
   const long base = (long)ctrl->cursor * ctrl->global_batch + ctrl->row0;
   const int n = ctrl->nsamples;
   const bool wrap = ctrl->wrap > 0;  // benchmark mode: the epoch wraps, every row is real
@@ -1691,6 +1715,7 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
       reinterpret_cast<uint4*>(xb)[2 * i] = pack8(v);
       reinterpret_cast<uint4*>(xb)[2 * i + 1] = pack8(v + 8);
     }
+    pc_finish();
     return;
   }
   if (Cp == 4) {
@@ -1715,6 +1740,7 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
       }
       reinterpret_cast<uint4*>(xb)[i] = pack8(v);
     }
+    pc_finish();
     return;
   }
   // one thread per 8 (padded) channels of one pixel: one 16-byte store
@@ -1739,6 +1765,7 @@ __global__ __launch_bounds__(NT) void gather_batch_k(const void* __restrict__ x,
     reinterpret_cast<uint4*>(xb)[i] = pack8(v);
     if (p == 0 && c8 == 0) yb[r] = valid ? labels[row] : -1;
   }
+  pc_finish();
 }
 
 __global__ __launch_bounds__(NT) void pad_cast_k(const float* src, int R, int C1, int C2, int C1p, int C2p,
@@ -1864,7 +1891,9 @@ hipError_t sgd_step(float* P, const float* G, float* V, uint16_t* Pb, long n, Ct
 
 hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* labels, Ctrl* ctrl, int per,
                         int HW, int Cin, int Cp, uint16_t* xb, int32_t* yb, hipStream_t s, void* zero, long zero_bytes,
-                        void* zero2, long zero2_bytes) {
+                        void* zero2, long zero2_bytes, PadCastJob pc) {
+  if (pc.src && (!pc.dst || pc.R < 1 || pc.C1 < 1 || pc.C2 < 1 || pc.C1p < pc.C1 || pc.C2p < pc.C2))
+    return hipErrorInvalidValue;
   if (Cp % 8 && !(Cp == 4 && Cin <= 4 && HW % 2 == 0)) return hipErrorInvalidValue;
   for (int k = 0; k < 2; ++k) {
     const void* z = k ? zero2 : zero;
@@ -1874,7 +1903,7 @@ hipError_t gather_batch(const void* x, int x_u8, float scale, const int32_t* lab
   }
   hipLaunchKernelGGL(gather_batch_k, dim3(grid_for((long)per * HW * Cp / 8)), dim3(NT), 0, s, x, x_u8, scale, labels,
                      ctrl, per, HW, Cin, Cp, xb, yb, static_cast<uint4*>(zero), zero_bytes / 16,
-                     static_cast<uint4*>(zero2), zero2_bytes / 16);
+                     static_cast<uint4*>(zero2), zero2_bytes / 16, pc);
   return hipGetLastError();
 }
 

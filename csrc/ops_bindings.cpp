@@ -352,14 +352,21 @@ void register_kernel_ops(py::module_& m) {
      py::arg("ctrl"), py::arg("tail"), py::arg("kind"), py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("rho"),
      py::arg("mom"), py::arg("flag"), py::arg("s"), py::arg("book") = 1);
   m.def("gather_batch", [](U x, int x_u8, float scale, U labels, U ctrl, int per, int HW, int Cin, int Cp, U xb, U yb,
-                           U s, U zero, long zero_bytes, U zero2, long zero2_bytes) {
+                           U s, U zero, long zero_bytes, U zero2, long zero2_bytes, U pc_src, U pc_dst,
+                           std::vector<int> pc_dims) {
+    damd::PadCastJob pc{P_<const float>(pc_src), P_<u16>(pc_dst), 0, 0, 0, 0, 0};
+    if (pc_src) {
+      if (pc_dims.size() != 5) throw std::runtime_error("gather_batch: pc_dims = (R, C1, C2, C1p, C2p)");
+      pc.R = pc_dims[0], pc.C1 = pc_dims[1], pc.C2 = pc_dims[2], pc.C1p = pc_dims[3], pc.C2p = pc_dims[4];
+    }
     check(damd::gather_batch(P_<const void>(x), x_u8, scale, P_<const int32_t>(labels), P_<damd::Ctrl>(ctrl),
                              per, HW, Cin, Cp, P_<u16>(xb), P_<int32_t>(yb), P_<ihipStream_t>(s), P_<void>(zero),
-                             zero_bytes, P_<void>(zero2), zero2_bytes),
+                             zero_bytes, P_<void>(zero2), zero2_bytes, pc),
           "gather_batch");
   }, py::arg("x"), py::arg("x_u8"), py::arg("scale"), py::arg("labels"), py::arg("ctrl"), py::arg("per"),
      py::arg("HW"), py::arg("Cin"), py::arg("Cp"), py::arg("xb"), py::arg("yb"), py::arg("s"), py::arg("zero") = 0,
-     py::arg("zero_bytes") = 0, py::arg("zero2") = 0, py::arg("zero2_bytes") = 0);
+     py::arg("zero_bytes") = 0, py::arg("zero2") = 0, py::arg("zero2_bytes") = 0, py::arg("pc_src") = 0,
+     py::arg("pc_dst") = 0, py::arg("pc_dims") = std::vector<int>{});
   m.def("pad_cast", [](U src, int R, int C1, int C2, int C1p, int C2p, U dst, U s) {
     check(damd::pad_cast(P_<const float>(src), R, C1, C2, C1p, C2p, P_<u16>(dst), P_<ihipStream_t>(s)), "pad_cast");
   });

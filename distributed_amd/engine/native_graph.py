@@ -951,11 +951,18 @@ class NativeGraphEngine(Engine):
         # the step's first launch also clears the gradient buffer (and the BN statistics
         # accumulators): no memset launch in the step
         acc = self.bn_acc
+        live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
+        # the first padded conv's bf16 weight copy (the packed-tap stem) is refreshed inside
+        # the gather launch (no pad_cast launch of its own): nothing writes the masters
+        # between this launch and that conv
+        self._pad_folded = next((nd for nd in live if nd.kind == "Conv2D" and self._pad_job(nd) is not None), None)
+        job = self._pad_job(self._pad_folded) if self._pad_folded is not None else None
         C.gather_batch(self.x_ep.data_ptr(), int(self.feed.x_u8), 255.0, self.y_ep.data_ptr(), self.ctrl.data_ptr(),
                        B, h * w, c, self.cin_pad, self.x0.buf.data_ptr(), self.labels.data_ptr(), s,
                        zero=self.G.data_ptr(), zero_bytes=self.G.numel() * 4,
-                       zero2=acc.data_ptr() if acc is not None else 0, zero2_bytes=acc.numel() * 8 if acc is not None else 0)
-        live = [nd for nd in self.nodes if not nd.attrs.get("dead")]
+                       zero2=acc.data_ptr() if acc is not None else 0, zero2_bytes=acc.numel() * 8 if acc is not None else 0,
+                       pc_src=job[0].data_ptr() if job else 0, pc_dst=job[1].data_ptr() if job else 0,
+                       pc_dims=list(job[2:]) if job else [])
         for nd in live:
             getattr(self, "_fwd_" + nd.kind)(nd)
         H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:],
@@ -1007,7 +1014,7 @@ class NativeGraphEngine(Engine):
         wb = self._w(nd, l.kernel)
         bias = self.views[id(l.bias)] if l.use_bias else None
         relu = getattr(l.activation, "__name__", "linear") == "relu"
-        if not self._weights_static:
+        if not self._weights_static and nd is not getattr(self, "_pad_folded", None):
             self._pad_weights(nd)
         if nd.attrs.get("stem4"):
             kh = l.kernel.shape[0]
@@ -1027,6 +1034,18 @@ class NativeGraphEngine(Engine):
                            stats=nd.attrs.get("stats_buf"), workspace=self.gemm_ws)
         self._act_epilogue(nd)
 
+    def _pad_job(self, nd):
+        """(fp32 master view, padded bf16 copy, R, C1, C2, C1p, C2p) of a padded conv's
+        pad_cast, or None."""
+        if nd.kind != "Conv2D" or "w_pad" not in nd.attrs:
+            return None
+        kh, kw, cin, cout = nd.layer.kernel.shape
+        src, dst = self.views[id(nd.layer.kernel)], nd.attrs["w_pad"]
+        if nd.attrs.get("stem4"):
+            # [KH][KW][cin][cout] -> [KH][8][4][cout]: the (cin, cout) rows padded at their tail
+            return (src, dst, kh, kw, cin * cout, 8, 4 * cout)
+        return (src, dst, kh * kw, cin, cout, nd.attrs["cin_pad"], cout)
+
     def _pad_weights(self, nd):
         """Refresh a layer's padded bf16 weight copy from the fp32 masters (every training
         step; once per call for an inference plan, whose weights do not move)."""
@@ -1034,12 +1053,8 @@ class NativeGraphEngine(Engine):
         if "w_pad" not in nd.attrs:
             return
         if nd.kind == "Conv2D":
-            kh, kw, cin, cout = l.kernel.shape
-            if nd.attrs.get("stem4"):
-                # [KH][KW][cin][cout] -> [KH][8][4][cout]: the (cin, cout) rows padded at their tail
-                H.pad_cast(self.views[id(l.kernel)], kh, kw, cin * cout, 8, 4 * cout, nd.attrs["w_pad"])
-            else:
-                H.pad_cast(self.views[id(l.kernel)], kh * kw, cin, cout, nd.attrs["cin_pad"], cout, nd.attrs["w_pad"])
+            src, dst, *dims = self._pad_job(nd)
+            H.pad_cast(src, *dims, dst)
         elif nd.kind == "Dense":
             kin, units = l.kernel.shape
             H.pad_cast(self.views[id(l.kernel)], 1, kin, units, kin, nd.attrs["w_pad"].shape[1], nd.attrs["w_pad"])
