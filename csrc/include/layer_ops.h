@@ -138,8 +138,12 @@ hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, fl
 // dlogits shares the row pitch ld of the logits; its padding columns are left untouched.
 // rows: scratch of 3 B floats + one int arrival counter (zero before the first call; the
 // kernel re-arms it): the batch sums are formed in a fixed order, not by float atomics.
+// bias_grad (optional): += the column sums of the stored dlogits, exactly as colsum with one
+// split (the logits layer's bias gradient without a colsum launch)
 hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale,
-                        const Ctrl* ctrl, uint16_t* dlogits, float* tail, float* rows, hipStream_t s);
+                        const Ctrl* ctrl, uint16_t* dlogits, float* tail, float* rows, hipStream_t s,
+                        float* bias_grad = nullptr);
+int colsum_splits(int M, int N);
 
 // Optimizer ---------------------------------------------------------------------------------
 // flat multi-tensor Keras SGD over the master buffer: P, V fp32 updated from G; Pb = bf16(P)

@@ -1456,7 +1456,7 @@ __global__ __launch_bounds__(NT) void colsum_fin_k(const float* slab, int splits
 // version re-read the row for the max, the exponent sum and the output, and reduced each
 // by an 8-level LDS tree (17 barriers per row, 30 more in the last block): 9.8 us for the
 // ResNet-18 head (64 x 1000) -- the 1000-class logits of 64 rows.
-constexpr int SX_KPT = 4, SX_NW = NT / 64;
+constexpr int SX_KPT = 4, SX_NW = NT / 64, SX_BK = 1024;
 __device__ __forceinline__ void sx_better(float& v, int& i, float ov, int oi) {
   if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }  // max, ties -> smallest index
 }
@@ -1468,7 +1468,7 @@ __device__ __forceinline__ float sx_wave_sum(float v) {
 __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ logits, int ld,
                                                      const int32_t* __restrict__ labels, int K, float scale,
                                                      const Ctrl* __restrict__ ctrl, uint16_t* __restrict__ dl,
-                                                     float* tail, float* rows) {
+                                                     float* tail, float* rows, float* bias_grad) {
   __shared__ float wmax[SX_NW], wsum[SX_NW], wtail[3][SX_NW];
   __shared__ int widx[SX_NW];
   __shared__ int last;
@@ -1567,6 +1567,52 @@ __global__ __launch_bounds__(NT) void softmax_xent_k(const float* __restrict__ l
     tail[t] += v;
   }
   if (t == 0) *counter = 0;
+  if (bias_grad) {
+    // the logits layer's bias gradient from the stored dl rows (every block's, acquired by
+    // last_arriver), in colsum_k's one-split order: 4 row phases each summed in row order,
+    // then (p0 + p1) + (p2 + p3), added to the gradient -- the same bits as its launch.
+    // Work item = (phase, 8 columns): 16-byte loads of 8 rows in flight at a time, the
+    // phase sums meet in LDS (a thread per column walking the rows one load at a time took
+    // the launch from 7.5 to 66 us)
+    __shared__ float bph[4][SX_BK];
+    if (K <= SX_BK && ld % 8 == 0) {
+      const int ng = (K + 7) / 8;
+      for (int wi = t; wi < 4 * ng; wi += NT) {
+        const int q = wi / ng, g = wi - q * ng;
+        float s8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int m0 = q; m0 < B; m0 += 32) {
+          uint4 v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int m = m0 + 4 * u;
+            v[u] = m < B ? *reinterpret_cast<const uint4*>(dl + (size_t)m * ld + 8 * g) : uint4{0u, 0u, 0u, 0u};
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            if (m0 + 4 * u >= B) break;
+            const uint32_t w4[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              s8[2 * e] += __uint_as_float(w4[e] << 16);
+              s8[2 * e + 1] += __uint_as_float(w4[e] & 0xffff0000u);
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bph[q][8 * g + e] = s8[e];
+      }
+      __syncthreads();
+      for (int k = t; k < K; k += NT) bias_grad[k] += (bph[0][k] + bph[1][k]) + (bph[2][k] + bph[3][k]);
+    } else {
+      for (int k = t; k < K; k += NT) {
+        float ph[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          for (int m = q; m < B; m += 4) ph[q] += bf2f(dl[(size_t)m * ld + k]);
+        bias_grad[k] += (ph[0] + ph[1]) + (ph[2] + ph[3]);
+      }
+    }
+  }
 }
 
 // ---- inference (predict / evaluate through the native forward plan) ----------------------
@@ -2244,9 +2290,11 @@ hipError_t colsum(const void* x, int x_f32, int M, int N, int ld, float* out, fl
 }
 
 hipError_t softmax_xent(const float* logits, int ld, const int32_t* labels, int B, int K, float scale, const Ctrl* ctrl,
-                        uint16_t* dlogits, float* tail, float* rows, hipStream_t s) {
+                        uint16_t* dlogits, float* tail, float* rows, hipStream_t s, float* bias_grad) {
   if (!rows || B < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, ctrl, dlogits, tail, rows);
+  if (bias_grad && colsum_splits(B, K) != 1) return hipErrorInvalidValue;  // the fold keeps colsum's order
+  hipLaunchKernelGGL(softmax_xent_k, dim3(B), dim3(NT), 0, s, logits, ld, labels, K, scale, ctrl, dlogits, tail, rows,
+                     bias_grad);
   return hipGetLastError();
 }
 

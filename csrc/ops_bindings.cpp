@@ -331,12 +331,14 @@ void register_kernel_ops(py::module_& m) {
     check(damd::colsum(P_<const void>(x), x_f32, M, N, ld, P_<float>(out), P_<float>(ws), P_<ihipStream_t>(s)),
           "colsum");
   });
-  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U ctrl, U dl, U tail, U rows, U s) {
+  m.def("softmax_xent", [](U logits, int ld, U labels, int B, int K, float scale, U ctrl, U dl, U tail, U rows, U s,
+                           U bias_grad) {
     check(damd::softmax_xent(P_<const float>(logits), ld, P_<const int32_t>(labels), B, K, scale,
                              P_<const damd::Ctrl>(ctrl), P_<u16>(dl), P_<float>(tail), P_<float>(rows),
-                             P_<ihipStream_t>(s)),
+                             P_<ihipStream_t>(s), P_<float>(bias_grad)),
           "softmax_xent");
-  });
+  }, py::arg("logits"), py::arg("ld"), py::arg("labels"), py::arg("B"), py::arg("K"), py::arg("scale"),
+     py::arg("ctrl"), py::arg("dl"), py::arg("tail"), py::arg("rows"), py::arg("s"), py::arg("bias_grad") = 0);
   m.def("sgd_step", [](U P, U G, U V, U Pb, long n, U ctrl, U tail, U s) {
     check(damd::sgd_step(P_<float>(P), P_<const float>(G), P_<float>(V), P_<u16>(Pb), n, P_<damd::Ctrl>(ctrl),
                          P_<const float>(tail), P_<ihipStream_t>(s)),

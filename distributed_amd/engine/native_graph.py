@@ -965,8 +965,14 @@ class NativeGraphEngine(Engine):
                        pc_dims=list(job[2:]) if job else [])
         for nd in live:
             getattr(self, "_fwd_" + nd.kind)(nd)
+        last = self.nodes[-1]
+        # the logits layer's bias gradient comes out of the loss launch (no colsum launch;
+        # DAMD_XENT_BIAS=0: the colsum launch, the same bits)
+        fold = (last.kind == "Dense" and last.layer.use_bias and "dz" not in last.attrs
+                and H.softmax_bias_fold_ok(self.B, self.K) and env.get_bool("DAMD_XENT_BIAS", True))
+        last.attrs["bias_folded"] = fold
         H.softmax_xent(self.logits, self.labels, self.K, 1.0 / self.global_batch, self.dlogits, self.G[self.nparam:],
-                       ctrl=self.ctrl, rows=self.xent_rows)
+                       ctrl=self.ctrl, rows=self.xent_rows, bias_grad=self.gviews[id(last.layer.bias)] if fold else None)
         self._mark("forward")
         for t in self._all_tensors():
             t.root().written = False
@@ -1414,7 +1420,7 @@ class NativeGraphEngine(Engine):
             self._act_bwd(nd, dy, y.buf, nd.attrs["dz"])
             dy = nd.attrs["dz"]
         units = l.units
-        if l.use_bias:
+        if l.use_bias and not nd.attrs.get("bias_folded"):
             H.colsum(dy, self.gviews[id(l.bias)], workspace=self.gemm_ws, M=dy.shape[0], N=units, ld=dy.shape[1])
         if "dw_pad" in nd.attrs:
             dwp = nd.attrs["dw_pad"]

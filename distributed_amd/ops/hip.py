@@ -1026,15 +1026,26 @@ def xent_rows(B: int, device) -> torch.Tensor:
     return torch.zeros(3 * B + 1, dtype=torch.float32, device=device)
 
 
-def softmax_xent(logits, labels, K, scale, dlogits, tail, ctrl=None, rows=None):
+def softmax_xent(logits, labels, K, scale, dlogits, tail, ctrl=None, rows=None, bias_grad=None):
     """ctrl (the engine's device control block) makes the scale 1 / real rows of the global
     batch; labels < 0 mark padding rows of a short final batch.  The loss / correct / count
-    sums are formed in a fixed row order (``rows``: :func:`xent_rows` scratch)."""
+    sums are formed in a fixed row order (``rows``: :func:`xent_rows` scratch).
+    ``bias_grad`` (fp32 [K], optional; needs :func:`softmax_bias_fold_ok`): += the column
+    sums of dlogits, bitwise as :func:`colsum` would add them."""
     B, ld = logits.shape
     if rows is None:
         rows = xent_rows(B, logits.device)  # (eager callers only: engines pass their own)
+    if bias_grad is not None:
+        _chk(bias_grad, torch.float32, "bias_grad")
+        if bias_grad.numel() < K or not softmax_bias_fold_ok(B, K):
+            raise ValueError("softmax_xent: bias_grad needs >= K floats and a one-split colsum shape")
     _C().softmax_xent(_ptr(logits), ld, _ptr(labels), B, K, float(scale), _ptr(ctrl), _ptr(dlogits), _ptr(tail),
-                      _ptr(rows), stream_handle())
+                      _ptr(rows), stream_handle(), bias_grad=_ptr(bias_grad))
+
+
+def softmax_bias_fold_ok(B: int, K: int) -> bool:
+    """colsum of a [B][K] gradient runs as one split (the order softmax_xent reproduces)."""
+    return _C().colsum_splits(B, K) == 1
 
 
 def sgd_flat(P, G, V, Pb, lr, momentum=0.0, nesterov=False):

@@ -330,6 +330,15 @@ def test_softmax_xent_wide_rows(H, B, K, ld):
     tail2 = torch.zeros(3, device=dev)
     H.softmax_xent(z, lab, K, 1.0 / B, dl2, tail2)
     assert torch.equal(dl, dl2) and torch.equal(tail, tail2)
+    # the bias-gradient fold (vectorised path for ld % 8 == 0 and K <= 1024, else the
+    # per-column loop) adds exactly what colsum adds
+    if H.softmax_bias_fold_ok(B, K):
+        base = rnd(K, seed=32)
+        bg, bc = base.clone(), base.clone()
+        dl3 = torch.zeros_like(dl)
+        H.softmax_xent(z, lab, K, 1.0 / B, dl3, torch.zeros(3, device=dev), bias_grad=bg)
+        H.colsum(dl3, bc, M=B, N=K, ld=ld)
+        assert torch.equal(bg, bc)
 
 
 @pytest.mark.parametrize("n,hw,c,f32", [(64, 7, 512, True), (5, 7, 2048, False), (3, 2, 64, False), (2, 14, 8, True)])

@@ -552,6 +552,25 @@ def test_weight_gradients_on_side_stream_are_bitwise(monkeypatch, allreduce):
     assert hs == h1
 
 
+def test_logits_bias_gradient_from_the_loss_launch_is_bitwise(monkeypatch):
+    """The logits layer's bias gradient summed in the loss launch's last block (no colsum
+    launch, DAMD_XENT_BIAS=1, default) == the colsum launch (DAMD_XENT_BIAS=0), bitwise over
+    momentum steps with 1000 classes (the ResNet-18 head width) and with the stem's padded
+    weights refreshed in the gather launch."""
+    def build():
+        return resnet18(classes=1000, input_shape=(64, 64, 3), widths=(64, 64, 128, 128), blocks=(1, 1, 1, 1))
+
+    x, y = _data(64, (64, 64, 3), 1000, seed=12)
+    tf.keras.backend.clear_session()
+    init = build().get_weights()
+    wf, hf, ef = _train(build, x, y, init, 32, 3, native=True, momentum=0.9, extra_env={"DAMD_XENT_BIAS": "1"})
+    wc, hc, ec = _train(build, x, y, init, 32, 3, native=True, momentum=0.9, extra_env={"DAMD_XENT_BIAS": "0"})
+    assert ef == ec == "native_graph"
+    for a, b in zip(wf, wc):
+        np.testing.assert_array_equal(a, b)
+    assert hf == hc
+
+
 def test_resnet18_full_size_trains():
     x, y = _data(64, (224, 224, 3), 1000, seed=3)
     tf.keras.backend.clear_session()
