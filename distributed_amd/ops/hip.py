@@ -361,7 +361,7 @@ def splitk_fixup_on(stats) -> bool:
 # They are split over K into fp32 slabs (one k-step or two per workgroup) and finished by
 # a fixed-order reduction kernel with the bias / ReLU / accumulate epilogue.
 DENSE_SPLIT_MAX_TILES = 32
-DENSE_SPLIT_TARGET_WG = 128
+DENSE_SPLIT_TARGET_WG = int(os.environ.get("DAMD_DENSE_SPLIT_WG", "128"))  # 1: no split-K (A/B runs)
 
 
 def dense_split_plan(M: int, N: int, K: int) -> Tuple[int, int]:
